@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Benchmark of the rtMRI -> mel -> 11 413 Hz waveform hot path on MI355X (libm2s).
+
+Metric (BASELINE.json): rtMRI frames/s (and real-time factor) end to end, 256x256 frames.
+Workload per GPU (weak scaling): ``--clips`` synthetic clips x ``--frames`` frames (default
+64 x 30 = the per-GPU share of configs[3], 512 clips over 8 GPUs), CNN-BiLSTM + head + mel glue
++ HiFi-GAN generator, compute dtype ``--dtype`` (bf16 default, configs[1]).  One step = one pass
+of the whole path over the per-GPU batch with frames already resident in HBM, followed by the
+RCCL gather of wav + mel to rank 0 (N > 1).  Weights are random-init of the reference
+architecture (no checkpoints offline), broadcast from rank 0 over RCCL once, outside the timing.
+
+Launch: ``python bench.py`` (N=1) or
+``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N``.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "mri-to-speech_amd"))
+
+from m2s import synth  # noqa: E402
+from m2s.config import HIFIGAN_H  # noqa: E402
+
+HOP = 420
+SR = 11413
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA peaks, MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--clips", type=int, default=64, help="clips per GPU")
+    p.add_argument("--frames", type=int, default=30, help="frames per clip")
+    p.add_argument("--hw", type=int, default=256)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--chunk", type=int, default=256, help="frames per CNN pass")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-profile", action="store_true")
+    return p.parse_args()
+
+
+def init_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def flat_state(sd):
+    keys = [k for k in sd if sd[k].dtype == np.float32]
+    sizes = [sd[k].size for k in keys]
+    return keys, sizes
+
+
+def broadcast_state(sd, device, world):
+    """C1: rank 0's weights to every rank over RCCL (one flat fp32 buffer)."""
+    keys, sizes = flat_state(sd)
+    if world == 1:
+        return sd
+    flat = torch.from_numpy(np.concatenate([sd[k].ravel() for k in keys])).to(device)
+    dist.broadcast(flat, 0)
+    host = flat.cpu().numpy()
+    out, off = {}, 0
+    for k, n in zip(keys, sizes):
+        out[k] = host[off:off + n].reshape(sd[k].shape)
+        off += n
+    for k in sd:
+        if k not in out:
+            out[k] = sd[k]
+    return out
+
+
+def make_frames(clips, frames, hw, rank, device):
+    g = torch.Generator(device=device)
+    g.manual_seed(1234 + rank)
+    x = torch.rand(clips, frames, hw, hw, generator=g, device=device, dtype=torch.float32)
+    lo = x.amin(dim=(2, 3), keepdim=True)
+    hi = x.amax(dim=(2, 3), keepdim=True)
+    return ((x - lo) / (hi - lo)).contiguous()
+
+
+def cpu_baseline(args, ac_sd, gen_sd, mean, std):
+    """Oracle (torch-CPU fp32 restatement of the reference graph) on this host's cores."""
+    sys.path.insert(0, REPO)
+    from oracle import acoustic, effnet, hifigan
+
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    sd = {k: torch.from_numpy(v) for k, v in ac_sd.items()}
+    gsd = {k: torch.from_numpy(v) for k, v in gen_sd.items()}
+    T = args.frames
+    frames = torch.from_numpy(synth.synth_frames(1, T, hw=(args.hw, args.hw), seed=77))
+    done, t0 = 0, time.perf_counter()
+    with torch.no_grad():
+        while True:
+            f = effnet.effnet_gap(sd, frames.reshape(T, args.hw, args.hw)).view(1, T, -1)
+            mn = acoustic.head(sd, acoustic.bilstm_summerge(sd, f))
+            ln = acoustic.mel_db_to_log(acoustic.denormalize_mel(mn[0], mean, std))
+            hifigan.generator(gsd, HIFIGAN_H, ln.t().unsqueeze(0))
+            done += 1
+            el = time.perf_counter() - t0
+            if el >= args.cpu_seconds or done >= 50:
+                break
+    return {"value": round(done * T / el, 3), "unit": "rtMRI frames/s", "cores": cores, "kind": "port",
+            "sample": f"{done} clip(s) x {T} frames at {args.hw}x{args.hw}, end to end (CNN-BiLSTM + glue + "
+                      f"HiFi-GAN), fp32 oracle (torch-CPU restatement of the reference graph), {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    world, rank, local = init_dist(args)
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    from m2s import _native, runtime
+
+    # weights: rank 0 generates, RCCL broadcast (C1), every rank packs its own copy
+    ac_sd = synth.synth_acoustic_state(0) if rank == 0 else synth.synth_acoustic_state(0)
+    gen_sd = synth.synth_generator_state(0)
+    ac_sd_b = broadcast_state(ac_sd, device, world)
+    gen_sd_b = broadcast_state(gen_sd, device, world)
+    mean, std = synth.synth_scaler()
+    ac = runtime.AcousticEngine(ac_sd_b, dtype=args.dtype, device=device, chunk=args.chunk)
+    voc = runtime.VocoderEngine(gen_sd_b, HIFIGAN_H, dtype=args.dtype, device=device)
+    pipe = runtime.Pipeline(ac, voc, mean, std)
+
+    B, T, HW = args.clips, args.frames, args.hw
+    frames = make_frames(B, T, HW, rank, device)
+    out = {"wav": torch.empty(B, T * HOP, device=device), "mel_db": torch.empty(B, T, 64, device=device),
+           "mel_log": torch.empty(B, T, 64, device=device)}
+    if world > 1:  # C3: clip lengths of every rank (uniform here; the driver sizes the gather with it)
+        lens = torch.full((B,), T, dtype=torch.int64, device=device)
+        all_lens = [torch.empty_like(lens) for _ in range(world)]
+        dist.all_gather(all_lens, lens)
+        gather_wav = [torch.empty_like(out["wav"]) for _ in range(world)] if rank == 0 else None
+        gather_mel = [torch.empty_like(out["mel_db"]) for _ in range(world)] if rank == 0 else None
+
+    def step():
+        pipe.forward(frames, out=out)
+        if world > 1:  # C2: results to rank 0 over RCCL
+            dist.gather(out["wav"], gather_wav, dst=0)
+            dist.gather(out["mel_db"], gather_mel, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+
+    def timed(k):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            step()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item())
+
+    elapsed = timed(args.steps)
+    frames_total = world * B * T * args.steps
+    fps = frames_total / elapsed
+    audio_s = frames_total * HOP / SR
+    result = {
+        "metric": "rtMRI frames/s end-to-end (256x256 frames -> 64-bin mel -> 11413 Hz wav)",
+        "value": round(fps, 2),
+        "unit": "rtMRI frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (seeded U[0,1) frames, per-frame min-max; random-init weights of the reference architecture)",
+        "rtf": round(elapsed / audio_s, 6),
+        "config": {"workload": f"e2e rtMRI->wav, {B} clips x {T} frames per GPU at {HW}x{HW} (configs[3] per-GPU share)",
+                   "clips_per_gpu": B, "frames_per_clip": T, "global_batch_clips": B * world, "hw": HW,
+                   "parallelism": f"dp{world}", "chunk": args.chunk},
+    }
+
+    # roofline: a second pass identical to the timed region with HIP events around every launch
+    if not args.no_profile:
+        _native.prof_enable(True)
+        timed(args.steps)
+        _native.prof_enable(False)
+        stats = _native.prof_collect()
+        tot_ms = sum(s["ms"] for s in stats)
+        dom = max(stats, key=lambda s: s["ms"])
+        mfma = dom["name"].startswith("conv_igemm")
+        if mfma:
+            achieved = dom["flops"] / (dom["ms"] * 1e-3) / 1e12
+            peak = PEAK_TFLOPS["bf16" if "bf16" in dom["name"] else "fp32"]
+            unit, bound = "TFLOP/s", "mfma"
+        else:
+            achieved = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9
+            peak, unit, bound = PEAK_HBM_GBS, "GB/s", "hbm"
+        conv_ms = sum(s["ms"] for s in stats if s["name"].startswith("conv_igemm"))
+        conv_fl = sum(s["flops"] for s in stats if s["name"].startswith("conv_igemm"))
+        result["roofline"] = {
+            "bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
+            "frac": round(achieved / peak, 4), "traffic": None,
+            "kernel": dom["name"], "launches_per_step": dom["launches"] // args.steps,
+            "avg_launch_us": round(1000.0 * dom["ms"] / dom["launches"], 2),
+            "kernel_share_of_gpu_time": round(dom["ms"] / tot_ms, 3),
+            "all_conv_igemm_tflops": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2),
+        }
+        if rank == 0 and os.environ.get("M2S_BENCH_KERNELS"):
+            for s in sorted(stats, key=lambda s: -s["ms"]):
+                print(f"# {s['name']:40s} n={s['launches']:6d} ms={s['ms']:9.3f} "
+                      f"TF/s={s['flops'] / max(s['ms'], 1e-9) / 1e9:8.2f} GB/s={s['bytes'] / max(s['ms'], 1e-9) / 1e6:8.1f}",
+                      file=sys.stderr)
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args, ac_sd, gen_sd, mean, std)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

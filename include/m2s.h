@@ -1,0 +1,139 @@
+/*
+ * m2s.h - C ABI of libm2s, the MI355X (gfx950) implementation of the rtMRI video -> mel ->
+ * waveform inference hot path of YamaneKoyo/mri-to-speech.
+ *
+ * Plain pointers and sizes only.  Every device pointer is a HIP device allocation on the
+ * object's device; `stream` is a hipStream_t (NULL = default stream).  Every call is
+ * asynchronous on `stream` unless stated otherwise.  Functions return M2S_OK or an error
+ * code; m2s_last_error() gives a thread-local message.  Nothing here falls back to the CPU:
+ * without a gfx950 device the create calls fail with M2S_E_NODEV.
+ *
+ * Reference interfaces replaced (paths inside the reference repository):
+ *   m2s_acoustic_*      OTNLikeCNNBiLSTM built by build_acoustic_model(**kw) and loaded with
+ *                       load_state_dict(strict=False)   mri2speech_code/mri_acoustic_model.py:74-156,
+ *                       scripts/run_mri_video_inference.py:119-148
+ *   m2s_acoustic_forward   OTNLikeCNNBiLSTM.forward (eval)   mri_acoustic_model.py:116-136
+ *   m2s_effnet_forward     EffNetV2B2Backbone.forward + GlobalAvgPool   mri_acoustic_model.py:15-18,39-48
+ *   m2s_bilstm_summerge    BiLSTMSumMerge.forward + head Linear   mri_acoustic_model.py:67-72,135
+ *   m2s_mel_glue           denormalize_mel + dB -> ln-power   run_mri_video_inference.py:160-163,227-233
+ *   m2s_vocoder_*          Generator(h) + load_state_dict(ckpt['generator']) + weight-norm removal
+ *                          models.py:88-109, run_mri_video_inference.py:89-116
+ *   m2s_vocoder_forward    Generator.forward   models.py:113-131
+ *   m2s_pipeline_forward   the no_grad section of main()   run_mri_video_inference.py:222-242
+ */
+#ifndef M2S_H_
+#define M2S_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define M2S_ABI_VERSION 1
+
+enum m2s_status { M2S_OK = 0, M2S_E_ARG = 1, M2S_E_HIP = 2, M2S_E_STATE = 3, M2S_E_NODEV = 4, M2S_E_INTERNAL = 5 };
+/* compute dtype of the convolution stacks (BiLSTM, head and glue always run in fp32) */
+enum m2s_dtype { M2S_DT_F32 = 0, M2S_DT_BF16 = 1 };
+/* host tensor element types */
+enum m2s_elem { M2S_ELEM_F32 = 0, M2S_ELEM_I64 = 1 };
+
+int m2s_abi_version(void);
+const char* m2s_last_error(void);
+/* M2S_OK if HIP device `device` exists and is gfx950 (synchronous). */
+int m2s_device_check(int device);
+
+/* One state-dict entry, reference key name, contiguous row-major HOST memory. */
+typedef struct m2s_tensor {
+  const char* name;
+  const void* data;
+  int elem; /* m2s_elem */
+  int ndim;
+  int64_t shape[4];
+} m2s_tensor;
+
+/* ------------------------------------------------------------------ acoustic model ---- */
+typedef struct m2s_acoustic m2s_acoustic;
+
+/* Packs a reference-format state dict (keys of OTNLikeCNNBiLSTM.state_dict(): cnn.backbone.*,
+ * rnn.lstm.*, head.*) for `device`: BatchNorm folded, grey->RGB repeat folded into conv_stem,
+ * layouts converted.  Unknown keys are ignored (strict=False); a missing required key is
+ * M2S_E_ARG naming the key.  Synchronous. */
+int m2s_acoustic_create(const m2s_tensor* sd, int n, int n_mels, int rnn_hidden, int dtype, int device,
+                        m2s_acoustic** out);
+void m2s_acoustic_destroy(m2s_acoustic* m);
+/* frames per CNN pass (bounds the CNN workspace); default 256 */
+int m2s_acoustic_set_chunk(m2s_acoustic* m, int frames);
+size_t m2s_acoustic_workspace_bytes(const m2s_acoustic* m, int B, int T, int H, int W);
+/* frames (B,T,H,W) fp32 in [0,1] -> mel_norm (B,T,n_mels) fp32. */
+int m2s_acoustic_forward(m2s_acoustic* m, const float* frames, int B, int T, int H, int W, float* mel_norm,
+                         void* ws, size_t ws_bytes, void* stream);
+/* frames (N,H,W) -> feats (N,208) fp32 (GAP of the last timm feature map). */
+int m2s_effnet_forward(m2s_acoustic* m, const float* frames, int N, int H, int W, float* feats, void* ws,
+                       size_t ws_bytes, void* stream);
+/* Debug tap: feature map after `n_blocks` timm blocks (0 = after conv_stem/bn1), written as
+ * (N,OH,OW,C) fp32 dense to `out`; returns OH, OW, C through the pointers. */
+int m2s_effnet_probe(m2s_acoustic* m, const float* frames, int N, int H, int W, int n_blocks, float* out,
+                     int* oh, int* ow, int* oc, void* ws, size_t ws_bytes, void* stream);
+/* feats (B,T,208) -> y (B,T,rnn_hidden) sum-merged BiLSTM output (may be NULL) and
+ * mel_norm (B,T,n_mels) head output (may be NULL). */
+int m2s_bilstm_summerge(m2s_acoustic* m, const float* feats, int B, int T, float* y, float* mel_norm, void* ws,
+                        size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------- mel glue ---- */
+/* mel_db = x*std + mean; mel_log = ln(clamp(10^(mel_db/10), 1e-5)); x (rows,n_mels).
+ * mean/std are DEVICE fp32 arrays of n_mels; either output may be NULL. */
+int m2s_mel_glue(const float* mel_norm, int rows, int n_mels, const float* mean, const float* std, float* mel_db,
+                 float* mel_log, void* stream);
+
+/* ----------------------------------------------------------------------- vocoder ---- */
+typedef struct m2s_hifigan_h {
+  int resblock; /* 1 or 2 (h.resblock "1"/"2") */
+  int num_mels;
+  int upsample_initial_channel;
+  int n_up;
+  int upsample_rates[8];
+  int upsample_kernel_sizes[8];
+  int n_kernels;
+  int resblock_kernel_sizes[8];
+  int n_dilations[8];
+  int resblock_dilation_sizes[8][8];
+} m2s_hifigan_h;
+
+typedef struct m2s_vocoder m2s_vocoder;
+/* Packs a Generator state dict (weight_g/weight_v or plain weight after remove_weight_norm).
+ * Strict like load_state_dict(ckpt['generator']): a missing key is M2S_E_ARG.  Synchronous. */
+int m2s_vocoder_create(const m2s_tensor* sd, int n, const m2s_hifigan_h* h, int dtype, int device, m2s_vocoder** out);
+void m2s_vocoder_destroy(m2s_vocoder* v);
+size_t m2s_vocoder_workspace_bytes(const m2s_vocoder* v, int B, int T);
+/* mel fp32, layout 0 = (B,num_mels,T) as Generator.forward takes it, 1 = (B,T,num_mels);
+ * wav (B, T*prod(upsample_rates)) fp32. */
+int m2s_vocoder_forward(m2s_vocoder* v, const float* mel, int mel_layout, int B, int T, float* wav, void* ws,
+                        size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------- end to end ---- */
+size_t m2s_pipeline_workspace_bytes(const m2s_acoustic* m, const m2s_vocoder* v, int B, int T, int H, int W);
+/* frames (B,T,H,W) -> mel_norm, mel_db, mel_log (B,T,n_mels) and wav (B,T*hop).  mel_* may be NULL. */
+int m2s_pipeline_forward(m2s_acoustic* m, m2s_vocoder* v, const float* frames, int B, int T, int H, int W,
+                         const float* mean, const float* std, float* mel_norm, float* mel_db, float* mel_log,
+                         float* wav, void* ws, size_t ws_bytes, void* stream);
+
+/* -------------------------------------------------------------------- profiling ---- */
+/* While enabled, every kernel launch is bracketed by HIP events on its own stream. */
+typedef struct m2s_prof_stat {
+  char name[96];     /* kernel symbol family, e.g. "conv_igemm<bf16,conv2d,2x4>" */
+  int64_t launches;
+  double ms;         /* summed event time */
+  double flops;      /* summed algorithmic FLOPs */
+  double bytes;      /* summed algorithmic HBM bytes (compulsory in + out + weights) */
+} m2s_prof_stat;
+int m2s_prof_enable(int on);
+/* Synchronises on the recorded events, writes up to `max` stats, clears the record. */
+int m2s_prof_collect(m2s_prof_stat* out, int max, int* n_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* M2S_H_ */

@@ -1,0 +1,63 @@
+// Implicit-GEMM convolution on MFMA (the workhorse of both the CNN encoder and the vocoder).
+//
+// One kernel family covers every dense conv of the hot path, channel-last layouts:
+//   KIND_CONV2D : NHWC 2-D conv, square kernel ks, stride, TF-SAME pads (pad_t, pad_l)
+//                 (timm conv_stem/conv/conv_exp/conv_pw/conv_pwl, mri_acoustic_model.py:28-34)
+//   KIND_CONV1D : NLC 1-D conv, taps ks, dilation, left pad (causal MRF convs, conv_pre;
+//                 models.py:11-49,94,114-115)
+//   KIND_CONVT  : one output phase r of a ConvTranspose1d (stride u) as a 1-D conv over the
+//                 input with reversed taps (models.py:98-101,117-118); grid.z = phase
+//   KIND_GEMM   : plain row GEMM (1x1 conv at stride 1, LSTM input projection)
+//
+// GEMM view: D[n][m] = sum_k W[n][k] * X[m][k], n = output channel, m = output position,
+// k = (tap, input channel).  The MFMA A operand is the weight tile, B is the activation
+// tile, so each lane ends up holding 4 consecutive output channels of ONE position and
+// the epilogue stores 8/16 contiguous bytes (channel-last) per lane.
+#pragma once
+
+#include "m2s_common.hpp"
+
+namespace m2s {
+
+enum ConvKind { KIND_CONV2D = 0, KIND_CONV1D = 1, KIND_CONVT = 2, KIND_GEMM = 3 };
+enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_LRELU = 2 };
+enum InXform { IN_NONE = 0, IN_LRELU = 1, IN_SE_SCALE = 2 };
+
+struct ConvArgs {
+  const void* x;        // input activations, channel-last, channel stride cs_in
+  const void* w;        // packed weights [phase][n_pad][kp]  (T)
+  const float* bias;    // [n_pad] fp32 (zero padded)
+  const void* res;      // residual, same layout as y (or null)
+  void* y;              // output, channel-last, channel stride cs_out
+  const float* in_scale;// IN_SE_SCALE: [img][cs_in] fp32
+  int kind;
+  int M;                // GEMM rows (output positions per phase)
+  int cs_in, cs_out;    // channel strides
+  int n_pad;            // weight rows per phase (>= grid.y * N tile)
+  int kp;               // weight row length
+  int ntaps;            // taps (ks*ks for 2-D)
+  int tpc;              // taps per K chunk (KC / cs_in if cs_in < KC else 1)
+  // 2-D
+  int IH, IW, OH, OW, ks, stride, pad_t, pad_l;
+  // 1-D / transposed
+  int L_in, L_out, dil, pad_left;
+  int ct_u, ct_pad, ct_k;  // transposed conv: stride, padding, kernel size
+  // epilogue
+  int act; float act_slope;
+  int in_xform; float in_slope;
+  int accum;            // 0: y = v ; 1: y = y_prev + v ; 2: y = (y_prev + v) / accum_div
+  float accum_div;
+};
+
+// flops / bytes: algorithmic work of this launch, recorded by the profiler (m2s_prof_*).
+template <typename T>
+void launch_conv(const ConvArgs& a, hipStream_t s, double flops = 0.0, double bytes = 0.0);
+
+// Host-side helpers shared by the packers.
+inline int conv_tpc(int cs_in, int kc) { return cs_in < kc ? kc / cs_in : 1; }
+inline int conv_kp(int ntaps, int cs_in, int kc) {
+  int tpc = conv_tpc(cs_in, kc);
+  return round_up(ntaps, tpc) * cs_in;
+}
+
+}  // namespace m2s

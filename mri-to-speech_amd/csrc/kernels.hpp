@@ -1,0 +1,62 @@
+// Launchers for the non-GEMM kernels of the hot path.
+#pragma once
+
+#include "m2s_common.hpp"
+
+namespace m2s {
+
+// conv_stem (3x3 s2 TF-SAME, grey repeat folded: w[o][9]) + bn1 + SiLU.  frames fp32 (N,H,W)
+// -> y (N,OH,OW,cs_out) T.  timm conv_stem/bn1, mri_acoustic_model.py:41-46.
+template <typename T>
+void launch_stem(const float* frames, int N, int H, int W, int OH, int OW, int pad_t, int pad_l,
+                 const float* w9, const float* bias, int cout, int cs_out, T* y, hipStream_t s);
+
+// conv_dw (3x3 depthwise, stride 1/2, TF-SAME) + bn2 + SiLU, plus per-(image, row group, channel)
+// partial sums of the output (SE squeeze).  x (N,IH,IW,cs) -> y (N,OH,OW,cs),
+// sums (N, dw_row_groups(OH), cs) fp32.
+inline int dw_row_groups(int OH) { return (OH + 3) / 4; }
+template <typename T>
+void launch_dwconv(const T* x, int N, int IH, int IW, int OH, int OW, int stride, int pad_t, int pad_l,
+                   int C, int cs, const float* w9, const float* bias, T* y, float* sums, hipStream_t s);
+
+// SE excitation: mean -> conv_reduce -> SiLU -> conv_expand -> sigmoid.  sums (N,cs) -> scale (N,cs).
+// w1 = conv_reduce [rd][C], w2 = conv_expand TRANSPOSED [rd][C].
+void launch_se_fc(const float* sums, int nrg, int N, int C, int cs, int rd, float inv_count, const float* w1,
+                  const float* b1, const float* w2, const float* b2, float* scale, bool exact, hipStream_t s);
+
+// Global average pool: x (N,P,cs) T -> feats (N,C) fp32 (dense, row stride C).
+template <typename T>
+void launch_gap(const T* x, int N, int P, int C, int cs, float* feats, hipStream_t s);
+
+// One BiLSTM time step for both directions (step s: fwd t = s, bwd t = T-1-s).
+// pre (B,T,8H) fp32 = x W_ih^T + b_ih + b_hh for [fwd | bwd]; whh (2,4H,H); hs (2,B,T,H); cst (2,B,H).
+void launch_lstm_step(const float* pre, const float* whh, float* hs, float* cst, int B, int T, int H,
+                      int step, hipStream_t s);
+
+// head: y = hs[0] + hs[1] (sum merge); out = y W^T + b.  wt (H, n_mels) transposed weight.
+void launch_mel_head(const float* hs, int rows, int H, const float* wt, const float* b, int n_mels,
+                     float* out, hipStream_t s);
+
+// mel glue: db = x*std + mean; ln = log(clamp(10^(db/10), 1e-5)).  Any output may be null.
+// ln_t (rows, cs) T channel-last copy feeds the vocoder.
+template <typename T>
+void launch_mel_glue(const float* x, int rows, int n_mels, const float* mean, const float* std_,
+                     float* db, float* ln, T* ln_t, int cs, hipStream_t s);
+
+// mel (B,C,T) fp32 [layout 0] or (B,T,C) fp32 [layout 1] -> (B,T,cs) T.
+template <typename T>
+void launch_mel_to_nlc(const float* mel, int B, int C, int Tn, int layout, T* y, int cs, hipStream_t s);
+
+// conv_post: leaky_relu(0.01) -> right pad 6 -> Conv1d(C,1,7) -> tanh.  x (B,L,cs) T -> wav (B,L) fp32.
+template <typename T>
+void launch_conv_post(const T* x, int B, int L, int C, int cs, const float* w /*[7][C]*/, float bias,
+                      float* wav, hipStream_t s);
+
+// y = a + b (fp32, n elements)
+void launch_add2(const float* a, const float* b, float* y, long n, hipStream_t s);
+
+// (rows, cs) T -> (rows, C) fp32 dense (debug taps)
+template <typename T>
+void launch_unpad(const T* x, long rows, int C, int cs, float* y, hipStream_t s);
+
+}  // namespace m2s

@@ -1,0 +1,756 @@
+// Weight packing and execution plans for the acoustic model (CNN + BiLSTM + head) and the
+// HiFi-GAN generator.  Packing mirrors what the reference does at load time and folds what is
+// constant at inference:
+//   * BatchNorm (eps 1e-3, torch's alpha = w / sqrt(var + eps), beta = b - mean * alpha) into
+//     the preceding conv (timm BatchNormAct2d);
+//   * the grey -> RGB repeat (mri_acoustic_model.py:43-44) into conv_stem (sum over in-channels);
+//   * weight norm w = g * v / ||v|| (models.py:94-108; run_mri_video_inference.py:99-115);
+//   * LSTM b_ih + b_hh.
+#include "model.hpp"
+
+#include <cmath>
+#include <cstring>
+
+#include "prof.hpp"
+
+namespace m2s {
+
+// ------------------------------------------------------------------------------------------
+StateDict make_state_dict(const m2s_tensor* t, int n) {
+  StateDict sd;
+  for (int i = 0; i < n; ++i) {
+    M2S_CHECK(t[i].name != nullptr, "state dict entry without a name");
+    if (t[i].elem != M2S_ELEM_F32) continue;  // num_batches_tracked etc.
+    M2S_CHECK(t[i].ndim >= 0 && t[i].ndim <= 4, std::string("bad ndim for ") + t[i].name);
+    HostTensor h;
+    h.data = static_cast<const float*>(t[i].data);
+    for (int d = 0; d < t[i].ndim; ++d) h.shape.push_back(t[i].shape[d]);
+    sd[t[i].name] = h;
+  }
+  return sd;
+}
+
+static const HostTensor& need(const StateDict& sd, const std::string& k, std::vector<int64_t> shape) {
+  auto it = sd.find(k);
+  if (it == sd.end()) throw Error(M2S_E_ARG, "missing state-dict key: " + k);
+  if (it->second.shape != shape) {
+    std::string got, want;
+    for (auto d : it->second.shape) got += std::to_string(d) + ",";
+    for (auto d : shape) want += std::to_string(d) + ",";
+    throw Error(M2S_E_ARG, "shape mismatch for " + k + ": got (" + got + ") want (" + want + ")");
+  }
+  return it->second;
+}
+
+size_t Arena::add(const void* p, size_t bytes) {
+  size_t off = (host_.size() + 255) & ~size_t(255);
+  host_.resize(off + bytes);
+  if (bytes) std::memcpy(host_.data() + off, p, bytes);
+  return off;
+}
+
+void Arena::upload(int device) {
+  M2S_HIP(hipSetDevice(device));
+  M2S_HIP(hipMalloc(&dev_, host_.size() + 256));
+  M2S_HIP(hipMemcpy(dev_, host_.data(), host_.size(), hipMemcpyHostToDevice));
+  std::vector<uint8_t>().swap(host_);
+}
+
+Arena::~Arena() {
+  if (dev_) (void)hipFree(dev_);
+}
+
+static uint16_t f2bf_host(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+static int kc_of(int dtype) { return dtype == M2S_DT_BF16 ? Elem<bf16_t>::KC : Elem<float>::KC; }
+
+static PConv make_pconv(int kind, int cin, int cout, int ntaps, int dtype) {
+  PConv p;
+  p.kind = kind;
+  p.cin = cin;
+  p.cout = cout;
+  p.cs_in = chan_stride(cin);
+  p.cs_out = chan_stride(cout);
+  p.ntaps = ntaps;
+  const int kc = kc_of(dtype);
+  p.tpc = conv_tpc(p.cs_in, kc);
+  p.kp = conv_kp(ntaps, p.cs_in, kc);
+  p.n_pad = round_up(p.cs_out, 64);
+  return p;
+}
+
+// get(phase, n, tap, c) for n < cout, tap < ntaps, c < cin; bias(n)
+template <class Get, class Bias>
+static void pack_conv(Arena& ar, int dtype, PConv& p, Get get, Bias bias) {
+  std::vector<float> w((size_t)p.phases * p.n_pad * p.kp, 0.f);
+  for (int ph = 0; ph < p.phases; ++ph)
+    for (int n = 0; n < p.cout; ++n)
+      for (int t = 0; t < p.ntaps; ++t)
+        for (int c = 0; c < p.cin; ++c)
+          w[((size_t)ph * p.n_pad + n) * p.kp + (size_t)t * p.cs_in + c] = get(ph, n, t, c);
+  if (dtype == M2S_DT_BF16) {
+    std::vector<uint16_t> h(w.size());
+    for (size_t i = 0; i < w.size(); ++i) h[i] = f2bf_host(w[i]);
+    p.w_off = ar.add_vec(h);
+  } else {
+    p.w_off = ar.add_vec(w);
+  }
+  std::vector<float> b(p.n_pad, 0.f);
+  for (int n = 0; n < p.cout; ++n) b[n] = bias(n);
+  p.b_off = ar.add_vec(b);
+}
+
+static ConvArgs conv_args(const PConv& p) {
+  ConvArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.w = p.w;
+  a.bias = p.b;
+  a.kind = p.kind;
+  a.cs_in = p.cs_in;
+  a.cs_out = p.cs_out;
+  a.n_pad = p.n_pad;
+  a.kp = p.kp;
+  a.ntaps = p.ntaps;
+  a.tpc = p.tpc;
+  a.ks = p.ks;
+  a.stride = p.stride;
+  a.dil = p.dil;
+  a.pad_left = p.pad_left;
+  a.ct_u = p.ct_u;
+  a.ct_pad = p.ct_pad;
+  a.ct_k = p.ct_k;
+  a.OH = 1;
+  a.accum_div = 1.f;
+  return a;
+}
+
+template <typename T>
+static void run_conv(const ConvArgs& a, const PConv& p, hipStream_t s) {
+  const double rows = (double)a.M;
+  const double flops = 2.0 * p.macs_per_row * rows;
+  const double es = sizeof(T);
+  // compulsory traffic: input once, output once (+ residual/accum read), weights once
+  double in_rows = p.kind == KIND_CONV2D ? (double)a.IH * a.IW * (a.M / ((double)a.OH * a.OW))
+                                         : (p.kind == KIND_GEMM ? rows : 0.0);
+  if (p.kind == KIND_CONV1D || p.kind == KIND_CONVT) in_rows = (double)a.L_in * (a.M / (double)(p.kind == KIND_CONV1D ? a.L_out : a.L_in));
+  const double out_rows = rows * (p.kind == KIND_CONVT ? p.ct_u : 1);
+  const double bytes = es * (in_rows * p.cin + out_rows * p.cout * (1 + (a.res ? 1 : 0) + (a.accum ? 1 : 0)) +
+                             (double)p.phases * p.cout * p.ntaps * p.cin);
+  launch_conv<T>(a, s, flops, bytes);
+}
+
+// TF "SAME": out = ceil(in / s), total pad = max((out - 1) * s + k - in, 0), top/left = total / 2
+static void same_pad(int in, int k, int s, int* out, int* pad) {
+  *out = (in + s - 1) / s;
+  if (s == 1) {
+    *pad = (k - 1) / 2;  // timm static padding for odd k, stride 1
+  } else {
+    int total = std::max((*out - 1) * s + k - in, 0);
+    *pad = total / 2;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Acoustic model
+static const int EFF_STEM = 32, EFF_OUT = 208;
+struct StageDef {
+  int type, reps, k, stride, exp, cout;
+  float se;
+};
+static const StageDef kStages[6] = {{0, 2, 3, 1, 1, 16, 0.f},   {1, 3, 3, 2, 4, 32, 0.f},
+                                    {1, 3, 3, 2, 4, 56, 0.f},   {2, 4, 3, 2, 4, 104, 0.25f},
+                                    {2, 6, 3, 1, 6, 120, 0.25f}, {2, 10, 3, 2, 6, 208, 0.25f}};
+static int make_divisible(double v, int d = 8) { return std::max(d, (int)(v + d / 2.0) / d * d); }
+
+struct BN {
+  std::vector<float> a, b;
+};
+static BN fold_bn(const StateDict& sd, const std::string& p, int c) {
+  const float* w = need(sd, p + ".weight", {c}).data;
+  const float* bb = need(sd, p + ".bias", {c}).data;
+  const float* m = need(sd, p + ".running_mean", {c}).data;
+  const float* v = need(sd, p + ".running_var", {c}).data;
+  BN r;
+  r.a.resize(c);
+  r.b.resize(c);
+  for (int i = 0; i < c; ++i) {
+    const float invstd = 1.0f / std::sqrt(v[i] + 1e-3f);
+    r.a[i] = invstd * w[i];
+    r.b[i] = bb[i] - m[i] * r.a[i];
+  }
+  return r;
+}
+
+Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int device)
+    : dtype_(dtype), device_(device), n_mels_(n_mels), hidden_(hidden) {
+  M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16, "bad dtype");
+  M2S_CHECK(n_mels > 0 && hidden > 0 && hidden % 8 == 0, "bad n_mels / rnn_hidden");
+  const std::string P = "cnn.backbone.";
+  {  // stem: fold repeat(1,3,1,1) by summing the 3 input channels; then BN
+    const float* w = need(sd, P + "conv_stem.weight", {EFF_STEM, 3, 3, 3}).data;
+    BN bn = fold_bn(sd, P + "bn1", EFF_STEM);
+    std::vector<float> w9(EFF_STEM * 9);
+    for (int o = 0; o < EFF_STEM; ++o)
+      for (int t = 0; t < 9; ++t)
+        w9[o * 9 + t] = (w[(o * 3 + 0) * 9 + t] + w[(o * 3 + 1) * 9 + t] + w[(o * 3 + 2) * 9 + t]) * bn.a[o];
+    stem_w_ = arena_.add_vec(w9);
+    stem_b_ = arena_.add_vec(bn.b);
+  }
+  int cin = EFF_STEM;
+  for (int s = 0; s < 6; ++s) {
+    const StageDef& sdf = kStages[s];
+    for (int r = 0; r < sdf.reps; ++r) {
+      Block b;
+      b.type = sdf.type;
+      b.stride = r == 0 ? sdf.stride : 1;
+      b.cin = cin;
+      b.cout = sdf.cout;
+      b.skip = b.stride == 1 && cin == sdf.cout;
+      const std::string q = P + "blocks." + std::to_string(s) + "." + std::to_string(r) + ".";
+      const int k = sdf.k;
+      auto conv2d_kxk = [&](PConv& pc, const std::string& wk, int ci, int co, const BN& bn) {
+        const float* w = need(sd, wk, {co, ci, k, k}).data;
+        pc = make_pconv(KIND_CONV2D, ci, co, k * k, dtype);
+        pc.ks = k;
+        pc.stride = b.stride;
+        pc.macs_per_row = (double)co * ci * k * k;
+        pack_conv(arena_, dtype, pc, [&](int, int n, int t, int c) { return w[((size_t)n * ci + c) * k * k + t] * bn.a[n]; },
+                  [&](int n) { return bn.b[n]; });
+      };
+      auto conv1x1 = [&](PConv& pc, const std::string& wk, int ci, int co, const BN& bn) {
+        const float* w = need(sd, wk, {co, ci, 1, 1}).data;
+        pc = make_pconv(KIND_GEMM, ci, co, 1, dtype);
+        pc.macs_per_row = (double)co * ci;
+        pack_conv(arena_, dtype, pc, [&](int, int n, int, int c) { return w[(size_t)n * ci + c] * bn.a[n]; },
+                  [&](int n) { return bn.b[n]; });
+      };
+      if (b.type == 0) {
+        conv2d_kxk(b.c1, q + "conv.weight", cin, b.cout, fold_bn(sd, q + "bn1", b.cout));
+      } else if (b.type == 1) {
+        b.mid = make_divisible(cin * (double)sdf.exp);
+        conv2d_kxk(b.c1, q + "conv_exp.weight", cin, b.mid, fold_bn(sd, q + "bn1", b.mid));
+        conv1x1(b.c2, q + "conv_pwl.weight", b.mid, b.cout, fold_bn(sd, q + "bn2", b.cout));
+      } else {
+        b.mid = make_divisible(cin * (double)sdf.exp);
+        b.rd = (int)std::lround(b.mid * (sdf.se / sdf.exp));
+        const int m = b.mid, cs = chan_stride(m);
+        max_mid_cs_ = std::max(max_mid_cs_, cs);
+        conv1x1(b.c1, q + "conv_pw.weight", cin, m, fold_bn(sd, q + "bn1", m));
+        const float* wd = need(sd, q + "conv_dw.weight", {m, 1, k, k}).data;
+        BN bn2 = fold_bn(sd, q + "bn2", m);
+        std::vector<float> w9((size_t)cs * 9, 0.f), bd(cs, 0.f);
+        for (int c = 0; c < m; ++c) {
+          for (int t = 0; t < 9; ++t) w9[(size_t)c * 9 + t] = wd[(size_t)c * 9 + t] * bn2.a[c];
+          bd[c] = bn2.b[c];
+        }
+        b.dw_w = arena_.add_vec(w9);
+        b.dw_b = arena_.add_vec(bd);
+        const float* w1 = need(sd, q + "se.conv_reduce.weight", {b.rd, m, 1, 1}).data;
+        const float* b1 = need(sd, q + "se.conv_reduce.bias", {b.rd}).data;
+        const float* w2 = need(sd, q + "se.conv_expand.weight", {m, b.rd, 1, 1}).data;
+        const float* b2 = need(sd, q + "se.conv_expand.bias", {m}).data;
+        b.se_w1 = arena_.add(w1, sizeof(float) * b.rd * m);
+        b.se_b1 = arena_.add(b1, sizeof(float) * b.rd);
+        std::vector<float> w2t((size_t)b.rd * m);  // [rd][mid]: coalesced over channels
+        for (int c = 0; c < m; ++c)
+          for (int r = 0; r < b.rd; ++r) w2t[(size_t)r * m + c] = w2[(size_t)c * b.rd + r];
+        b.se_w2 = arena_.add_vec(w2t);
+        b.se_b2 = arena_.add(b2, sizeof(float) * m);
+        conv1x1(b.c2, q + "conv_pwl.weight", m, b.cout, fold_bn(sd, q + "bn3", b.cout));
+      }
+      blocks_.push_back(b);
+      cin = sdf.cout;
+    }
+  }
+  // BiLSTM: input projection of both directions as one fp32 GEMM (rows [fwd 4H | bwd 4H]).
+  const int H = hidden_;
+  const float* wih[2] = {need(sd, "rnn.lstm.weight_ih_l0", {4 * H, EFF_OUT}).data,
+                         need(sd, "rnn.lstm.weight_ih_l0_reverse", {4 * H, EFF_OUT}).data};
+  const float* bih[2] = {need(sd, "rnn.lstm.bias_ih_l0", {4 * H}).data, need(sd, "rnn.lstm.bias_ih_l0_reverse", {4 * H}).data};
+  const float* bhh[2] = {need(sd, "rnn.lstm.bias_hh_l0", {4 * H}).data, need(sd, "rnn.lstm.bias_hh_l0_reverse", {4 * H}).data};
+  const float* whh[2] = {need(sd, "rnn.lstm.weight_hh_l0", {4 * H, H}).data,
+                         need(sd, "rnn.lstm.weight_hh_l0_reverse", {4 * H, H}).data};
+  lstm_ih_ = make_pconv(KIND_GEMM, EFF_OUT, 8 * H, 1, M2S_DT_F32);
+  lstm_ih_.cs_in = EFF_OUT;  // 208 = 13 x 16: valid fp32 K chunking without padding
+  lstm_ih_.tpc = 1;
+  lstm_ih_.kp = EFF_OUT;
+  lstm_ih_.cs_out = 8 * H;
+  lstm_ih_.n_pad = round_up(8 * H, 64);
+  lstm_ih_.macs_per_row = 8.0 * H * EFF_OUT;
+  pack_conv(arena_, M2S_DT_F32, lstm_ih_,
+            [&](int, int n, int, int c) { return wih[n / (4 * H)][(size_t)(n % (4 * H)) * EFF_OUT + c]; },
+            [&](int n) { return bih[n / (4 * H)][n % (4 * H)] + bhh[n / (4 * H)][n % (4 * H)]; });
+  std::vector<float> wh((size_t)2 * 4 * H * H);
+  std::memcpy(wh.data(), whh[0], sizeof(float) * 4 * H * H);
+  std::memcpy(wh.data() + (size_t)4 * H * H, whh[1], sizeof(float) * 4 * H * H);
+  whh_ = arena_.add_vec(wh);
+  const float* hw = need(sd, "head.weight", {n_mels, H}).data;
+  const float* hb = need(sd, "head.bias", {n_mels}).data;
+  std::vector<float> wt((size_t)H * n_mels);
+  for (int n = 0; n < n_mels; ++n)
+    for (int k = 0; k < H; ++k) wt[(size_t)k * n_mels + n] = hw[(size_t)n * H + k];
+  head_wt_ = arena_.add_vec(wt);
+  head_b_ = arena_.add(hb, sizeof(float) * n_mels);
+
+  arena_.upload(device);
+  for (auto& b : blocks_) {
+    b.c1.resolve(arena_);
+    if (b.type != 0) b.c2.resolve(arena_);
+  }
+  lstm_ih_.resolve(arena_);
+}
+
+void Acoustic::effnet_dims(int H, int W, size_t* io, size_t* mid, size_t* se) const {
+  int oh, ow, ph, pw;
+  same_pad(H, 3, 2, &oh, &ph);
+  same_pad(W, 3, 2, &ow, &pw);
+  size_t mio = (size_t)oh * ow * chan_stride(EFF_STEM), mmid = 0, mse = 0;
+  for (const Block& b : blocks_) {
+    int nh, nw;
+    same_pad(oh, 3, b.stride, &nh, &ph);
+    same_pad(ow, 3, b.stride, &nw, &pw);
+    if (b.type == 1) mmid = std::max(mmid, (size_t)nh * nw * chan_stride(b.mid));
+    if (b.type == 2) {
+      mmid = std::max(mmid, (size_t)oh * ow * chan_stride(b.mid));
+      mse = std::max(mse, (size_t)dw_row_groups(nh) * chan_stride(b.mid));
+    }
+    mio = std::max(mio, (size_t)nh * nw * chan_stride(b.cout));
+    oh = nh;
+    ow = nw;
+  }
+  *io = mio;
+  *mid = mmid;
+  *se = mse;
+}
+
+size_t Acoustic::effnet_ws(int N, int H, int W) const {
+  size_t io, mid, se;
+  effnet_dims(H, W, &io, &mid, &se);
+  const size_t es = dtype_ == M2S_DT_BF16 ? 2 : 4;
+  const size_t nc = std::min(N, chunk);
+  Workspace ws(nullptr, 0);
+  ws.take<char>(nc * io * es);
+  ws.take<char>(nc * io * es);
+  ws.take<char>(nc * mid * es);
+  ws.take<char>(nc * mid * es);
+  ws.take<float>(nc * se);
+  ws.take<float>(nc * max_mid_cs_);
+  return ws.used();
+}
+
+size_t Acoustic::workspace_bytes(int B, int T, int H, int W) const {
+  const size_t BT = (size_t)B * T;
+  Workspace ws(nullptr, 0);
+  ws.take<float>(BT * EFF_OUT);
+  ws.take<char>(effnet_ws(B * T, H, W));
+  ws.take<float>(BT * 8 * hidden_);
+  ws.take<float>(2 * BT * hidden_);
+  ws.take<float>((size_t)2 * B * hidden_);
+  return ws.used();
+}
+
+void Acoustic::effnet(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe,
+                      int* probe_dims, Workspace& ws, hipStream_t s) {
+  if (dtype_ == M2S_DT_BF16)
+    effnet_t<bf16_t>(frames, N, H, W, feats, stop_after, probe, probe_dims, ws, s);
+  else
+    effnet_t<float>(frames, N, H, W, feats, stop_after, probe, probe_dims, ws, s);
+}
+
+template <typename T>
+void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe,
+                        int* probe_dims, Workspace& ws, hipStream_t s) {
+  M2S_CHECK(N > 0 && H >= 32 && W >= 32, "effnet: bad input size");
+  size_t io, mid, se;
+  effnet_dims(H, W, &io, &mid, &se);
+  const int nc_max = std::min(N, chunk);
+  T* A = ws.take<T>((size_t)nc_max * io);
+  T* Bb = ws.take<T>((size_t)nc_max * io);
+  T* M = ws.take<T>((size_t)nc_max * mid);
+  T* M2 = ws.take<T>((size_t)nc_max * mid);
+  float* sums = ws.take<float>((size_t)nc_max * se);
+  float* scale = ws.take<float>((size_t)nc_max * max_mid_cs_);
+  const bool exact = sizeof(T) == 4;
+
+  for (int n0 = 0; n0 < N; n0 += nc_max) {
+    const int nc = std::min(nc_max, N - n0);
+    int oh, ow, pt, pl;
+    same_pad(H, 3, 2, &oh, &pt);
+    same_pad(W, 3, 2, &ow, &pl);
+    {
+      ProfScope ps("stem", 2.0 * nc * oh * ow * EFF_STEM * 27, 4.0 * nc * H * W + sizeof(T) * (double)nc * oh * ow * 32, s);
+      launch_stem<T>(frames + (size_t)n0 * H * W, nc, H, W, oh, ow, pt, pl, static_cast<const float*>(arena_.ptr(stem_w_)),
+                     static_cast<const float*>(arena_.ptr(stem_b_)), EFF_STEM, chan_stride(EFF_STEM), A, s);
+    }
+    T* cur = A;
+    T* nxt = Bb;
+    int cc = EFF_STEM;
+    int bi = 0;
+    auto tap = [&](int done) {
+      if (stop_after == done && probe) {
+        launch_unpad<T>(cur, (long)nc * oh * ow, cc, chan_stride(cc), probe + (size_t)n0 * oh * ow * cc, s);
+        if (probe_dims) {
+          probe_dims[0] = oh;
+          probe_dims[1] = ow;
+          probe_dims[2] = cc;
+        }
+        return true;
+      }
+      return false;
+    };
+    if (tap(0)) continue;
+    bool stopped = false;
+    for (const Block& b : blocks_) {
+      int nh, nw, qt, ql;
+      same_pad(oh, 3, b.stride, &nh, &qt);
+      same_pad(ow, 3, b.stride, &nw, &ql);
+      auto a2d = [&](const PConv& pc, const void* x, void* y) {
+        ConvArgs a = conv_args(pc);
+        a.x = x;
+        a.y = y;
+        a.IH = oh;
+        a.IW = ow;
+        a.OH = nh;
+        a.OW = nw;
+        a.pad_t = qt;
+        a.pad_l = ql;
+        a.M = nc * nh * nw;
+        return a;
+      };
+      if (b.type == 0) {
+        ConvArgs a = a2d(b.c1, cur, nxt);
+        a.act = ACT_SILU;
+        a.res = b.skip ? cur : nullptr;
+        run_conv<T>(a, b.c1, s);
+      } else if (b.type == 1) {
+        ConvArgs a = a2d(b.c1, cur, M);
+        a.act = ACT_SILU;
+        run_conv<T>(a, b.c1, s);
+        ConvArgs p = conv_args(b.c2);
+        p.x = M;
+        p.y = nxt;
+        p.M = nc * nh * nw;
+        p.OH = nh * nw;
+        p.res = b.skip ? cur : nullptr;
+        run_conv<T>(p, b.c2, s);
+      } else {
+        const int cs = chan_stride(b.mid);
+        ConvArgs e = conv_args(b.c1);
+        e.x = cur;
+        e.y = M;
+        e.M = nc * oh * ow;
+        e.OH = oh * ow;
+        e.act = ACT_SILU;
+        run_conv<T>(e, b.c1, s);
+        {
+          ProfScope ps("dwconv_se", 2.0 * nc * nh * nw * b.mid * 9,
+                       sizeof(T) * (double)nc * (oh * ow + nh * nw) * b.mid, s);
+          launch_dwconv<T>(M, nc, oh, ow, nh, nw, b.stride, qt, ql, b.mid, cs,
+                           static_cast<const float*>(arena_.ptr(b.dw_w)), static_cast<const float*>(arena_.ptr(b.dw_b)),
+                           M2, sums, s);
+        }
+        {
+          ProfScope ps("se_fc", 4.0 * nc * b.mid * b.rd, 8.0 * nc * b.mid, s);
+          launch_se_fc(sums, dw_row_groups(nh), nc, b.mid, cs, b.rd, 1.0f / (float)(nh * nw), static_cast<const float*>(arena_.ptr(b.se_w1)),
+                       static_cast<const float*>(arena_.ptr(b.se_b1)), static_cast<const float*>(arena_.ptr(b.se_w2)),
+                       static_cast<const float*>(arena_.ptr(b.se_b2)), scale, exact, s);
+        }
+        ConvArgs p = conv_args(b.c2);
+        p.x = M2;
+        p.y = nxt;
+        p.M = nc * nh * nw;
+        p.OH = nh * nw;
+        p.in_xform = IN_SE_SCALE;
+        p.in_scale = scale;
+        p.res = b.skip ? cur : nullptr;
+        run_conv<T>(p, b.c2, s);
+      }
+      std::swap(cur, nxt);
+      oh = nh;
+      ow = nw;
+      cc = b.cout;
+      ++bi;
+      if (tap(bi)) {
+        stopped = true;
+        break;
+      }
+    }
+    if (stopped || !feats) continue;
+    ProfScope ps("gap", (double)nc * oh * ow * cc, sizeof(T) * (double)nc * oh * ow * cc, s);
+    launch_gap<T>(cur, nc, oh * ow, cc, chan_stride(cc), feats + (size_t)n0 * EFF_OUT, s);
+  }
+}
+
+void Acoustic::bilstm(const float* feats, int B, int T, float* y, float* mel_norm, Workspace& ws, hipStream_t s) {
+  M2S_CHECK(B > 0 && T > 0, "bilstm: empty input");
+  const int H = hidden_;
+  const size_t BT = (size_t)B * T;
+  float* pre = ws.take<float>(BT * 8 * H);
+  float* hs = ws.take<float>(2 * BT * H);
+  float* cst = ws.take<float>((size_t)2 * B * H);
+  ConvArgs a = conv_args(lstm_ih_);
+  a.x = feats;
+  a.y = pre;
+  a.M = (int)BT;
+  run_conv<float>(a, lstm_ih_, s);
+  for (int st = 0; st < T; ++st) {
+    ProfScope ps("lstm_step", 2.0 * 2 * B * 4.0 * H * H, 4.0 * 2 * 4 * H * H, s);
+    launch_lstm_step(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, cst, B, T, H, st, s);
+  }
+  if (mel_norm) {
+    ProfScope ps("mel_head", 2.0 * BT * H * n_mels_, 4.0 * BT * (2 * H + n_mels_), s);
+    launch_mel_head(hs, (int)BT, H, static_cast<const float*>(arena_.ptr(head_wt_)),
+                    static_cast<const float*>(arena_.ptr(head_b_)), n_mels_, mel_norm, s);
+  }
+  if (y) launch_add2(hs, hs + BT * H, y, (long)(BT * H), s);
+}
+
+void Acoustic::forward(const float* frames, int B, int T, int H, int W, float* mel_norm, void* wsp, size_t wsb,
+                       hipStream_t s) {
+  M2S_CHECK(B > 0 && T > 0, "acoustic: empty input");
+  Workspace ws(wsp, wsb);
+  float* feats = ws.take<float>((size_t)B * T * EFF_OUT);
+  effnet(frames, B * T, H, W, feats, -1, nullptr, nullptr, ws, s);
+  bilstm(feats, B, T, nullptr, mel_norm, ws, s);
+}
+
+// ------------------------------------------------------------------------------------------
+// Vocoder
+static std::vector<float> fold_wn(const StateDict& sd, const std::string& p, std::vector<int64_t> shape) {
+  auto it = sd.find(p + ".weight");
+  if (it != sd.end()) {
+    const HostTensor& t = need(sd, p + ".weight", shape);
+    return std::vector<float>(t.data, t.data + t.numel());
+  }
+  std::vector<int64_t> gs(shape.size(), 1);
+  gs[0] = shape[0];
+  const HostTensor& g = need(sd, p + ".weight_g", gs);
+  const HostTensor& v = need(sd, p + ".weight_v", shape);
+  const size_t inner = v.numel() / shape[0];
+  std::vector<float> w(v.numel());
+  for (int64_t i = 0; i < shape[0]; ++i) {
+    double acc = 0.0;
+    for (size_t j = 0; j < inner; ++j) acc += (double)v.data[i * inner + j] * v.data[i * inner + j];
+    const float sc = g.data[i] / (float)std::sqrt(acc);
+    for (size_t j = 0; j < inner; ++j) w[i * inner + j] = v.data[i * inner + j] * sc;
+  }
+  return w;
+}
+
+Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int device)
+    : h_(h), dtype_(dtype), device_(device) {
+  M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16, "bad dtype");
+  M2S_CHECK(h.resblock == 1 || h.resblock == 2, "resblock must be 1 or 2");
+  M2S_CHECK(h.n_up >= 1 && h.n_up <= 8 && h.n_kernels >= 1 && h.n_kernels <= 8, "bad generator config");
+  const int c0 = h.upsample_initial_channel;
+  {  // conv_pre: Conv1d(num_mels, c0, 7), no weight norm (models.py:94)
+    const HostTensor& w = need(sd, "conv_pre.weight", {c0, h.num_mels, 7});
+    const HostTensor& b = need(sd, "conv_pre.bias", {c0});
+    pre_ = make_pconv(KIND_CONV1D, h.num_mels, c0, 7, dtype);
+    pre_.ks = 7;
+    pre_.pad_left = 0;  // F.pad(x, (0, 6)): look-ahead of 6 frames, zeros past the end
+    pre_.macs_per_row = (double)c0 * h.num_mels * 7;
+    const int ci = h.num_mels;
+    pack_conv(arena_, dtype, pre_, [&](int, int n, int t, int c) { return w.data[((size_t)n * ci + c) * 7 + t]; },
+              [&](int n) { return b.data[n]; });
+  }
+  hop_ = 1;
+  for (int i = 0; i < h.n_up; ++i) {
+    const int u = h.upsample_rates[i], k = h.upsample_kernel_sizes[i];
+    const int ci = c0 >> i, co = c0 >> (i + 1);
+    M2S_CHECK(co >= 4, "generator too narrow");
+    hop_ *= u;
+    const std::string p = "ups." + std::to_string(i);
+    std::vector<float> w = fold_wn(sd, p, {ci, co, k});  // ConvTranspose1d weight (in, out, k)
+    const HostTensor& b = need(sd, p + ".bias", {co});
+    PConv pc = make_pconv(KIND_CONVT, ci, co, (k + u - 1) / u, dtype);
+    pc.phases = u;
+    pc.ct_u = u;
+    pc.ct_pad = (k - u) / 2;
+    pc.ct_k = k;
+    pc.macs_per_row = (double)ci * co * k / u;  // per output position, averaged over phases
+    const int pad = pc.ct_pad;
+    pack_conv(arena_, dtype, pc,
+              [&](int ph, int n, int t, int c) {
+                const int j = (ph + pad) % u + t * u;  // tap t of phase ph uses kernel index j
+                return j < k ? w[((size_t)c * co + n) * k + j] : 0.f;
+              },
+              [&](int n) { return b.data[n]; });
+    ups_.push_back(pc);
+    for (int j = 0; j < h.n_kernels; ++j) {
+      RB rb;
+      rb.k = h.resblock_kernel_sizes[j];
+      const int kk = rb.k;
+      for (int d = 0; d < h.n_dilations[j]; ++d) rb.dil.push_back(h.resblock_dilation_sizes[j][d]);
+      const std::string q = "resblocks." + std::to_string(i * h.n_kernels + j);
+      auto mk = [&](const std::string& name, int dil) {
+        std::vector<float> wv = fold_wn(sd, name, {co, co, kk});
+        const HostTensor& bv = need(sd, name + ".bias", {co});
+        PConv c = make_pconv(KIND_CONV1D, co, co, kk, dtype);
+        c.ks = kk;
+        c.dil = dil;
+        c.pad_left = (kk - 1) * dil;  // get_padding(k, d) = k*d - d, then truncation: causal (utils.py:33-34)
+        c.macs_per_row = (double)co * co * kk;
+        pack_conv(arena_, dtype, c, [&](int, int n, int t, int cc) { return wv[((size_t)n * co + cc) * kk + t]; },
+                  [&](int n) { return bv.data[n]; });
+        return c;
+      };
+      for (size_t d = 0; d < rb.dil.size(); ++d) {
+        if (h.resblock == 1) {
+          rb.c1.push_back(mk(q + ".convs1." + std::to_string(d), rb.dil[d]));
+          rb.c2.push_back(mk(q + ".convs2." + std::to_string(d), 1));
+        } else {
+          rb.c1.push_back(mk(q + ".convs." + std::to_string(d), rb.dil[d]));
+        }
+      }
+      rbs_.push_back(rb);
+    }
+  }
+  post_c_ = c0 >> h.n_up;
+  {
+    std::vector<float> w = fold_wn(sd, "conv_post", {1, post_c_, 7});
+    const HostTensor& b = need(sd, "conv_post.bias", {1});
+    std::vector<float> wt((size_t)7 * post_c_);
+    for (int c = 0; c < post_c_; ++c)
+      for (int t = 0; t < 7; ++t) wt[(size_t)t * post_c_ + c] = w[(size_t)c * 7 + t];
+    post_w_ = arena_.add_vec(wt);
+    post_b_ = b.data[0];
+  }
+  arena_.upload(device);
+  pre_.resolve(arena_);
+  for (auto& u : ups_) u.resolve(arena_);
+  for (auto& rb : rbs_) {
+    for (auto& c : rb.c1) c.resolve(arena_);
+    for (auto& c : rb.c2) c.resolve(arena_);
+  }
+}
+
+size_t Vocoder::act_elems(int B, int T) const {
+  size_t m = (size_t)B * T * chan_stride(h_.upsample_initial_channel);
+  size_t L = T;
+  for (int i = 0; i < h_.n_up; ++i) {
+    L *= h_.upsample_rates[i];
+    m = std::max(m, (size_t)B * L * chan_stride(h_.upsample_initial_channel >> (i + 1)));
+  }
+  return m;
+}
+
+size_t Vocoder::workspace_bytes(int B, int T) const {
+  const size_t es = dtype_ == M2S_DT_BF16 ? 2 : 4;
+  Workspace ws(nullptr, 0);
+  ws.take<char>((size_t)B * T * chan_stride(h_.num_mels) * es);
+  for (int i = 0; i < 5; ++i) ws.take<char>(act_elems(B, T) * es);
+  return ws.used();
+}
+
+void Vocoder::forward(const float* mel, int layout, int B, int T, float* wav, Workspace& ws, hipStream_t s) {
+  M2S_CHECK(B > 0 && T > 0, "vocoder: empty input");
+  const int cs = chan_stride(h_.num_mels);
+  if (dtype_ == M2S_DT_BF16) {
+    bf16_t* mn = ws.take<bf16_t>((size_t)B * T * cs);
+    launch_mel_to_nlc<bf16_t>(mel, B, h_.num_mels, T, layout, mn, cs, s);
+    run_t<bf16_t>(mn, B, T, wav, ws, s);
+  } else {
+    float* mn = ws.take<float>((size_t)B * T * cs);
+    launch_mel_to_nlc<float>(mel, B, h_.num_mels, T, layout, mn, cs, s);
+    run_t<float>(mn, B, T, wav, ws, s);
+  }
+}
+
+void Vocoder::forward_from_norm(const float* mel_norm, const float* mean, const float* std_, int B, int T,
+                                float* mel_db, float* mel_log, void* ln_buf, float* wav, Workspace& ws, hipStream_t s) {
+  M2S_CHECK(B > 0 && T > 0, "vocoder: empty input");
+  const int nm = h_.num_mels, cs = chan_stride(nm);
+  ws.take<char>((size_t)B * T * cs * (dtype_ == M2S_DT_BF16 ? 2 : 4));  // same carve as forward()
+  const bool bf = dtype_ == M2S_DT_BF16;
+  {
+    ProfScope ps("mel_glue", 0.0, 4.0 * B * T * nm * 4, s);
+    if (bf)
+      launch_mel_glue<bf16_t>(mel_norm, B * T, nm, mean, std_, mel_db, mel_log, static_cast<bf16_t*>(ln_buf), cs, s);
+    else
+      launch_mel_glue<float>(mel_norm, B * T, nm, mean, std_, mel_db, mel_log, static_cast<float*>(ln_buf), cs, s);
+  }
+  if (bf)
+    run_t<bf16_t>(ln_buf, B, T, wav, ws, s);
+  else
+    run_t<float>(ln_buf, B, T, wav, ws, s);
+}
+
+template <typename T>
+void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& ws, hipStream_t s) {
+  const size_t n = act_elems(B, Tn);
+  T* X = ws.take<T>(n);
+  T* Hb[2] = {ws.take<T>(n), ws.take<T>(n)};
+  T* T1 = ws.take<T>(n);
+  T* S = ws.take<T>(n);
+  int L = Tn;
+  {
+    ConvArgs a = conv_args(pre_);
+    a.x = mel_nlc;
+    a.y = S;
+    a.L_in = L;
+    a.L_out = L;
+    a.M = B * L;
+    run_conv<T>(a, pre_, s);
+  }
+  const int nk = h_.n_kernels;
+  for (int i = 0; i < h_.n_up; ++i) {
+    const PConv& up = ups_[i];
+    ConvArgs a = conv_args(up);
+    a.x = S;
+    a.y = X;
+    a.L_in = L;
+    a.L_out = L * up.ct_u;
+    a.M = B * L;  // rows per phase
+    a.in_xform = IN_LRELU;
+    a.in_slope = 0.1f;
+    run_conv<T>(a, up, s);
+    L *= up.ct_u;
+    for (int j = 0; j < nk; ++j) {
+      const RB& rb = rbs_[i * nk + j];
+      const T* hcur = X;
+      const int np = (int)rb.dil.size();
+      for (int p = 0; p < np; ++p) {
+        const bool last = p == np - 1;
+        T* out = last ? S : Hb[p & 1];
+        ConvArgs c = conv_args(rb.c1[p]);
+        c.x = hcur;
+        c.L_in = L;
+        c.L_out = L;
+        c.M = B * L;
+        c.in_xform = IN_LRELU;
+        c.in_slope = 0.1f;
+        if (h_.resblock == 1) {  // xt = c2(lrelu(c1(lrelu(x)))) ; x = xt + x
+          c.y = T1;
+          c.act = ACT_LRELU;
+          c.act_slope = 0.1f;
+          run_conv<T>(c, rb.c1[p], s);
+          c = conv_args(rb.c2[p]);
+          c.x = T1;
+          c.L_in = L;
+          c.L_out = L;
+          c.M = B * L;
+        }
+        c.y = out;
+        c.res = hcur;
+        if (last) {  // xs = sum_j resblock_j(x); x = xs / num_kernels (models.py:119-125)
+          c.accum = j == 0 ? 0 : (j == nk - 1 ? 2 : 1);
+          c.accum_div = (float)nk;
+        }
+        run_conv<T>(c, h_.resblock == 1 ? rb.c2[p] : rb.c1[p], s);
+        hcur = out;
+      }
+    }
+  }
+  ProfScope ps("conv_post", 2.0 * B * L * post_c_ * 7, sizeof(T) * (double)B * L * post_c_ + 4.0 * B * L, s);
+  launch_conv_post<T>(S, B, L, post_c_, chan_stride(post_c_), static_cast<const float*>(arena_.ptr(post_w_)), post_b_,
+                      wav, s);
+}
+
+}  // namespace m2s

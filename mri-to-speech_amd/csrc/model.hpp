@@ -1,0 +1,149 @@
+// Packed models and their execution plans (host side of libm2s).
+#pragma once
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/m2s.h"
+#include "conv_igemm.hpp"
+#include "kernels.hpp"
+
+namespace m2s {
+
+struct HostTensor {
+  const float* data = nullptr;
+  std::vector<int64_t> shape;
+  size_t numel() const {
+    size_t n = 1;
+    for (auto d : shape) n *= (size_t)d;
+    return n;
+  }
+};
+using StateDict = std::map<std::string, HostTensor>;
+StateDict make_state_dict(const m2s_tensor* t, int n);
+
+// Host staging of every packed array; one device allocation per model.
+class Arena {
+ public:
+  size_t add(const void* p, size_t bytes);
+  template <class V>
+  size_t add_vec(const std::vector<V>& v) {
+    return add(v.data(), v.size() * sizeof(V));
+  }
+  void upload(int device);
+  void* ptr(size_t off) const { return static_cast<char*>(dev_) + off; }
+  size_t bytes() const { return host_.size(); }
+  ~Arena();
+
+ private:
+  std::vector<uint8_t> host_;
+  void* dev_ = nullptr;
+};
+
+// One packed dense conv layer (rows = output channels [x phases], k = tap * cs_in + c).
+struct PConv {
+  int kind = KIND_GEMM;
+  int cin = 0, cout = 0, cs_in = 0, cs_out = 0;
+  int ntaps = 1, ks = 1, stride = 1, kp = 0, n_pad = 0, tpc = 1, phases = 1;
+  int dil = 1, pad_left = 0;
+  int ct_u = 1, ct_pad = 0, ct_k = 1;
+  double macs_per_row = 0;  // algorithmic MACs per output position (all phases)
+  size_t w_off = 0, b_off = 0;
+  const void* w = nullptr;
+  const float* b = nullptr;
+  void resolve(const Arena& a) {
+    w = a.ptr(w_off);
+    b = static_cast<const float*>(a.ptr(b_off));
+  }
+};
+
+class Workspace {  // bump allocator over a caller-provided device buffer
+ public:
+  Workspace(void* base, size_t bytes) : base_(static_cast<char*>(base)), cap_(bytes) {}
+  template <class T>
+  T* take(size_t n) {
+    size_t off = (used_ + 255) & ~size_t(255);
+    used_ = off + n * sizeof(T);
+    if (base_ && used_ > cap_) throw Error(M2S_E_ARG, "workspace too small");
+    return base_ ? reinterpret_cast<T*>(base_ + off) : nullptr;
+  }
+  size_t used() const { return (used_ + 255) & ~size_t(255); }
+
+ private:
+  char* base_;
+  size_t cap_;
+  size_t used_ = 0;
+};
+
+class Acoustic {
+ public:
+  Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int device);
+  int device() const { return device_; }
+  int n_mels() const { return n_mels_; }
+  int chunk = 256;
+
+  size_t workspace_bytes(int B, int T, int H, int W) const;
+  void forward(const float* frames, int B, int T, int H, int W, float* mel_norm, void* ws, size_t wsb, hipStream_t s);
+  void effnet(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe, int* probe_dims,
+              Workspace& ws, hipStream_t s);
+  void bilstm(const float* feats, int B, int T, float* y, float* mel_norm, Workspace& ws, hipStream_t s);
+
+ private:
+  struct Block {
+    int type = 0;  // 0 cn, 1 er, 2 ir
+    int stride = 1, cin = 0, cout = 0, mid = 0, rd = 0;
+    bool skip = false;
+    PConv c1, c2;              // cn: c1 ; er: conv_exp, conv_pwl ; ir: conv_pw, conv_pwl
+    size_t dw_w = 0, dw_b = 0;  // ir depthwise (cs_mid x 9, cs_mid) fp32
+    size_t se_w1 = 0, se_b1 = 0, se_w2 = 0, se_b2 = 0;
+  };
+  template <typename T>
+  void effnet_t(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe, int* probe_dims,
+                Workspace& ws, hipStream_t s);
+  size_t effnet_ws(int N, int H, int W) const;
+  void effnet_dims(int H, int W, size_t* io_elems, size_t* mid_elems, size_t* se_elems) const;
+
+  int dtype_, device_, n_mels_, hidden_;
+  Arena arena_;
+  size_t stem_w_ = 0, stem_b_ = 0;
+  std::vector<Block> blocks_;
+  PConv lstm_ih_;
+  size_t whh_ = 0, head_wt_ = 0, head_b_ = 0;
+  int max_mid_cs_ = 0;
+};
+
+class Vocoder {
+ public:
+  Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int device);
+  int device() const { return device_; }
+  int hop() const { return hop_; }
+  int num_mels() const { return h_.num_mels; }
+  size_t workspace_bytes(int B, int T) const;
+  void forward(const float* mel, int layout, int B, int T, float* wav, Workspace& ws, hipStream_t s);
+  // pipeline entry: mel glue (dB, ln-power; run_mri_video_inference.py:227-233) fused with the
+  // cast to the channel-last vocoder input (ln_buf: rows x cs(num_mels) x 4 bytes), then the generator.
+  void forward_from_norm(const float* mel_norm, const float* mean, const float* std_, int B, int T, float* mel_db,
+                         float* mel_log, void* ln_buf, float* wav, Workspace& ws, hipStream_t s);
+  size_t act_elems(int B, int T) const;
+
+ private:
+  template <typename T>
+  void run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& ws, hipStream_t s);
+  struct RB {
+    int k = 3;
+    std::vector<int> dil;
+    std::vector<PConv> c1, c2;  // resblock "1": c1 (dilated) + c2 ; "2": c1 only
+  };
+  m2s_hifigan_h h_;
+  int dtype_, device_, hop_ = 1;
+  Arena arena_;
+  PConv pre_;
+  std::vector<PConv> ups_;
+  std::vector<RB> rbs_;
+  size_t post_w_ = 0;
+  float post_b_ = 0.f;
+  int post_c_ = 0;
+};
+
+}  // namespace m2s

@@ -1,0 +1,22 @@
+// Event-based per-kernel timing used by bench.py's roofline figure (m2s_prof_* in m2s.h).
+#pragma once
+
+#include <string>
+
+#include "m2s_common.hpp"
+
+namespace m2s {
+
+bool prof_on();
+// Brackets one kernel launch with HIP events on `s` when profiling is enabled.
+class ProfScope {
+ public:
+  ProfScope(const char* name, double flops, double bytes, hipStream_t s);
+  ~ProfScope();
+
+ private:
+  int slot_ = -1;
+  hipStream_t s_;
+};
+
+}  // namespace m2s

@@ -1,0 +1,187 @@
+"""Drop-in ``mri_acoustic_model`` plug-in backed by libm2s (MI355X / gfx950).
+
+Same import path and factory as the reference plug-in (mri2speech_code/mri_acoustic_model.py:139-156):
+``--mri-code-dir`` -> ``from mri_acoustic_model import build_acoustic_model`` ->
+``build_acoustic_model(n_mels, cnn_pretrained, rnn_hidden, dropout, use_checkpoint, ckpt_segments,
+use_reentrant)``.  The returned module has the reference's tree (``cnn.backbone``, ``cnn.gap``,
+``rnn.lstm``, ``rnn.dropout``, ``head``) and state-dict keys (timm ``EfficientNetFeatures`` names for
+the backbone), so ``load_state_dict(checkpoint['model_state_dict'], strict=False)`` behaves the same.
+
+``forward`` (eval, HIP tensors) runs the whole CNN -> BiLSTM -> head graph in libm2s; the torch
+sub-modules are parameter containers only.  Compute dtype: ``M2S_DTYPE`` env var or
+``model.m2s_dtype`` ("fp32" default = reference numerics; "bf16" = MFMA fast path).
+No CPU fallback: CPU tensors, training mode and autograd raise.
+"""
+from __future__ import annotations
+
+import os
+import sys
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _PKG not in sys.path:
+    sys.path.insert(0, _PKG)
+
+from m2s.config import BN_EPS, EFFNET_STEM, effnet_blocks  # noqa: E402
+
+
+def _bn(c):
+    return nn.BatchNorm2d(c, eps=BN_EPS)
+
+
+class _ConvBnAct(nn.Module):  # timm ConvBnAct ('cn')
+    def __init__(self, b):
+        super().__init__()
+        self.conv = nn.Conv2d(b["cin"], b["cout"], b["k"], b["stride"], bias=False)
+        self.bn1 = _bn(b["cout"])
+
+
+class _EdgeResidual(nn.Module):  # timm EdgeResidual ('er')
+    def __init__(self, b):
+        super().__init__()
+        self.conv_exp = nn.Conv2d(b["cin"], b["mid"], b["k"], b["stride"], bias=False)
+        self.bn1 = _bn(b["mid"])
+        self.conv_pwl = nn.Conv2d(b["mid"], b["cout"], 1, bias=False)
+        self.bn2 = _bn(b["cout"])
+
+
+class _SqueezeExcite(nn.Module):
+    def __init__(self, c, rd):
+        super().__init__()
+        self.conv_reduce = nn.Conv2d(c, rd, 1, bias=True)
+        self.conv_expand = nn.Conv2d(rd, c, 1, bias=True)
+
+
+class _InvertedResidual(nn.Module):  # timm InvertedResidual ('ir', SE)
+    def __init__(self, b):
+        super().__init__()
+        m = b["mid"]
+        self.conv_pw = nn.Conv2d(b["cin"], m, 1, bias=False)
+        self.bn1 = _bn(m)
+        self.conv_dw = nn.Conv2d(m, m, b["k"], b["stride"], groups=m, bias=False)
+        self.bn2 = _bn(m)
+        self.se = _SqueezeExcite(m, b["rd"])
+        self.conv_pwl = nn.Conv2d(m, b["cout"], 1, bias=False)
+        self.bn3 = _bn(b["cout"])
+
+
+class _FeatureInfo:
+    def channels(self):
+        return [16, 32, 56, 120, 208]
+
+
+class _EffNetV2B2Features(nn.Module):
+    """Parameter container with timm ``tf_efficientnetv2_b2`` features_only key names."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv_stem = nn.Conv2d(3, EFFNET_STEM, 3, 2, bias=False)
+        self.bn1 = _bn(EFFNET_STEM)
+        stages = {}
+        for b in effnet_blocks():
+            cls = {"cn": _ConvBnAct, "er": _EdgeResidual, "ir": _InvertedResidual}[b["type"]]
+            stages.setdefault(b["stage"], []).append(cls(b))
+        self.blocks = nn.Sequential(*[nn.Sequential(*stages[s]) for s in sorted(stages)])
+        self.feature_info = _FeatureInfo()
+
+    def forward(self, x):
+        raise NotImplementedError("m2s runs the backbone fused inside libm2s; per-stage feature maps "
+                                  "(Grad-CAM, mri_gradcam_formant.py:155-158) are not exposed yet")
+
+
+class GlobalAvgPool(nn.Module):
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return torch.mean(x, dim=(2, 3))
+
+
+class EffNetV2B2Backbone(nn.Module):
+    def __init__(self, pretrained: bool = False):
+        super().__init__()
+        if pretrained:
+            raise ValueError("pretrained timm weights cannot be fetched offline; load a checkpoint instead")
+        self.backbone = _EffNetV2B2Features()
+        self.out_channels = self.backbone.feature_info.channels()[-1]
+        self.gap = GlobalAvgPool()
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """(N,1,H,W) or (N,H,W) grey frames -> (N, 208) (mri_acoustic_model.py:39-48)."""
+        if x.dim() == 4:
+            if x.size(1) != 1:
+                raise ValueError("m2s expects grey (1-channel) frames")
+            x = x[:, 0]
+        return self._root()._engine(x.device).effnet(x)
+
+
+class BiLSTMSumMerge(nn.Module):
+    def __init__(self, in_dim: int, hidden_size: int = 640, dropout: float = 0.0):
+        super().__init__()
+        self.lstm = nn.LSTM(input_size=in_dim, hidden_size=hidden_size, num_layers=1, batch_first=True,
+                            bidirectional=True, dropout=0.0)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """(B,T,C) -> (B,T,H) forward + backward hidden states (mri_acoustic_model.py:67-72)."""
+        return self._root()._engine(x.device).bilstm(x)[0]
+
+
+class OTNLikeCNNBiLSTM(nn.Module):
+    def __init__(self, n_mels: int = 64, cnn_pretrained: bool = False, rnn_hidden: int = 640,
+                 dropout: float = 0.5, use_checkpoint: bool = False, ckpt_segments: int = 2,
+                 use_reentrant: bool = False):
+        super().__init__()
+        self.n_mels = n_mels
+        self.use_checkpoint = use_checkpoint
+        self.ckpt_segments = ckpt_segments
+        self.use_reentrant = use_reentrant
+        self.cnn = EffNetV2B2Backbone(pretrained=cnn_pretrained)
+        self.rnn = BiLSTMSumMerge(in_dim=self.cnn.out_channels, hidden_size=rnn_hidden, dropout=dropout)
+        self.head = nn.Linear(rnn_hidden, n_mels)
+        self.m2s_dtype = os.environ.get("M2S_DTYPE", "fp32")
+        self.m2s_chunk = int(os.environ.get("M2S_CHUNK", "256"))
+        root = lambda: self  # noqa: E731  (children reach the engine without registering a cycle)
+        for m in (self.cnn, self.rnn):
+            object.__setattr__(m, "_root", root)
+        object.__setattr__(self, "_eng", None)
+        object.__setattr__(self, "_eng_key", None)
+
+    def _signature(self, device):
+        return (str(device), self.m2s_dtype, self.m2s_chunk,
+                tuple((t.data_ptr(), t._version) for t in self.state_dict().values()))
+
+    def _engine(self, device: torch.device):
+        if self.training:
+            raise NotImplementedError("m2s implements inference only; call .eval() (training / Grad-CAM "
+                                      "autograd is outside the accelerated path)")
+        if device.type != "cuda":
+            raise RuntimeError("m2s runs on MI355X (HIP) tensors only; move the model and frames to 'cuda'")
+        key = self._signature(device)
+        if self._eng is None or self._eng_key != key:
+            from m2s.runtime import AcousticEngine
+            sd = {k: v.detach().to("cpu") for k, v in self.state_dict().items()}
+            object.__setattr__(self, "_eng", AcousticEngine(sd, n_mels=self.n_mels,
+                                                            rnn_hidden=self.rnn.lstm.hidden_size,
+                                                            dtype=self.m2s_dtype, device=device,
+                                                            chunk=self.m2s_chunk))
+            object.__setattr__(self, "_eng_key", key)
+        return self._eng
+
+    def _check_grad(self, x):
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            if x.requires_grad:
+                raise NotImplementedError("m2s forward has no autograd; run under torch.no_grad()")
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """(B,T,1,H,W) or (B,T,H,W) -> (B,T,n_mels)  (mri_acoustic_model.py:116-136, eval)."""
+        self._check_grad(x)
+        return self._engine(x.device).forward(x)
+
+
+def build_acoustic_model(n_mels: int = 64, cnn_pretrained: bool = False, rnn_hidden: int = 640,
+                         dropout: float = 0.5, use_checkpoint: bool = False, ckpt_segments: int = 2,
+                         use_reentrant: bool = False) -> nn.Module:
+    return OTNLikeCNNBiLSTM(n_mels=n_mels, cnn_pretrained=cnn_pretrained, rnn_hidden=rnn_hidden,
+                            dropout=dropout, use_checkpoint=use_checkpoint, ckpt_segments=ckpt_segments,
+                            use_reentrant=use_reentrant)

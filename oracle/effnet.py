@@ -95,8 +95,11 @@ def _bn(x, sd, p, act):
     return F.silu(y) if act else y
 
 
-def effnet_features(sd: Dict[str, torch.Tensor], x: torch.Tensor, prefix: str = "cnn.backbone.") -> torch.Tensor:
-    """(N,1,H,W) or (N,H,W) or (N,3,H,W) fp32 -> last feature map (N,208,H/32,W/32)."""
+def effnet_features(sd: Dict[str, torch.Tensor], x: torch.Tensor, prefix: str = "cnn.backbone.",
+                    taps: list | None = None) -> torch.Tensor:
+    """(N,1,H,W) or (N,H,W) or (N,3,H,W) fp32 -> last feature map (N,208,H/32,W/32).
+
+    ``taps``, if given, receives the output of the stem and of every block (29 tensors)."""
     if x.dim() == 3:
         x = x.unsqueeze(1)
     if x.size(1) == 1:  # mri_acoustic_model.py:43-44
@@ -104,6 +107,8 @@ def effnet_features(sd: Dict[str, torch.Tensor], x: torch.Tensor, prefix: str = 
     p = prefix
     x = _conv(x, sd[p + "conv_stem.weight"], 3, 2)
     x = _bn(x, sd, p + "bn1", True)
+    if taps is not None:
+        taps.append(x)
     for b in block_table():
         q = f"{p}blocks.{b['stage']}.{b['idx']}."
         sc = x
@@ -129,6 +134,8 @@ def effnet_features(sd: Dict[str, torch.Tensor], x: torch.Tensor, prefix: str = 
             x = _bn(x, sd, q + "bn3", False)
         if b["skip"]:
             x = x + sc
+        if taps is not None:
+            taps.append(x)
     return x
 
 

@@ -1,0 +1,202 @@
+"""HIP path (libm2s through its C ABI) vs the CPU oracle / reference golden vectors.  GPU box only.
+
+Tolerances (fp32 path; the reference runs fp32 on CPU):
+  * vocoder waveform       max |dwav|  <= 1e-4        (tanh output in [-1, 1])
+  * BiLSTM / head          max |dy|    <= 2e-5 / 5e-5
+  * CNN features / taps    max |d| / max|ref| <= 1e-4 (relative to the tensor's scale)
+  * mel_norm end to end    max |d|     <= 1e-4 ; mel_log <= 5e-4 (x ln10/10 * std amplification)
+bf16 path (compute dtype of configs[1]): waveform SNR >= 25 dB, mel cosine >= 0.999 / max |d| <= 5e-2.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from m2s import synth
+from m2s.config import HIFIGAN_H
+from oracle import acoustic, effnet, hifigan
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+DEV = torch.device("cuda", 0)
+
+
+def _gold(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+def _snr_db(ref, x):
+    ref, x = np.asarray(ref, np.float64), np.asarray(x, np.float64)
+    return 10 * np.log10(np.sum(ref ** 2) / max(np.sum((ref - x) ** 2), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from m2s import runtime
+    return runtime
+
+
+@pytest.fixture(scope="module")
+def ac_state():
+    g = _gold("acoustic.npz")
+    return int(g["seed"]), synth.synth_acoustic_state(int(g["seed"]))
+
+
+@pytest.fixture(scope="module")
+def ac_f32(rt, ac_state):
+    return rt.AcousticEngine(ac_state[1], dtype="fp32", device=DEV)
+
+
+@pytest.fixture(scope="module")
+def ac_bf16(rt, ac_state):
+    return rt.AcousticEngine(ac_state[1], dtype="bf16", device=DEV)
+
+
+# ------------------------------------------------------------------------------ vocoder
+@pytest.mark.parametrize("case", ["r1", "r2"])
+def test_vocoder_fp32_matches_reference_golden(rt, case):
+    g = _gold("generator.npz")
+    h = json.loads(bytes(g[f"{case}_h"]).decode())
+    voc = rt.VocoderEngine(synth.synth_generator_state(int(g["seed"]), h), h, dtype="fp32", device=DEV)
+    wav = voc.forward(torch.from_numpy(g[f"{case}_mel"]).to(DEV)).cpu().numpy()
+    assert wav.shape == g[f"{case}_wav"].shape
+    np.testing.assert_allclose(wav, g[f"{case}_wav"], atol=1e-4, rtol=0)
+
+
+def test_vocoder_fp32_long_and_layouts(rt):
+    g = _gold("generator.npz")
+    h = json.loads(bytes(g["r1_h"]).decode())
+    voc = rt.VocoderEngine(synth.synth_generator_state(int(g["seed"]), h), h, dtype="fp32", device=DEV)
+    mel = torch.from_numpy(g["r1_mel30"]).to(DEV)
+    np.testing.assert_allclose(voc.forward(mel).cpu().numpy(), g["r1_wav30"], atol=1e-4, rtol=0)
+    nlc = voc.forward(mel.transpose(1, 2).contiguous(), layout=1).cpu().numpy()
+    np.testing.assert_allclose(nlc, g["r1_wav30"], atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("B,T", [(1, 1), (3, 17), (2, 64)])
+def test_vocoder_fp32_vs_oracle_shapes(rt, B, T):
+    h = HIFIGAN_H
+    sd = synth.synth_generator_state(5, h)
+    voc = rt.VocoderEngine(sd, h, dtype="fp32", device=DEV)
+    mel = synth.synth_mel_log(B, 64, T, seed=B * 100 + T)
+    ref = hifigan.generator({k: torch.from_numpy(v) for k, v in sd.items()}, h, torch.from_numpy(mel)).numpy()
+    wav = voc.forward(torch.from_numpy(mel).to(DEV)).cpu().numpy()
+    np.testing.assert_allclose(wav, ref, atol=1e-4, rtol=0)
+
+
+def test_vocoder_bf16_snr(rt):
+    h = HIFIGAN_H
+    sd = synth.synth_generator_state(5, h)
+    voc = rt.VocoderEngine(sd, h, dtype="bf16", device=DEV)
+    mel = synth.synth_mel_log(2, 64, 30, seed=9)
+    ref = hifigan.generator({k: torch.from_numpy(v) for k, v in sd.items()}, h, torch.from_numpy(mel)).numpy()
+    wav = voc.forward(torch.from_numpy(mel).to(DEV)).cpu().numpy()
+    assert _snr_db(ref, wav) >= 25.0
+
+
+# ------------------------------------------------------------------------------ BiLSTM + head
+@pytest.mark.parametrize("bt", ["2x7", "1x1", "8x4", "1x30"])
+def test_bilstm_head_matches_reference_golden(ac_f32, bt):
+    g = _gold("acoustic.npz")
+    y, m = ac_f32.bilstm(torch.from_numpy(g[f"lstm_{bt}_in"]).to(DEV))
+    np.testing.assert_allclose(y.cpu().numpy(), g[f"lstm_{bt}_y"], atol=2e-5, rtol=0)
+    np.testing.assert_allclose(m.cpu().numpy(), g[f"lstm_{bt}_head"], atol=5e-5, rtol=0)
+
+
+def test_bilstm_batch_over_32(ac_f32, ac_state):
+    sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
+    x = torch.from_numpy(np.random.default_rng(1).normal(0, 0.5, (37, 5, 208)).astype(np.float32))
+    ref_y = acoustic.bilstm_summerge(sd, x)
+    y, m = ac_f32.bilstm(x.to(DEV))
+    np.testing.assert_allclose(y.cpu().numpy(), ref_y.numpy(), atol=2e-5, rtol=0)
+    np.testing.assert_allclose(m.cpu().numpy(), acoustic.head(sd, ref_y).numpy(), atol=5e-5, rtol=0)
+
+
+# ------------------------------------------------------------------------------ CNN encoder
+def _rel(a, b):
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-6))
+
+
+def test_effnet_every_block_fp32(ac_f32, ac_state):
+    sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
+    fr = torch.from_numpy(synth.synth_frames(1, 2, seed=4)[0])
+    taps = []
+    effnet.effnet_features(sd, fr, taps=taps)
+    x = fr.to(DEV)
+    for i, ref in enumerate(taps):
+        got = ac_f32.probe(x, i).cpu().numpy()
+        assert got.shape == ref.shape, (i, got.shape, ref.shape)
+        assert _rel(got, ref.numpy()) <= 1e-4, f"block {i}: rel err {_rel(got, ref.numpy())}"
+
+
+@pytest.mark.parametrize("hw", [(256, 256), (96, 80), (67, 101)])
+def test_effnet_gap_fp32_sizes(ac_f32, ac_state, hw):
+    sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
+    fr = torch.from_numpy(synth.synth_frames(1, 3, hw=hw, seed=8)[0])
+    ref = effnet.effnet_gap(sd, fr).numpy()
+    got = ac_f32.effnet(fr.to(DEV)).cpu().numpy()
+    assert _rel(got, ref) <= 1e-4
+
+
+def test_effnet_chunking_is_exact(rt, ac_state):
+    eng = rt.AcousticEngine(ac_state[1], dtype="fp32", device=DEV, chunk=2)
+    ref_eng = rt.AcousticEngine(ac_state[1], dtype="fp32", device=DEV, chunk=256)
+    fr = torch.from_numpy(synth.synth_frames(1, 5, seed=12)[0]).to(DEV)
+    assert torch.equal(eng.effnet(fr), ref_eng.effnet(fr))
+
+
+def test_effnet_bf16_close(ac_bf16, ac_state):
+    sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
+    fr = torch.from_numpy(synth.synth_frames(1, 4, seed=8)[0])
+    ref = effnet.effnet_gap(sd, fr).numpy()
+    got = ac_bf16.effnet(fr.to(DEV)).cpu().numpy()
+    cos = float((got * ref).sum() / np.sqrt((got ** 2).sum() * (ref ** 2).sum()))
+    assert cos >= 0.999, cos
+
+
+# ------------------------------------------------------------------------------ acoustic model / pipeline
+def test_acoustic_forward_matches_reference_wiring(ac_f32):
+    g = _gold("acoustic.npz")
+    fr = synth.synth_frames(2, 3, seed=int(g["model_frames_seed"]))
+    out = ac_f32.forward(torch.from_numpy(fr[:1]).unsqueeze(2).to(DEV)).cpu().numpy()
+    np.testing.assert_allclose(out, g["model_out"], atol=1e-4, rtol=0)
+    out4 = ac_f32.forward(torch.from_numpy(fr[:, :2]).to(DEV)).cpu().numpy()
+    np.testing.assert_allclose(out4, g["model_out4d"], atol=1e-4, rtol=0)
+
+
+def test_mel_glue_matches_reference_golden(rt):
+    g = _gold("glue.npz")
+    db, ln = rt.mel_glue(torch.from_numpy(g["pred_norm"]).to(DEV), torch.from_numpy(g["scaler_mean"]),
+                         torch.from_numpy(g["scaler_std"]))
+    np.testing.assert_array_equal(db.cpu().numpy(), g["mel_db"])
+    np.testing.assert_allclose(ln.cpu().numpy(), g["mel_log"], atol=2e-6, rtol=0)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_pipeline_end_to_end(rt, ac_state, dtype):
+    sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
+    gsd = synth.synth_generator_state(3)
+    mean, std = synth.synth_scaler()
+    ac = rt.AcousticEngine(ac_state[1], dtype=dtype, device=DEV)
+    voc = rt.VocoderEngine(gsd, HIFIGAN_H, dtype=dtype, device=DEV)
+    pipe = rt.Pipeline(ac, voc, mean, std)
+    fr = synth.synth_frames(2, 6, seed=21)
+    out = pipe.forward(torch.from_numpy(fr).to(DEV))
+    # oracle: reference graph on CPU
+    B, T = fr.shape[:2]
+    f = effnet.effnet_gap(sd, torch.from_numpy(fr).reshape(B * T, 256, 256)).view(B, T, -1)
+    mn = acoustic.head(sd, acoustic.bilstm_summerge(sd, f))
+    db = acoustic.denormalize_mel(mn, mean, std)
+    ln = acoustic.mel_db_to_log(db)
+    wav = hifigan.generator({k: torch.from_numpy(v) for k, v in gsd.items()}, HIFIGAN_H, ln.transpose(1, 2))
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    if dtype == "fp32":
+        np.testing.assert_allclose(got["mel_norm"], mn.numpy(), atol=1e-4, rtol=0)
+        np.testing.assert_allclose(got["mel_db"], db.numpy(), atol=2e-3, rtol=0)
+        np.testing.assert_allclose(got["mel_log"], ln.numpy(), atol=5e-4, rtol=0)
+        np.testing.assert_allclose(got["wav"], wav[:, 0].numpy(), atol=2e-4, rtol=0)
+    else:
+        assert np.abs(got["mel_norm"] - mn.numpy()).max() <= 5e-2
+        assert _snr_db(wav[:, 0].numpy(), got["wav"]) >= 20.0
