@@ -1,0 +1,115 @@
+"""The drop-in surface on the GPU: plug-in acoustic model, models.Generator and the CLI script,
+driven exactly as the reference drives them, checked against the oracle / reference goldens."""
+import importlib.util
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from m2s import synth
+from m2s.config import HIFIGAN_H
+from oracle import acoustic, effnet, hifigan
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(REPO, "tests", "golden")
+
+
+def _t(sd):
+    return {k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}
+
+
+def test_plugin_forward_matches_reference_wiring():
+    from mri_acoustic_model import build_acoustic_model
+    g = np.load(os.path.join(GOLD, "acoustic.npz"))
+    m = build_acoustic_model(n_mels=64, cnn_pretrained=False, rnn_hidden=640, dropout=0.5).to("cuda")
+    missing, unexpected = m.load_state_dict(_t(synth.synth_acoustic_state(int(g["seed"]))), strict=False)
+    assert not missing and not unexpected
+    m.eval()
+    fr = synth.synth_frames(2, 3, seed=int(g["model_frames_seed"]))
+    with torch.no_grad():
+        out = m(torch.from_numpy(fr[:1]).unsqueeze(2).cuda())
+        feats = m.cnn(torch.from_numpy(fr[0]).unsqueeze(1).cuda())
+        y = m.rnn(feats.view(1, 3, 208))
+        head_out = m.head(y)
+    np.testing.assert_allclose(out.cpu().numpy(), g["model_out"], atol=1e-4, rtol=0)
+    np.testing.assert_allclose(head_out.cpu().numpy(), g["model_out"], atol=1e-4, rtol=0)
+    # re-loading weights invalidates the packed engine
+    m.load_state_dict(_t(synth.synth_acoustic_state(0)), strict=False)
+    with torch.no_grad():
+        out2 = m(torch.from_numpy(fr[:1]).unsqueeze(2).cuda())
+    assert not torch.allclose(out, out2)
+
+
+def test_generator_plugin_after_reference_loader():
+    from env import AttrDict
+    from models import Generator
+    from torch.nn.utils import remove_weight_norm
+    g = np.load(os.path.join(GOLD, "generator.npz"))
+    h = AttrDict(json.loads(bytes(g["r1_h"]).decode()))
+    gen = Generator(h).to("cuda")
+    gen.load_state_dict(_t(synth.synth_generator_state(int(g["seed"]), h)))
+    gen.eval()
+    with torch.no_grad():
+        w1 = gen(torch.from_numpy(g["r1_mel"]).cuda()).cpu().numpy()
+    for mod in list(gen.ups) + [gen.conv_post]:
+        remove_weight_norm(mod)
+    for r in gen.resblocks:
+        r.remove_weight_norm()
+    with torch.no_grad():
+        w2 = gen(torch.from_numpy(g["r1_mel"]).cuda()).cpu().numpy()
+    np.testing.assert_allclose(w1, g["r1_wav"], atol=1e-4, rtol=0)
+    np.testing.assert_allclose(w2, g["r1_wav_folded"], atol=1e-4, rtol=0)
+
+
+def _cli():
+    spec = importlib.util.spec_from_file_location(
+        "m2s_cli_gpu", os.path.join(REPO, "mri-to-speech_amd", "scripts", "run_mri_video_inference.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_cli_end_to_end(tmp_path, dtype):
+    """The reference CLI contract: checkpoint formats, plug-in dir, output files, numerics."""
+    T = 9
+    ac_sd = synth.synth_acoustic_state(4)
+    gen_sd = synth.synth_generator_state(4)
+    mean, std = synth.synth_scaler()
+    ckdir = tmp_path / "ck" / "mri"
+    ckdir.mkdir(parents=True)
+    torch.save({"epoch": 3, "model_state_dict": _t(ac_sd), "val_loss": 0.1}, ckdir / "best.pt")
+    torch.save({"generator": _t(gen_sd)}, tmp_path / "g_00000001")
+    (tmp_path / "config.json").write_text(json.dumps(dict(HIFIGAN_H)))
+    (tmp_path / "scaler.json").write_text(json.dumps({"mean": mean.tolist(), "std": std.tolist(), "count_frames": 5}))
+    rng = np.random.default_rng(0)
+    video = rng.integers(0, 256, size=(T + 2, 256, 256), dtype=np.uint8)
+    np.save(tmp_path / "clip01.npy", video)
+    cli = _cli()
+    res = cli.main(["--video", str(tmp_path / "clip01.npy"), "--mri-checkpoint", str(ckdir / "best.pt"),
+                    "--scaler-json", str(tmp_path / "scaler.json"), "--hifigan-config", str(tmp_path / "config.json"),
+                    "--hifigan-checkpoint", str(tmp_path / "g_00000001"), "--output-dir", str(tmp_path / "out"),
+                    "--mri-code-dir", os.path.join(REPO, "mri-to-speech_amd", "mri2speech_code"),
+                    "--max-frames", str(T), "--dtype", dtype])
+    out = tmp_path / "out"
+    for f in ("clip01_generated.wav", "clip01_mel.npy", "clip01_mel_log.npy", "clip01_mel.png"):
+        assert (out / f).exists(), f
+    mel_db = np.load(out / "clip01_mel.npy")
+    assert mel_db.shape == (T, 64) and res["audio"].shape == (T * 420,)
+    # oracle of the same call
+    frames = np.stack([acoustic.preprocess_frame(f) for f in video[:T]])
+    sd = _t(ac_sd)
+    f = effnet.effnet_gap(sd, torch.from_numpy(frames)).view(1, T, -1)
+    mn = acoustic.head(sd, acoustic.bilstm_summerge(sd, f))[0]
+    db = acoustic.denormalize_mel(mn, mean, std)
+    ln = acoustic.mel_db_to_log(db)
+    wav = hifigan.generator(_t(gen_sd), HIFIGAN_H, ln.t().unsqueeze(0))[0, 0].numpy()
+    if dtype == "fp32":
+        np.testing.assert_allclose(mel_db, db.numpy(), atol=2e-3, rtol=0)
+        np.testing.assert_allclose(np.load(out / "clip01_mel_log.npy"), ln.numpy(), atol=5e-4, rtol=0)
+        np.testing.assert_allclose(res["audio"], wav, atol=2e-4, rtol=0)
+    else:
+        assert np.abs(mel_db - db.numpy()).max() < 1.0  # dB; mel_norm x std(<=15) amplifies bf16 error
