@@ -64,30 +64,6 @@ def init_dist(args):
     return world, rank, local
 
 
-def flat_state(sd):
-    keys = [k for k in sd if sd[k].dtype == np.float32]
-    sizes = [sd[k].size for k in keys]
-    return keys, sizes
-
-
-def broadcast_state(sd, device, world):
-    """C1: rank 0's weights to every rank over RCCL (one flat fp32 buffer)."""
-    keys, sizes = flat_state(sd)
-    if world == 1:
-        return sd
-    flat = torch.from_numpy(np.concatenate([sd[k].ravel() for k in keys])).to(device)
-    dist.broadcast(flat, 0)
-    host = flat.cpu().numpy()
-    out, off = {}, 0
-    for k, n in zip(keys, sizes):
-        out[k] = host[off:off + n].reshape(sd[k].shape)
-        off += n
-    for k in sd:
-        if k not in out:
-            out[k] = sd[k]
-    return out
-
-
 def make_frames(clips, frames, hw, rank, device):
     g = torch.Generator(device=device)
     g.manual_seed(1234 + rank)
@@ -129,13 +105,14 @@ def main():
     world, rank, local = init_dist(args)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    from m2s import _native, runtime
+    from m2s import _native, dp, runtime
 
-    # weights: rank 0 generates, RCCL broadcast (C1), every rank packs its own copy
-    ac_sd = synth.synth_acoustic_state(0) if rank == 0 else synth.synth_acoustic_state(0)
-    gen_sd = synth.synth_generator_state(0)
-    ac_sd_b = broadcast_state(ac_sd, device, world)
-    gen_sd_b = broadcast_state(gen_sd, device, world)
+    # weights: rank 0's state dicts reach every rank over RCCL (C1); every rank packs its own copy.
+    # (Other ranks start from a differently seeded state so the broadcast is what makes them equal.)
+    ac_sd = synth.synth_acoustic_state(0 if rank == 0 else 1000 + rank)
+    gen_sd = synth.synth_generator_state(0 if rank == 0 else 1000 + rank)
+    ac_sd_b = dp.broadcast_state(ac_sd, device)
+    gen_sd_b = dp.broadcast_state(gen_sd, device)
     mean, std = synth.synth_scaler()
     ac = runtime.AcousticEngine(ac_sd_b, dtype=args.dtype, device=device, chunk=args.chunk)
     voc = runtime.VocoderEngine(gen_sd_b, HIFIGAN_H, dtype=args.dtype, device=device)
@@ -145,18 +122,14 @@ def main():
     frames = make_frames(B, T, HW, rank, device)
     out = {"wav": torch.empty(B, T * HOP, device=device), "mel_db": torch.empty(B, T, 64, device=device),
            "mel_log": torch.empty(B, T, 64, device=device)}
-    if world > 1:  # C3: clip lengths of every rank (uniform here; the driver sizes the gather with it)
-        lens = torch.full((B,), T, dtype=torch.int64, device=device)
-        all_lens = [torch.empty_like(lens) for _ in range(world)]
-        dist.all_gather(all_lens, lens)
-        gather_wav = [torch.empty_like(out["wav"]) for _ in range(world)] if rank == 0 else None
-        gather_mel = [torch.empty_like(out["mel_db"]) for _ in range(world)] if rank == 0 else None
+    if world > 1:  # C3: clip lengths of every rank (the gather is sized from them)
+        all_lens = dp.all_gather_lengths([T] * B, device)
 
     def step():
         pipe.forward(frames, out=out)
-        if world > 1:  # C2: results to rank 0 over RCCL
-            dist.gather(out["wav"], gather_wav, dst=0)
-            dist.gather(out["mel_db"], gather_mel, dst=0)
+        if world > 1:  # C2: wav + dB mel of every clip to rank 0 over RCCL
+            dp.gather_results(out["wav"], all_lens)
+            dp.gather_results(out["mel_db"], all_lens)
 
     for _ in range(args.warmup):
         step()
@@ -207,7 +180,7 @@ def main():
         stats = _native.prof_collect()
         tot_ms = sum(s["ms"] for s in stats)
         dom = max(stats, key=lambda s: s["ms"])
-        mfma = dom["name"].startswith("conv_igemm")
+        mfma = dom["name"].startswith("conv_")
         if mfma:
             achieved = dom["flops"] / (dom["ms"] * 1e-3) / 1e12
             peak = PEAK_TFLOPS["bf16" if "bf16" in dom["name"] else "fp32"]
@@ -215,8 +188,8 @@ def main():
         else:
             achieved = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9
             peak, unit, bound = PEAK_HBM_GBS, "GB/s", "hbm"
-        conv_ms = sum(s["ms"] for s in stats if s["name"].startswith("conv_igemm"))
-        conv_fl = sum(s["flops"] for s in stats if s["name"].startswith("conv_igemm"))
+        conv_ms = sum(s["ms"] for s in stats if s["name"].startswith("conv_") and "post" not in s["name"])
+        conv_fl = sum(s["flops"] for s in stats if s["name"].startswith("conv_") and "post" not in s["name"])
         result["roofline"] = {
             "bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
             "frac": round(achieved / peak, 4), "traffic": None,

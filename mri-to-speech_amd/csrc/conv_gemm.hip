@@ -1,0 +1,381 @@
+// bf16 implicit-GEMM convolution with an LDS-DMA (global_load_lds) pipeline: the fast path of every
+// bf16 conv.  ConvArgs contract: conv_igemm.hpp (shared with the fp32 parity kernel).
+//
+// Why this shape.  The hot-path GEMMs are short in K (64..1248 = 2..39 steps of 32) and long in M
+// (positions x frames), so per-step load latency, not arithmetic, is what a workgroup waits on.
+// Each workgroup (4 waves) keeps S-1 K-steps of its A (activation) and B (weight) tiles in flight
+// as LDS-DMA transfers - no staging registers - retired by a counted `s_waitcnt vmcnt` and a raw
+// s_barrier (cdna_hip_programming.md §5 "Pipelining across barriers").  A tile row = one output
+// position, gathered per lane (implicit GEMM: the lane's source address is the input position for
+// its tap; padding lanes read a zero page).  LDS rows are 64 B (32 bf16 = one MFMA k-step); the
+// 16-byte chunks are XOR-swizzled on the SOURCE side (chunk p of row r holds logical chunk
+// p ^ ((r >> 2) & 3)) so the ds_read_b128 fragment reads are bank-conflict free (rule 21).
+// LeakyReLU / SE scales are applied to the activation fragments after the LDS read; the SE table
+// of the workgroup's images is staged in LDS once.  Blocks are remapped so that the N tiles of
+// one M tile run on one XCD (shared A rows stay in that XCD's L2).
+#include "conv_igemm.hpp"
+
+#include "prof.hpp"
+
+namespace m2s {
+namespace {
+
+__device__ __attribute__((aligned(16))) uint4 g_zero_page[4];  // padding lanes' DMA source
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void dma16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 lrelu_frag(bf16x8 v, float slope) {
+  uint4 u = __builtin_bit_cast(uint4, v);
+  uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float lo = __uint_as_float(w[j] << 16), hi = __uint_as_float(w[j] & 0xffff0000u);
+    lo = lo > 0.f ? lo : lo * slope;
+    hi = hi > 0.f ? hi : hi * slope;
+    w[j] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  }
+  return __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3]));
+}
+
+// SE scales come from an LDS table.  Read through inline asm (loads + wait in ONE statement,
+// cdna_hip_programming.md §5.7 form (i)): a plain ds_read there makes hipcc assume it may alias
+// the in-flight LDS-DMA and drain the whole pipeline with vmcnt(0) every step.
+__device__ __forceinline__ bf16x8 scale_frag(bf16x8 v, const float* s) {
+  uint4 u = __builtin_bit_cast(uint4, v);
+  uint32_t w[4] = {u.x, u.y, u.z, u.w};
+  float4 s0, s1;
+  const uint32_t addr = (uint32_t)(uintptr_t)s;
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(s0), "=&v"(s1)
+               : "v"(addr)
+               : "memory");
+  const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float lo = __uint_as_float(w[j] << 16) * sc[2 * j];
+    const float hi = __uint_as_float(w[j] & 0xffff0000u) * sc[2 * j + 1];
+    w[j] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  }
+  return __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3]));
+}
+
+__device__ __forceinline__ void ld4f(const bf16_t* p, float* v) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  v[0] = __uint_as_float(u.x << 16);
+  v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16);
+  v[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+
+constexpr int ROW = 64;  // bytes per LDS row = 32 bf16 = one k-step
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * ROW + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+template <int BM, int BN, int MT, int NT, int S, int KIND, int XF>
+__global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a, int n_tiles, int se_imgs) {
+  constexpr int WN = BN / (NT * 16);
+  constexpr int WM = 4 / WN;
+  static_assert(WM * WN == 4 && WM * MT * 16 == BM, "bad tile");
+  constexpr int A_PER_WAVE = BM / 64;              // 16-row DMA blocks per wave for A
+  constexpr int B_BLOCKS = BN / 16;                // 16-row DMA blocks for B
+  constexpr int B_PER_WAVE = (B_BLOCKS + 3) / 4;   // waves >= B_BLOCKS issue into a scratch block
+  constexpr int SLOT = (BM + BN + 16) * ROW;       // +16 rows: scratch for surplus B DMAs
+  constexpr int PER_STAGE = A_PER_WAVE + B_PER_WAVE;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* se_tab = reinterpret_cast<float*>(smem + S * SLOT);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int g = lane >> 4, r16 = lane & 15;
+
+  // XCD-aware block -> (m tile, n tile): the n tiles of one m tile share blockIdx % 8 (one XCD).
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xq = nwg / 8, xr = nwg % 8, xcd = orig % 8;
+  const int wid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + orig / 8;
+  const int mt = wid / n_tiles, nt = wid - (wid / n_tiles) * n_tiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int phase = blockIdx.z;
+
+  const bf16_t* __restrict__ X = static_cast<const bf16_t*>(a.x);
+  const bf16_t* __restrict__ W = static_cast<const bf16_t*>(a.w) + (size_t)phase * a.n_pad * a.kp;
+  const int nsteps = a.kp / 32;
+
+  // ---- DMA roles: lane -> (row within a 16-row block, physical chunk) -------------------------
+  const int lrow = lane >> 2;
+  const int q = (lane & 3) ^ ((lane >> 4) & 3);  // logical chunk this lane fetches ((row>>2)&3 = lane>>4 & 3)
+  int rb[A_PER_WAVE], rp0[A_PER_WAVE], rp1[A_PER_WAVE];
+  bool rok[A_PER_WAVE];
+  const int delta = (KIND == KIND_CONVT) ? (phase + a.ct_pad) / a.ct_u : 0;
+#pragma unroll
+  for (int j = 0; j < A_PER_WAVE; ++j) {
+    const int m = m0 + (wave * A_PER_WAVE + j) * 16 + lrow;
+    rok[j] = m < a.M;
+    const int mm = rok[j] ? m : 0;
+    if constexpr (KIND == KIND_CONV2D) {
+      const int hw = a.OH * a.OW;
+      const int img = mm / hw, rem = mm - (mm / hw) * hw;
+      const int oy = rem / a.OW, ox = rem - (rem / a.OW) * a.OW;
+      rb[j] = img;
+      rp0[j] = oy * a.stride - a.pad_t;
+      rp1[j] = ox * a.stride - a.pad_l;
+    } else if constexpr (KIND == KIND_CONV1D) {
+      rb[j] = mm / a.L_out;
+      rp0[j] = mm - rb[j] * a.L_out - a.pad_left;
+      rp1[j] = 0;
+    } else if constexpr (KIND == KIND_CONVT) {
+      rb[j] = mm / a.L_in;
+      rp0[j] = mm - rb[j] * a.L_in + delta;
+      rp1[j] = 0;
+    } else {
+      rb[j] = 0;
+      rp0[j] = mm;
+      rp1[j] = 0;
+    }
+  }
+  int s_tap = (q * 8) / a.cs_in, s_c = (q * 8) % a.cs_in;
+  const bf16_t* bsrc[B_PER_WAVE];
+#pragma unroll
+  for (int j = 0; j < B_PER_WAVE; ++j) {
+    const int blk = wave * B_PER_WAVE + j;
+    const int n = n0 + blk * 16 + lrow;
+    bsrc[j] = (blk < B_BLOCKS && n < a.n_pad) ? W + (size_t)n * a.kp + q * 8 : nullptr;
+  }
+
+  auto issue = [&](int st, int slot) {
+    char* As = smem + slot * SLOT;
+    char* Bs = As + BM * ROW;
+#pragma unroll
+    for (int j = 0; j < A_PER_WAVE; ++j) {
+      const void* src = g_zero_page;
+      if (rok[j] && s_tap < a.ntaps) {
+        long off = -1;
+        if constexpr (KIND == KIND_CONV2D) {
+          const int ky = s_tap / 3, kx = s_tap - (s_tap / 3) * 3;
+          const int iy = rp0[j] + ky, ix = rp1[j] + kx;
+          if (iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW) off = ((long)(rb[j] * a.IH + iy) * a.IW + ix) * a.cs_in;
+        } else if constexpr (KIND == KIND_CONV1D) {
+          const int it = rp0[j] + s_tap * a.dil;
+          if (it >= 0 && it < a.L_in) off = ((long)rb[j] * a.L_in + it) * a.cs_in;
+        } else if constexpr (KIND == KIND_CONVT) {
+          const int it = rp0[j] - s_tap;
+          if (it >= 0 && it < a.L_in) off = ((long)rb[j] * a.L_in + it) * a.cs_in;
+        } else {
+          off = (long)rp0[j] * a.cs_in;
+        }
+        if (off >= 0) src = X + off + s_c;
+      }
+      dma16(src, As + (wave * A_PER_WAVE + j) * 16 * ROW);
+    }
+#pragma unroll
+    for (int j = 0; j < B_PER_WAVE; ++j) {
+      const int blk = wave * B_PER_WAVE + j;
+      const void* src = bsrc[j] ? (const void*)(bsrc[j] + st * 32) : (const void*)g_zero_page;
+      dma16(src, blk < B_BLOCKS ? Bs + blk * 16 * ROW : As + (BM + BN) * ROW);
+    }
+    s_c += 32;
+    while (s_c >= a.cs_in) {
+      s_c -= a.cs_in;
+      ++s_tap;
+    }
+  };
+
+  // ---- SE scale table for this workgroup's images (GEMM kind only) ---------------------------
+  int img0 = 0;
+  if constexpr (XF == IN_SE_SCALE) {
+    img0 = m0 / a.OH;
+    for (int i = tid; i < se_imgs * a.cs_in; i += 256) {
+      const int im = i / a.cs_in, c = i - (i / a.cs_in) * a.cs_in;
+      se_tab[i] = (img0 + im) * a.OH < a.M ? a.in_scale[(size_t)(img0 + im) * a.cs_in + c] : 0.f;
+    }
+  }
+  int frow_img[MT];
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi) {
+    const int m = m0 + wm * MT * 16 + mi * 16 + r16;
+    frow_img[mi] = XF == IN_SE_SCALE ? (m < a.M ? m / a.OH : img0) - img0 : 0;
+  }
+
+  f32x4 acc[NT][MT];
+#pragma unroll
+  for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) acc[ni][mi] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nsteps) issue(s, s);
+
+  for (int st = 0; st < nsteps; ++st) {
+    // stage st has landed once at most min(S-2, nsteps-1-st) younger stages are outstanding
+    const int younger = min(S - 2, nsteps - 1 - st);
+    if (younger >= 2)
+      wait_vm<2 * PER_STAGE>();
+    else if (younger == 1)
+      wait_vm<PER_STAGE>();
+    else
+      wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for `st` landed; slot (st-1)%S is free
+    if (st + S - 1 < nsteps) issue(st + S - 1, (st + S - 1) % S);
+
+    const char* As = smem + (st % S) * SLOT;
+    const char* Bs = As + BM * ROW;
+    bf16x8 af[NT], bx[MT];
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni)
+      af[ni] = *reinterpret_cast<const bf16x8*>(Bs + swz(wn * NT * 16 + ni * 16 + r16, g));
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+      bx[mi] = *reinterpret_cast<const bf16x8*>(As + swz(wm * MT * 16 + mi * 16 + r16, g));
+    if constexpr (XF == IN_LRELU) {
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) bx[mi] = lrelu_frag(bx[mi], a.in_slope);
+    } else if constexpr (XF == IN_SE_SCALE) {
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) bx[mi] = scale_frag(bx[mi], se_tab + frow_img[mi] * a.cs_in + st * 32 + g * 8);
+    }
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+        acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ni], bx[mi], acc[ni][mi], 0, 0, 0);
+  }
+
+  // ---- epilogue: 4 consecutive channels of one position per lane ------------------------------
+  bf16_t* __restrict__ Y = static_cast<bf16_t*>(a.y);
+  const bf16_t* __restrict__ R = static_cast<const bf16_t*>(a.res);
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi) {
+    const int m = m0 + wm * MT * 16 + mi * 16 + r16;
+    if (m >= a.M) continue;
+    long orow;
+    if constexpr (KIND == KIND_CONVT) {
+      const int b = m / a.L_in, qq = m - (m / a.L_in) * a.L_in;
+      orow = ((long)b * a.L_out + (long)qq * a.ct_u + phase) * a.cs_out;
+    } else {
+      orow = (long)m * a.cs_out;
+    }
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni) {
+      const int n4 = n0 + wn * NT * 16 + ni * 16 + 4 * g;
+      if (n4 >= a.cs_out) continue;
+      const float4 bb = *reinterpret_cast<const float4*>(a.bias + n4);
+      float v[4] = {acc[ni][mi][0] + bb.x, acc[ni][mi][1] + bb.y, acc[ni][mi][2] + bb.z, acc[ni][mi][3] + bb.w};
+      if (a.act == ACT_SILU) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = silu(v[j]);
+      } else if (a.act == ACT_LRELU) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * a.act_slope;
+      }
+      if (R) {
+        float r[4];
+        ld4f(R + orow + n4, r);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += r[j];
+      }
+      if (a.accum) {
+        float p[4];
+        ld4f(Y + orow + n4, p);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = p[j] + v[j];
+        if (a.accum == 2) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = v[j] / a.accum_div;
+        }
+      }
+      uint2 u;
+      u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(Y + orow + n4) = u;
+    }
+  }
+}
+
+const char* kname(int k) {
+  switch (k) {
+    case KIND_CONV2D: return "conv2d";
+    case KIND_CONV1D: return "conv1d";
+    case KIND_CONVT: return "convT";
+    default: return "gemm";
+  }
+}
+
+template <int BM, int BN, int MT, int NT, int KIND, int XF>
+void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
+  constexpr int S = BM >= 256 ? 3 : 4;  // keep two workgroups' LDS per CU
+  static bool attr = [] {
+    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    return true;
+  }();
+  (void)attr;
+  const int m_tiles = ceil_div(a.M, BM), n_tiles = ceil_div(a.cs_out, BN);
+  int se_imgs = 0;
+  if (a.in_xform == IN_SE_SCALE) {
+    M2S_CHECK(KIND == KIND_GEMM && a.OH > 0, "SE scale needs the GEMM kind with OH = rows per image");
+    se_imgs = (BM + a.OH - 1) / a.OH + 1;
+  }
+  const size_t lds = (size_t)S * (BM + BN + 16) * ROW + (size_t)se_imgs * a.cs_in * sizeof(float);
+  M2S_CHECK(lds <= 160 * 1024, "conv_gemm: LDS budget");
+  dim3 grid(m_tiles * n_tiles, 1, phases);
+  char name[96];
+  snprintf(name, sizeof(name), "conv_gemm<bf16,%s,%dx%d>", kname(KIND), BM, BN);
+  ProfScope ps(name, flops, bytes, s);
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF>), grid, dim3(256), lds, s, a, n_tiles, se_imgs);
+}
+
+template <int KIND, int XF>
+void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
+  const int n = a.cs_out;
+  if (n <= 16)
+    launch_tile<256, 16, 4, 1, KIND, XF>(a, s, phases, flops, bytes);
+  else if (n <= 32)
+    launch_tile<256, 32, 4, 2, KIND, XF>(a, s, phases, flops, bytes);
+  else if (n <= 64 || (n % 128 != 0 && ceil_div(n, 64) * 64 < ceil_div(n, 128) * 128))
+    launch_tile<256, 64, 4, 4, KIND, XF>(a, s, phases, flops, bytes);
+  else
+    launch_tile<128, 128, 4, 4, KIND, XF>(a, s, phases, flops, bytes);
+}
+
+// Only the (kind, input transform) pairs the hot path uses are instantiated.
+template <int KIND>
+void launch_kind(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
+  if (a.in_xform == IN_NONE) {
+    launch_kind_xf<KIND, IN_NONE>(a, s, phases, flops, bytes);
+  } else if constexpr (KIND == KIND_CONV1D || KIND == KIND_CONVT) {
+    M2S_CHECK(a.in_xform == IN_LRELU, "conv_gemm: 1-D kinds take LeakyReLU inputs only");
+    launch_kind_xf<KIND, IN_LRELU>(a, s, phases, flops, bytes);
+  } else if constexpr (KIND == KIND_GEMM) {
+    M2S_CHECK(a.in_xform == IN_SE_SCALE, "conv_gemm: GEMM kind takes SE-scaled inputs only");
+    launch_kind_xf<KIND, IN_SE_SCALE>(a, s, phases, flops, bytes);
+  } else {
+    M2S_CHECK(false, "conv_gemm: 2-D convs take untransformed inputs");
+  }
+}
+
+}  // namespace
+
+void launch_conv_bf16_fast(const ConvArgs& a, hipStream_t s, double flops, double bytes) {
+  M2S_CHECK(a.cs_in % 8 == 0 && a.cs_out % 4 == 0, "conv_gemm: channel strides");
+  M2S_CHECK(a.kp % 32 == 0 && a.kp >= a.ntaps * a.cs_in, "conv_gemm: kp");
+  M2S_CHECK(a.kind != KIND_CONV2D || a.ks == 3, "conv_gemm: 2-D kernels are 3x3 (1x1 runs as GEMM)");
+  if (a.M <= 0) return;
+  switch (a.kind) {
+    case KIND_CONV2D: launch_kind<KIND_CONV2D>(a, s, 1, flops, bytes); break;
+    case KIND_CONV1D: launch_kind<KIND_CONV1D>(a, s, 1, flops, bytes); break;
+    case KIND_CONVT: launch_kind<KIND_CONVT>(a, s, a.ct_u, flops, bytes); break;
+    case KIND_GEMM: launch_kind<KIND_GEMM>(a, s, 1, flops, bytes); break;
+    default: M2S_CHECK(false, "conv_gemm: bad kind");
+  }
+  M2S_HIP(hipGetLastError());
+}
+
+}  // namespace m2s

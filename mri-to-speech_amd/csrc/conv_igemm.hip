@@ -279,6 +279,16 @@ void launch_kind(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
 
 template <typename T>
 void launch_conv(const ConvArgs& a, hipStream_t s, double flops, double bytes) {
+  if constexpr (sizeof(T) == 2) {
+    static const bool v1 = [] {
+      const char* e = getenv("M2S_CONV_IMPL");
+      return e && std::string(e) == "v1";
+    }();
+    if (!v1 && (a.kind != KIND_CONV2D || a.ks == 3)) {
+      launch_conv_bf16_fast(a, s, flops, bytes);
+      return;
+    }
+  }
   constexpr int KC = Elem<T>::KC;
   M2S_CHECK(a.cs_in % KC == 0 || KC % a.cs_in == 0, "conv: cs_in incompatible with K chunk");
   M2S_CHECK(a.cs_out % 4 == 0, "conv: cs_out must be a multiple of 4");

@@ -50,8 +50,11 @@ struct ConvArgs {
 };
 
 // flops / bytes: algorithmic work of this launch, recorded by the profiler (m2s_prof_*).
+// bf16 runs the LDS-DMA pipelined kernel (conv_gemm.hip) unless M2S_CONV_IMPL=v1; fp32 (the
+// parity path) runs the direct-load kernel of conv_igemm.hip.
 template <typename T>
 void launch_conv(const ConvArgs& a, hipStream_t s, double flops = 0.0, double bytes = 0.0);
+void launch_conv_bf16_fast(const ConvArgs& a, hipStream_t s, double flops, double bytes);
 
 // Host-side helpers shared by the packers.
 inline int conv_tpc(int cs_in, int kc) { return cs_in < kc ? kc / cs_in : 1; }
