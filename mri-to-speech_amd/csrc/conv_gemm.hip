@@ -193,7 +193,9 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a, int n_
     img0 = m0 / a.OH;
     for (int i = tid; i < se_imgs * a.cs_in; i += 256) {
       const int im = i / a.cs_in, c = i - (i / a.cs_in) * a.cs_in;
-      se_tab[i] = (img0 + im) * a.OH < a.M ? a.in_scale[(size_t)(img0 + im) * a.cs_in + c] : 0.f;
+      se_tab[i] = (img0 + im) * a.OH < a.M
+                      ? bf2f(static_cast<const bf16_t*>(a.in_scale)[(size_t)(img0 + im) * a.cs_in + c])
+                      : 0.f;
     }
   }
   int frow_img[MT];
@@ -274,6 +276,9 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a, int n_
       } else if (a.act == ACT_LRELU) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * a.act_slope;
+      } else if (a.act == ACT_SIGMOID) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = sigmoidf_(v[j]);
       }
       if (R) {
         float r[4];
@@ -327,7 +332,11 @@ void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
   M2S_CHECK(lds <= 160 * 1024, "conv_gemm: LDS budget");
   dim3 grid(m_tiles * n_tiles, 1, phases);
   char name[96];
-  snprintf(name, sizeof(name), "conv_gemm<bf16,%s,%dx%d>", kname(KIND), BM, BN);
+  static const bool detail = getenv("M2S_PROF_DETAIL") != nullptr;
+  if (detail)  // per-layer records for analysis: K x N and rows per launch
+    snprintf(name, sizeof(name), "conv_gemm<%s,%dx%d> K%d N%d M%d", kname(KIND), BM, BN, a.kp, a.cs_out, a.M);
+  else
+    snprintf(name, sizeof(name), "conv_gemm<bf16,%s,%dx%d>", kname(KIND), BM, BN);
   ProfScope ps(name, flops, bytes, s);
   hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF>), grid, dim3(256), lds, s, a, n_tiles, se_imgs);
 }

@@ -30,18 +30,17 @@ __device__ __forceinline__ void xform_lrelu(uint4& v, float slope) {
 }
 
 template <typename T>
-__device__ __forceinline__ void xform_scale(uint4& v, const float* __restrict__ s) {
+__device__ __forceinline__ void xform_scale(uint4& v, const T* __restrict__ s) {
   if constexpr (sizeof(T) == 4) {
     float* f = reinterpret_cast<float*>(&v);
     const float4 sc = *reinterpret_cast<const float4*>(s);
     f[0] *= sc.x; f[1] *= sc.y; f[2] *= sc.z; f[3] *= sc.w;
   } else {
     bf16_t* h = reinterpret_cast<bf16_t*>(&v);
-    const float4 s0 = *reinterpret_cast<const float4*>(s);
-    const float4 s1 = *reinterpret_cast<const float4*>(s + 4);
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const uint4 su = *reinterpret_cast<const uint4*>(s);
+    const bf16_t* sc = reinterpret_cast<const bf16_t*>(&su);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) h[e] = f2bf(bf2f(h[e]) * sc[e]);
+    for (int e = 0; e < 8; ++e) h[e] = f2bf(bf2f(h[e]) * bf2f(sc[e]));
   }
 }
 
@@ -62,6 +61,7 @@ template <typename T>
 __device__ __forceinline__ float act_apply(float v, int act, float slope) {
   if (act == ACT_SILU) return sizeof(T) == 4 ? silu_exact(v) : silu(v);
   if (act == ACT_LRELU) return v > 0.f ? v : v * slope;
+  if (act == ACT_SIGMOID) return sizeof(T) == 4 ? sigmoid_exact(v) : sigmoidf_(v);
   return v;
 }
 
@@ -196,7 +196,8 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
       } else if (a.in_xform == IN_SE_SCALE) {
 #pragma unroll
         for (int mi = 0; mi < MT; ++mi)
-          if (xo[mi] >= 0) xform_scale<T>(bx[mi], a.in_scale + (size_t)img_row[mi] * a.cs_in + c_off + cc * KC);
+          if (xo[mi] >= 0)
+            xform_scale<T>(bx[mi], static_cast<const T*>(a.in_scale) + (size_t)img_row[mi] * a.cs_in + c_off + cc * KC);
       }
 #pragma unroll
       for (int ni = 0; ni < NT; ++ni)

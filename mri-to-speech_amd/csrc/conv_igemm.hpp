@@ -20,7 +20,7 @@
 namespace m2s {
 
 enum ConvKind { KIND_CONV2D = 0, KIND_CONV1D = 1, KIND_CONVT = 2, KIND_GEMM = 3 };
-enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_LRELU = 2 };
+enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_LRELU = 2, ACT_SIGMOID = 3 };
 enum InXform { IN_NONE = 0, IN_LRELU = 1, IN_SE_SCALE = 2 };
 
 struct ConvArgs {
@@ -29,7 +29,7 @@ struct ConvArgs {
   const float* bias;    // [n_pad] fp32 (zero padded)
   const void* res;      // residual, same layout as y (or null)
   void* y;              // output, channel-last, channel stride cs_out
-  const float* in_scale;// IN_SE_SCALE: [img][cs_in] fp32
+  const void* in_scale; // IN_SE_SCALE: [img][cs_in] in the compute dtype (SE gates)
   int kind;
   int M;                // GEMM rows (output positions per phase)
   int cs_in, cs_out;    // channel strides

@@ -76,219 +76,6 @@ __global__ void __launch_bounds__(256) stem_kernel(const float* __restrict__ fra
 }
 
 // ---------------------------------------------------------------------------------------------
-// depthwise 3x3 + bias + SiLU + SE squeeze.  grid (ceil(cs/512), N, ceil(OH/4)); a thread owns
-// 8 channels (one 16-byte vector) of ONE output row and slides a 3x3 window along it, so each
-// input vector is loaded once per row it feeds (3 loads per output at stride 1 instead of 9).
-// SE partial sums: the 4 rows of a workgroup are added in a fixed order and written per row
-// group (psum[n][row_group][cs]); se_fc adds the groups in order (deterministic).
-template <typename T>
-__device__ __forceinline__ void ld8(const T* p, float* v) {
-  if constexpr (sizeof(T) == 4) {
-    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-  } else {
-    const uint4 u = *reinterpret_cast<const uint4*>(p);
-    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      v[2 * j] = __uint_as_float(w[j] << 16);
-      v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
-    }
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ void st8(T* p, const float* v) {
-  if constexpr (sizeof(T) == 4) {
-    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
-  } else {
-    uint4 u;
-    u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-    u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-    u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-    *reinterpret_cast<uint4*>(p) = u;
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ void dw_col(const T* xn, int iy0, int ix, int IH, int IW, int cs, float (&c)[3][8]) {
-#pragma unroll
-  for (int ky = 0; ky < 3; ++ky) {
-    const int iy = iy0 + ky;
-    if (iy >= 0 && iy < IH && ix >= 0 && ix < IW) {
-      ld8<T>(xn + ((long)iy * IW + ix) * cs, c[ky]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) c[ky][j] = 0.f;
-    }
-  }
-}
-
-template <typename T, int S>
-__global__ void __launch_bounds__(256) dwconv_kernel(const T* __restrict__ x, int IH, int IW, int OH, int OW,
-                                                     int pad_t, int pad_l, int cs, const float* __restrict__ w9,
-                                                     const float* __restrict__ bias, T* __restrict__ y,
-                                                     float* __restrict__ sums) {
-  __shared__ float red[4][512];
-  const int n = blockIdx.y;
-  const int cg = threadIdx.x & 63, rl = threadIdx.x >> 6;
-  const int c0 = blockIdx.x * 512 + cg * 8;
-  const int oy = blockIdx.z * 4 + rl;
-  const bool active = c0 < cs && oy < OH;
-  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (active) {
-    float w[9][8], b[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int t = 0; t < 9; ++t) w[t][j] = w9[(c0 + j) * 9 + t];
-      b[j] = bias[c0 + j];
-    }
-    const T* xn = x + (long)n * IH * IW * cs + c0;
-    T* yn = y + (long)n * OH * OW * cs + c0;
-    {
-      const int iy0 = oy * S - pad_t;
-      float c0w[3][8], c1w[3][8], c2w[3][8];
-      dw_col<T>(xn, iy0, -pad_l, IH, IW, cs, c0w);
-      dw_col<T>(xn, iy0, -pad_l + 1, IH, IW, cs, c1w);
-      dw_col<T>(xn, iy0, -pad_l + 2, IH, IW, cs, c2w);
-      for (int ox = 0; ox < OW; ++ox) {
-        float acc[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float a = b[j];
-#pragma unroll
-          for (int ky = 0; ky < 3; ++ky) {
-            a += w[ky * 3 + 0][j] * c0w[ky][j];
-            a += w[ky * 3 + 1][j] * c1w[ky][j];
-            a += w[ky * 3 + 2][j] * c2w[ky][j];
-          }
-          a = act_silu<T>(a);
-          s[j] += a;
-          acc[j] = a;
-        }
-        st8<T>(yn + ((long)oy * OW + ox) * cs, acc);
-        const int ixn = (ox + 1) * S - pad_l;  // first input column of the next output
-        if (S == 1) {
-#pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              c0w[ky][j] = c1w[ky][j];
-              c1w[ky][j] = c2w[ky][j];
-            }
-          dw_col<T>(xn, iy0, ixn + 2, IH, IW, cs, c2w);
-        } else {
-#pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) c0w[ky][j] = c2w[ky][j];
-          dw_col<T>(xn, iy0, ixn + 1, IH, IW, cs, c1w);
-          dw_col<T>(xn, iy0, ixn + 2, IH, IW, cs, c2w);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) red[rl][cg * 8 + j] = s[j];
-  __syncthreads();
-  if (rl == 0 && c0 < cs) {
-    float* ps = sums + ((long)n * gridDim.z + blockIdx.z) * cs + c0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = cg * 8 + j;
-      ps[j] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// SE excitation for SE_G images per workgroup.  psum [n][nrg][cs] (row-group partial sums of
-// the depthwise output), w1 [rd][C] (conv_reduce), w2t [rd][C] (conv_expand transposed so
-// consecutive threads read consecutive c).  Each wave reduces SE_R rows of w1 per pass with
-// independent loads in flight (the loop is latency-, not bandwidth-bound).
-constexpr int SE_G = 2, SE_R = 8;
-__global__ void __launch_bounds__(256) se_fc_kernel(const float* __restrict__ psum, int nrg, int N, int C, int cs,
-                                                    int rd, float inv_count, const float* __restrict__ w1,
-                                                    const float* __restrict__ b1, const float* __restrict__ w2t,
-                                                    const float* __restrict__ b2, float* __restrict__ scale,
-                                                    int exact) {
-  __shared__ float m[SE_G][1280];
-  __shared__ float z[SE_G][128];
-  const int n0 = blockIdx.x * SE_G;
-  for (int i = threadIdx.x; i < SE_G * C; i += 256) {
-    const int g = i / C, c = i - (i / C) * C;
-    float acc = 0.f;
-    if (n0 + g < N)
-      for (int q = 0; q < nrg; ++q) acc += psum[((long)(n0 + g) * nrg + q) * cs + c];
-    m[g][c] = acc * inv_count;
-  }
-  __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int r0 = wave * SE_R; r0 < rd; r0 += 4 * SE_R) {
-    float acc[SE_R][SE_G];
-#pragma unroll
-    for (int q = 0; q < SE_R; ++q)
-#pragma unroll
-      for (int g = 0; g < SE_G; ++g) acc[q][g] = 0.f;
-#pragma unroll 4
-    for (int c = lane; c < C; c += 64) {
-      float mv[SE_G];
-#pragma unroll
-      for (int g = 0; g < SE_G; ++g) mv[g] = m[g][c];
-#pragma unroll
-      for (int q = 0; q < SE_R; ++q) {
-        const float wv = r0 + q < rd ? w1[(long)(r0 + q) * C + c] : 0.f;
-#pragma unroll
-        for (int g = 0; g < SE_G; ++g) acc[q][g] += wv * mv[g];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < SE_R; ++q)
-#pragma unroll
-      for (int g = 0; g < SE_G; ++g) {
-        float a = acc[q][g];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
-        acc[q][g] = a;
-      }
-    if (lane == 0) {
-#pragma unroll
-      for (int q = 0; q < SE_R; ++q) {
-        if (r0 + q >= rd) break;
-#pragma unroll
-        for (int g = 0; g < SE_G; ++g) {
-          const float v = acc[q][g] + b1[r0 + q];
-          z[g][r0 + q] = exact ? silu_exact(v) : silu(v);
-        }
-      }
-    }
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < cs; c += 256) {
-    float acc[SE_G];
-    const float bb = c < C ? b2[c] : 0.f;
-#pragma unroll
-    for (int g = 0; g < SE_G; ++g) acc[g] = bb;
-    if (c < C) {
-#pragma unroll 8
-      for (int r = 0; r < rd; ++r) {
-        const float wv = w2t[(long)r * C + c];
-#pragma unroll
-        for (int g = 0; g < SE_G; ++g) acc[g] += wv * z[g][r];
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < SE_G; ++g) {
-      if (n0 + g >= N) break;
-      scale[(long)(n0 + g) * cs + c] = c < C ? (exact ? sigmoid_exact(acc[g]) : sigmoidf_(acc[g])) : 0.f;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 template <typename T>
 __global__ void __launch_bounds__(256) gap_kernel(const T* __restrict__ x, int N, int P, int C, int cs,
                                                   float* __restrict__ feats) {
@@ -476,30 +263,6 @@ void launch_stem(const float* frames, int N, int H, int W, int OH, int OW, int p
 }
 
 template <typename T>
-void launch_dwconv(const T* x, int N, int IH, int IW, int OH, int OW, int stride, int pad_t, int pad_l, int C, int cs,
-                   const float* w9, const float* bias, T* y, float* sums, hipStream_t s) {
-  (void)C;
-  M2S_CHECK(cs % 8 == 0, "dwconv: cs % 8");
-  M2S_CHECK(stride == 1 || stride == 2, "dwconv: stride");
-  const dim3 grid(ceil_div(cs, 512), N, dw_row_groups(OH));
-  if (stride == 1)
-    hipLaunchKernelGGL((dwconv_kernel<T, 1>), grid, dim3(256), 0, s, x, IH, IW, OH, OW, pad_t, pad_l, cs, w9, bias, y,
-                       sums);
-  else
-    hipLaunchKernelGGL((dwconv_kernel<T, 2>), grid, dim3(256), 0, s, x, IH, IW, OH, OW, pad_t, pad_l, cs, w9, bias, y,
-                       sums);
-  M2S_HIP(hipGetLastError());
-}
-
-void launch_se_fc(const float* sums, int nrg, int N, int C, int cs, int rd, float inv_count, const float* w1,
-                  const float* b1, const float* w2, const float* b2, float* scale, bool exact, hipStream_t s) {
-  M2S_CHECK(C <= 1280 && rd <= 128, "se: too many channels");
-  hipLaunchKernelGGL(se_fc_kernel, dim3(ceil_div(N, SE_G)), dim3(256), 0, s, sums, nrg, N, C, cs, rd, inv_count, w1,
-                     b1, w2, b2, scale, exact ? 1 : 0);
-  M2S_HIP(hipGetLastError());
-}
-
-template <typename T>
 void launch_gap(const T* x, int N, int P, int C, int cs, float* feats, hipStream_t s) {
   hipLaunchKernelGGL(gap_kernel<T>, dim3(nblk((long)N * C)), dim3(256), 0, s, x, N, P, C, cs, feats);
   M2S_HIP(hipGetLastError());
@@ -546,8 +309,6 @@ void launch_conv_post(const T* x, int B, int L, int C, int cs, const float* w, f
 #define M2S_INST(T)                                                                                                  \
   template void launch_stem<T>(const float*, int, int, int, int, int, int, int, const float*, const float*, int, int, \
                                T*, hipStream_t);                                                                     \
-  template void launch_dwconv<T>(const T*, int, int, int, int, int, int, int, int, int, int, const float*,           \
-                                 const float*, T*, float*, hipStream_t);                                             \
   template void launch_gap<T>(const T*, int, int, int, int, float*, hipStream_t);                                    \
   template void launch_mel_glue<T>(const float*, int, int, const float*, const float*, float*, float*, T*, int,      \
                                    hipStream_t);                                                                     \

@@ -11,18 +11,18 @@ template <typename T>
 void launch_stem(const float* frames, int N, int H, int W, int OH, int OW, int pad_t, int pad_l,
                  const float* w9, const float* bias, int cout, int cs_out, T* y, hipStream_t s);
 
-// conv_dw (3x3 depthwise, stride 1/2, TF-SAME) + bn2 + SiLU, plus per-(image, row group, channel)
+// conv_dw (3x3 depthwise, stride 1/2, TF-SAME) + bn2 + SiLU, plus per-(image, pixel block, channel)
 // partial sums of the output (SE squeeze).  x (N,IH,IW,cs) -> y (N,OH,OW,cs),
-// sums (N, dw_row_groups(OH), cs) fp32.
-inline int dw_row_groups(int OH) { return (OH + 3) / 4; }
+// sums (N, dw_pixel_blocks(OH, OW), cs) fp32.  (dwse.hip)
+int dw_pixel_blocks(int OH, int OW);
 template <typename T>
 void launch_dwconv(const T* x, int N, int IH, int IW, int OH, int OW, int stride, int pad_t, int pad_l,
                    int C, int cs, const float* w9, const float* bias, T* y, float* sums, hipStream_t s);
 
-// SE excitation: mean -> conv_reduce -> SiLU -> conv_expand -> sigmoid.  sums (N,cs) -> scale (N,cs).
-// w1 = conv_reduce [rd][C], w2 = conv_expand TRANSPOSED [rd][C].
-void launch_se_fc(const float* sums, int nrg, int N, int C, int cs, int rd, float inv_count, const float* w1,
-                  const float* b1, const float* w2, const float* b2, float* scale, bool exact, hipStream_t s);
+// SE squeeze: mean (N, cs) in the compute dtype from the depthwise partial sums (N, npb, cs).
+// (The excitation conv_reduce -> SiLU -> conv_expand -> sigmoid then runs as two MFMA GEMMs.)
+template <typename T>
+void launch_se_mean(const float* psum, int N, int npb, int cs, float inv_count, T* mean, hipStream_t s);
 
 // Global average pool: x (N,P,cs) T -> feats (N,C) fp32 (dense, row stride C).
 template <typename T>

@@ -54,8 +54,9 @@ template <> struct Elem<bf16_t> {
   __device__ static __forceinline__ bf16_t from_f(float v) { return f2bf(v); }
 };
 
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// bf16-path activations: v_exp_f32 + v_rcp_f32 (1 ulp) instead of an IEEE divide sequence.
+__device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
 // Exact-libm variants used by the fp32 parity path (the reference runs fp32 libm on CPU).
 __device__ __forceinline__ float silu_exact(float x) { return x / (1.0f + expf(-x)); }

@@ -159,6 +159,7 @@ static void same_pad(int in, int k, int s, int* out, int* pad) {
 // ------------------------------------------------------------------------------------------
 // Acoustic model
 static const int EFF_STEM = 32, EFF_OUT = 208;
+static const int SE_RD_MAX = 64;  // SE reduce width of tf_efficientnetv2_b2 is <= 52 (chan_stride <= 64)
 struct StageDef {
   int type, reps, k, stride, exp, cout;
   float se;
@@ -246,7 +247,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
         BN bn2 = fold_bn(sd, q + "bn2", m);
         std::vector<float> w9((size_t)cs * 9, 0.f), bd(cs, 0.f);
         for (int c = 0; c < m; ++c) {
-          for (int t = 0; t < 9; ++t) w9[(size_t)c * 9 + t] = wd[(size_t)c * 9 + t] * bn2.a[c];
+          for (int t = 0; t < 9; ++t) w9[(size_t)t * cs + c] = wd[(size_t)c * 9 + t] * bn2.a[c];  // tap-major
           bd[c] = bn2.b[c];
         }
         b.dw_w = arena_.add_vec(w9);
@@ -255,13 +256,16 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
         const float* b1 = need(sd, q + "se.conv_reduce.bias", {b.rd}).data;
         const float* w2 = need(sd, q + "se.conv_expand.weight", {m, b.rd, 1, 1}).data;
         const float* b2 = need(sd, q + "se.conv_expand.bias", {m}).data;
-        b.se_w1 = arena_.add(w1, sizeof(float) * b.rd * m);
-        b.se_b1 = arena_.add(b1, sizeof(float) * b.rd);
-        std::vector<float> w2t((size_t)b.rd * m);  // [rd][mid]: coalesced over channels
-        for (int c = 0; c < m; ++c)
-          for (int r = 0; r < b.rd; ++r) w2t[(size_t)r * m + c] = w2[(size_t)c * b.rd + r];
-        b.se_w2 = arena_.add_vec(w2t);
-        b.se_b2 = arena_.add(b2, sizeof(float) * m);
+        // SE excitation as two GEMMs over all images: (N x mid) . W1^T -> SiLU -> . W2^T -> sigmoid
+        const int rd = b.rd;
+        b.se1 = make_pconv(KIND_GEMM, m, rd, 1, dtype);
+        b.se1.macs_per_row = (double)m * rd;
+        pack_conv(arena_, dtype, b.se1, [&](int, int n, int, int c) { return w1[(size_t)n * m + c]; },
+                  [&](int n) { return b1[n]; });
+        b.se2 = make_pconv(KIND_GEMM, rd, m, 1, dtype);
+        b.se2.macs_per_row = (double)m * rd;
+        pack_conv(arena_, dtype, b.se2, [&](int, int n, int, int c) { return w2[(size_t)n * rd + c]; },
+                  [&](int n) { return b2[n]; });
         conv1x1(b.c2, q + "conv_pwl.weight", m, b.cout, fold_bn(sd, q + "bn3", b.cout));
       }
       blocks_.push_back(b);
@@ -302,6 +306,10 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   for (auto& b : blocks_) {
     b.c1.resolve(arena_);
     if (b.type != 0) b.c2.resolve(arena_);
+    if (b.type == 2) {
+      b.se1.resolve(arena_);
+      b.se2.resolve(arena_);
+    }
   }
   lstm_ih_.resolve(arena_);
 }
@@ -318,7 +326,7 @@ void Acoustic::effnet_dims(int H, int W, size_t* io, size_t* mid, size_t* se) co
     if (b.type == 1) mmid = std::max(mmid, (size_t)nh * nw * chan_stride(b.mid));
     if (b.type == 2) {
       mmid = std::max(mmid, (size_t)oh * ow * chan_stride(b.mid));
-      mse = std::max(mse, (size_t)dw_row_groups(nh) * chan_stride(b.mid));
+      mse = std::max(mse, (size_t)dw_pixel_blocks(nh, nw) * chan_stride(b.mid));
     }
     mio = std::max(mio, (size_t)nh * nw * chan_stride(b.cout));
     oh = nh;
@@ -340,7 +348,9 @@ size_t Acoustic::effnet_ws(int N, int H, int W) const {
   ws.take<char>(nc * mid * es);
   ws.take<char>(nc * mid * es);
   ws.take<float>(nc * se);
-  ws.take<float>(nc * max_mid_cs_);
+  ws.take<char>(nc * max_mid_cs_ * es);   // SE means
+  ws.take<char>(nc * SE_RD_MAX * es);     // SE hidden (rd <= 64)
+  ws.take<char>(nc * max_mid_cs_ * es);   // SE gates
   return ws.used();
 }
 
@@ -375,8 +385,9 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
   T* M = ws.take<T>((size_t)nc_max * mid);
   T* M2 = ws.take<T>((size_t)nc_max * mid);
   float* sums = ws.take<float>((size_t)nc_max * se);
-  float* scale = ws.take<float>((size_t)nc_max * max_mid_cs_);
-  const bool exact = sizeof(T) == 4;
+  T* se_mean = ws.take<T>((size_t)nc_max * max_mid_cs_);
+  T* se_hid = ws.take<T>((size_t)nc_max * SE_RD_MAX);
+  T* scale = ws.take<T>((size_t)nc_max * max_mid_cs_);
 
   for (int n0 = 0; n0 < N; n0 += nc_max) {
     const int nc = std::min(nc_max, N - n0);
@@ -456,11 +467,21 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                            M2, sums, s);
         }
         {
-          ProfScope ps("se_fc", 4.0 * nc * b.mid * b.rd, 8.0 * nc * b.mid, s);
-          launch_se_fc(sums, dw_row_groups(nh), nc, b.mid, cs, b.rd, 1.0f / (float)(nh * nw), static_cast<const float*>(arena_.ptr(b.se_w1)),
-                       static_cast<const float*>(arena_.ptr(b.se_b1)), static_cast<const float*>(arena_.ptr(b.se_w2)),
-                       static_cast<const float*>(arena_.ptr(b.se_b2)), scale, exact, s);
+          ProfScope ps("se_mean", 0.0, 4.0 * nc * cs * dw_pixel_blocks(nh, nw) + sizeof(T) * (double)nc * cs, s);
+          launch_se_mean<T>(sums, nc, dw_pixel_blocks(nh, nw), cs, 1.0f / (float)(nh * nw), se_mean, s);
         }
+        ConvArgs r1 = conv_args(b.se1);  // conv_reduce + SiLU, all images of the chunk at once
+        r1.x = se_mean;
+        r1.y = se_hid;
+        r1.M = nc;
+        r1.act = ACT_SILU;
+        run_conv<T>(r1, b.se1, s);
+        ConvArgs r2 = conv_args(b.se2);  // conv_expand + sigmoid -> per-(image, channel) gates
+        r2.x = se_hid;
+        r2.y = scale;
+        r2.M = nc;
+        r2.act = ACT_SIGMOID;
+        run_conv<T>(r2, b.se2, s);
         ConvArgs p = conv_args(b.c2);
         p.x = M2;
         p.y = nxt;

@@ -95,8 +95,8 @@ class Acoustic {
     int stride = 1, cin = 0, cout = 0, mid = 0, rd = 0;
     bool skip = false;
     PConv c1, c2;              // cn: c1 ; er: conv_exp, conv_pwl ; ir: conv_pw, conv_pwl
-    size_t dw_w = 0, dw_b = 0;  // ir depthwise (cs_mid x 9, cs_mid) fp32
-    size_t se_w1 = 0, se_b1 = 0, se_w2 = 0, se_b2 = 0;
+    size_t dw_w = 0, dw_b = 0;  // ir depthwise, tap-major (9 x cs_mid) and (cs_mid), fp32
+    PConv se1, se2;             // ir SE: conv_reduce (mid -> rd, SiLU), conv_expand (rd -> mid, sigmoid)
   };
   template <typename T>
   void effnet_t(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe, int* probe_dims,

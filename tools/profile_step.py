@@ -1,0 +1,25 @@
+"""Run the bench workload for a few steps with no timing/extras (for rocprofv3 --pmc passes)."""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "mri-to-speech_amd"))
+sys.path.insert(0, REPO)
+from m2s import runtime, synth  # noqa: E402
+from m2s.config import HIFIGAN_H  # noqa: E402
+import bench  # noqa: E402
+
+steps = int(os.environ.get("STEPS", "2"))
+clips, frames = int(os.environ.get("CLIPS", "64")), int(os.environ.get("FRAMES", "30"))
+dev = torch.device("cuda", 0)
+ac = runtime.AcousticEngine(synth.synth_acoustic_state(0), dtype="bf16", device=dev, chunk=1920)
+voc = runtime.VocoderEngine(synth.synth_generator_state(0), HIFIGAN_H, dtype="bf16", device=dev)
+mean, std = synth.synth_scaler()
+pipe = runtime.Pipeline(ac, voc, mean, std)
+x = bench.make_frames(clips, frames, 256, 0, dev)
+for _ in range(steps):
+    pipe.forward(x)
+torch.cuda.synchronize()
+print("done")
