@@ -1,0 +1,238 @@
+// Fused InvertedResidual front half for stride-1 blocks on small maps (bf16):
+//   conv_pw (1x1 expand, MFMA) + bn1 + SiLU  ->  LDS tile  ->  conv_dw 3x3 + bn2 + SiLU  ->  HBM
+//   + the SE squeeze (complete per-image channel means).
+// (timm InvertedResidual conv_pw/bn1/conv_dw/bn2/se.mean; mri_acoustic_model.py:28-34.)
+//
+// One workgroup = G whole images (G*P <= 256 positions, G in {1,2,4}) x a strided set of 32-channel
+// slices of the expanded width, processed one after another (the position->tile map and the zero
+// halo are built once).  The expanded activation never leaves the CU: the unfused sequence writes
+// it to HBM from the GEMM and reads it back in the depthwise (2 x 416..1248 channels x P x 2 B per
+// image), which made these blocks the largest HBM consumer of the encoder (profiles/ PMC).
+// Per slice:
+//   phase 1: D[c][m] = sum_k Wpw[c][k] x[m][k] on v_mfma_f32_16x16x32_bf16 (weights = A, positions
+//            = B, fragments loaded straight from L1/L2 with a one-step register prefetch), bias +
+//            SiLU, bf16 into the LDS tile.  The tile holds each image with a one-pixel zero halo,
+//            rows of 32 channels padded by 16 B, so the depthwise needs no bounds checks.
+//   phase 2: 4 channel groups x 64 pixel lanes (split evenly over the G images), 9 ds_read_b128 at
+//            constant offsets per pixel, v_dot2_f32_bf16 against (w_c, 0) / (0, w_c+1) weight
+//            dwords (no unpacking), SiLU, one v_cvt_pk_bf16_f32 per channel pair, 16-byte stores.
+//   squeeze: per-lane channel sums -> fixed xor-shuffle tree within each wave -> per-wave partials
+//            in LDS -> the image's waves added in order -> SE mean (deterministic).
+#include "conv_igemm.hpp"
+#include "kernels.hpp"
+#include "prof.hpp"
+
+namespace m2s {
+namespace {
+
+constexpr int SL = 32;         // expanded channels per slice
+constexpr int MROW = SL + 8;   // LDS row stride in bf16 (80 B)
+constexpr int NT = SL / 16;    // 16-channel MFMA subtiles
+constexpr int CG = SL / 8;     // phase-2 channel groups (8 channels = one 16-byte vector)
+constexpr int PL = 256 / CG;   // phase-2 pixel lanes (64; 16 per wave)
+constexpr int ROWS_MAX = 400;  // haloed pixel rows per workgroup (4 x 10x10, 1 x 18x18)
+constexpr int POS_MAX = 256;   // positions per workgroup
+constexpr int SLICES_PER_WG = 4;
+
+__device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float acc) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x), __builtin_bit_cast(bf16x2_t, w), acc,
+                                         false);
+}
+
+template <int MT>
+__global__ void __launch_bounds__(256) ir_pwdw_kernel(const bf16_t* __restrict__ x, int cs_in, int kp,
+                                                         const bf16_t* __restrict__ wpw, const float* __restrict__ bpw,
+                                                         const uint32_t* __restrict__ wdw2,
+                                                         const float* __restrict__ bdw, int N, int OH, int OW, int G,
+                                                         int cs_mid, bf16_t* __restrict__ y,
+                                                         bf16_t* __restrict__ se_mean) {
+  __shared__ __attribute__((aligned(16))) bf16_t tile[ROWS_MAX * MROW];
+  __shared__ uint16_t lut[POS_MAX];
+  __shared__ float red[4][SL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g16 = lane >> 4, r16 = lane & 15;
+  const int P = OH * OW, WR = OW + 2, IR = (OH + 2) * WR;
+  const int n0 = blockIdx.y * G, gi = min(G, N - n0), MP = gi * P;
+  const int nsl = (cs_mid + SL - 1) / SL;
+
+  // ---- once per workgroup: position -> haloed tile row; zero the tile (halo stays zero) -------
+  if (tid < G * P) {
+    const int g = tid / P, p = tid - g * P, oy = p / OW, ox = p - oy * OW;
+    lut[tid] = (uint16_t)(g * IR + (oy + 1) * WR + ox + 1);
+  }
+  {
+    uint4* t4 = reinterpret_cast<uint4*>(tile);
+    for (int i = tid; i < G * IR * (MROW / 8); i += 256) t4[i] = make_uint4(0, 0, 0, 0);
+  }
+
+  const bf16_t* xi = x + (size_t)n0 * P * cs_in;
+  const int mw = wave * MT * 16;
+  const int cg = tid % CG, pl = tid / CG;
+  const int lpi = PL / G, g = pl / lpi, q = pl - g * lpi;  // phase-2 image and lane within it
+  int off[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) off[t] = ((t / 3 - 1) * WR + (t % 3 - 1)) * MROW;
+
+  for (int sl = blockIdx.x; sl < nsl; sl += gridDim.x) {
+    const int c0 = sl * SL;
+    // ---- phase 1: expand GEMM, positions [mw, mw + MT*16) x channels [c0, c0 + SL) ------------
+    f32x4 acc[NT][MT];
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) acc[ni][mi] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint4 fa[2][NT], fb[2][MT];
+    auto load = [&](int buf, int k0) {
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni)
+        fa[buf][ni] = *reinterpret_cast<const uint4*>(wpw + (size_t)(c0 + ni * 16 + r16) * kp + k0 + 8 * g16);
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) {
+        const int m = mw + mi * 16 + r16, k = k0 + 8 * g16;
+        fb[buf][mi] = (m < MP && k < cs_in) ? *reinterpret_cast<const uint4*>(xi + (size_t)m * cs_in + k)
+                                            : make_uint4(0, 0, 0, 0);
+      }
+    };
+    auto mma = [&](int buf) {
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi)
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[buf][ni]),
+                                                                __builtin_bit_cast(bf16x8, fb[buf][mi]), acc[ni][mi],
+                                                                0, 0, 0);
+    };
+    load(0, 0);
+    for (int k0 = 0;;) {
+      if (k0 + 32 < kp) load(1, k0 + 32);
+      mma(0);
+      if ((k0 += 32) >= kp) break;
+      if (k0 + 32 < kp) load(0, k0 + 32);
+      mma(1);
+      if ((k0 += 32) >= kp) break;
+    }
+    __syncthreads();  // lut/zeroes visible; the previous slice's phase 2 is done with the tile
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni) {
+      const int cl = ni * 16 + 4 * g16;  // slice-local channel of acc[ni][.][0]
+      const float4 bb = *reinterpret_cast<const float4*>(bpw + c0 + cl);
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) {
+        const int m = mw + mi * 16 + r16;
+        if (m >= MP) continue;
+        uint2 u;
+        u.x = pack_bf16x2(silu(acc[ni][mi][0] + bb.x), silu(acc[ni][mi][1] + bb.y));
+        u.y = pack_bf16x2(silu(acc[ni][mi][2] + bb.z), silu(acc[ni][mi][3] + bb.w));
+        *reinterpret_cast<uint2*>(tile + lut[m] * MROW + cl) = u;
+      }
+    }
+    __syncthreads();
+
+    // ---- phase 2: depthwise 3x3 (stride 1, pad 1) from the haloed tile ------------------------
+    const int c = c0 + cg * 8;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (g < gi && c < cs_mid) {
+      uint32_t w[9][8];
+      float b[8];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const uint4 lo = *reinterpret_cast<const uint4*>(wdw2 + (size_t)t * cs_mid + c);
+        const uint4 hi = *reinterpret_cast<const uint4*>(wdw2 + (size_t)t * cs_mid + c + 4);
+        w[t][0] = lo.x; w[t][1] = lo.y; w[t][2] = lo.z; w[t][3] = lo.w;
+        w[t][4] = hi.x; w[t][5] = hi.y; w[t][6] = hi.z; w[t][7] = hi.w;
+      }
+      {
+        const float4 lo = *reinterpret_cast<const float4*>(bdw + c);
+        const float4 hi = *reinterpret_cast<const float4*>(bdw + c + 4);
+        b[0] = lo.x; b[1] = lo.y; b[2] = lo.z; b[3] = lo.w;
+        b[4] = hi.x; b[5] = hi.y; b[6] = hi.z; b[7] = hi.w;
+      }
+      bf16_t* yi = y + (size_t)(n0 + g) * P * cs_mid + c;
+      for (int p = q; p < P; p += lpi) {
+        const bf16_t* base = tile + lut[g * P + p] * MROW + cg * 8;
+        uint4 in[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) in[t] = *reinterpret_cast<const uint4*>(base + off[t]);
+        float a[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = b[j];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const uint32_t u[4] = {in[t].x, in[t].y, in[t].z, in[t].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            a[2 * j] = dot2(u[j], w[t][2 * j], a[2 * j]);
+            a[2 * j + 1] = dot2(u[j], w[t][2 * j + 1], a[2 * j + 1]);
+          }
+        }
+        uint4 o;
+        uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v0 = silu(a[2 * j]), v1 = silu(a[2 * j + 1]);
+          s[2 * j] += v0;
+          s[2 * j + 1] += v1;
+          ow[j] = pack_bf16x2(v0, v1);
+        }
+        *reinterpret_cast<uint4*>(yi + (size_t)p * cs_mid) = o;
+      }
+    }
+    // ---- squeeze: the wave's 16 pixel lanes (lane / CG) share cg = lane % CG; one image per wave
+    // when G = 4, else the image spans 4/G waves.
+#pragma unroll
+    for (int msk = CG; msk < 64; msk <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += __shfl_xor(s[j], msk);
+    if (lane < CG)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = s[j];
+    __syncthreads();
+    if (tid < G * SL) {
+      const int gg = tid / SL, cl = tid - gg * SL, wpi = 4 / G;
+      if (gg < gi && c0 + cl < cs_mid) {
+        float t = 0.f;
+        for (int wv = gg * wpi; wv < (gg + 1) * wpi; ++wv) t += red[wv][cl];
+        se_mean[(size_t)(n0 + gg) * cs_mid + c0 + cl] = f2bf(t / (float)P);
+      }
+    }
+  }
+}
+
+int ir_group(int OH, int OW) {
+  const int P = OH * OW, rows = (OH + 2) * (OW + 2);
+  for (int G = 4; G >= 1; G /= 2)
+    if (G * P <= POS_MAX && G * rows <= ROWS_MAX) return G;
+  return 0;
+}
+
+}  // namespace
+
+bool ir_fused_supported(int OH, int OW, int cs_in, int cs_mid) {
+  (void)cs_in;
+  return ir_group(OH, OW) > 0 && cs_mid % 8 == 0;
+}
+
+void launch_ir_pwdw(const bf16_t* x, int N, int cs_in, int kp, const bf16_t* wpw, const float* bpw,
+                    const uint32_t* wdw2, const float* bdw, int OH, int OW, int cs_mid, bf16_t* y, bf16_t* se_mean,
+                    double flops, double bytes, hipStream_t s) {
+  M2S_CHECK(ir_fused_supported(OH, OW, cs_in, cs_mid), "ir_pwdw: unsupported shape");
+  M2S_CHECK(kp % 32 == 0 && kp >= cs_in, "ir_pwdw: kp");
+  const int G = ir_group(OH, OW), pos = G * OH * OW;
+  const dim3 grid(ceil_div(ceil_div(cs_mid, SL), SLICES_PER_WG), ceil_div(N, G));
+  if (pos <= 64) {
+    ProfScope ps("ir_pwdw<1>", flops, bytes, s);
+    hipLaunchKernelGGL(ir_pwdw_kernel<1>, grid, dim3(256), 0, s, x, cs_in, kp, wpw, bpw, wdw2, bdw, N, OH, OW, G,
+                       cs_mid, y, se_mean);
+  } else if (pos <= 128) {
+    ProfScope ps("ir_pwdw<2>", flops, bytes, s);
+    hipLaunchKernelGGL(ir_pwdw_kernel<2>, grid, dim3(256), 0, s, x, cs_in, kp, wpw, bpw, wdw2, bdw, N, OH, OW, G,
+                       cs_mid, y, se_mean);
+  } else {
+    ProfScope ps(OH * OW > 64 ? "ir_pwdw<4>" : "ir_pwdw<4,grouped>", flops, bytes, s);
+    hipLaunchKernelGGL(ir_pwdw_kernel<4>, grid, dim3(256), 0, s, x, cs_in, kp, wpw, bpw, wdw2, bdw, N, OH, OW, G,
+                       cs_mid, y, se_mean);
+  }
+  M2S_HIP(hipGetLastError());
+}
+
+}  // namespace m2s

@@ -24,6 +24,15 @@ void launch_dwconv(const T* x, int N, int IH, int IW, int OH, int OW, int stride
 template <typename T>
 void launch_se_mean(const float* psum, int N, int npb, int cs, float inv_count, T* mean, hipStream_t s);
 
+// bf16 fused conv_pw + bn1 + SiLU + conv_dw (stride 1) + bn2 + SiLU + SE squeeze for maps whose
+// haloed tile fits a workgroup ((OH+2)(OW+2) <= 400, OH*OW <= 256): x (N,P,cs_in) -> y
+// (N,P,cs_mid), se_mean (N,cs_mid).  wpw packed [>=ceil64(cs_mid)][kp], bpw likewise padded;
+// wdw2 tap-major [9][cs_mid] bf16 weights in the dword half of their channel.  (ir_fused.hip)
+bool ir_fused_supported(int OH, int OW, int cs_in, int cs_mid);
+void launch_ir_pwdw(const bf16_t* x, int N, int cs_in, int kp, const bf16_t* wpw, const float* bpw,
+                    const uint32_t* wdw2, const float* bdw, int OH, int OW, int cs_mid, bf16_t* y, bf16_t* se_mean,
+                    double flops, double bytes, hipStream_t s);
+
 // Global average pool: x (N,P,cs) T -> feats (N,C) fp32 (dense, row stride C).
 template <typename T>
 void launch_gap(const T* x, int N, int P, int C, int cs, float* feats, hipStream_t s);

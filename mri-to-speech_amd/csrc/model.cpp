@@ -9,7 +9,9 @@
 #include "model.hpp"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "prof.hpp"
 
@@ -192,6 +194,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
     : dtype_(dtype), device_(device), n_mels_(n_mels), hidden_(hidden) {
   M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16, "bad dtype");
   M2S_CHECK(n_mels > 0 && hidden > 0 && hidden % 8 == 0, "bad n_mels / rnn_hidden");
+  if (const char* e = std::getenv("M2S_IR_FUSED")) ir_fused_ = std::strcmp(e, "0") != 0;
   const std::string P = "cnn.backbone.";
   {  // stem: fold repeat(1,3,1,1) by summing the 3 input channels; then BN
     const float* w = need(sd, P + "conv_stem.weight", {EFF_STEM, 3, 3, 3}).data;
@@ -252,6 +255,14 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
         }
         b.dw_w = arena_.add_vec(w9);
         b.dw_b = arena_.add_vec(bd);
+        if (dtype == M2S_DT_BF16) {  // fused kernel: bf16 weight in the half matching the channel
+          std::vector<uint32_t> w2(w9.size());  // (v_dot2 against a (c, c+1) activation dword)
+          for (size_t i = 0; i < w9.size(); ++i) {
+            const uint32_t h = f2bf_host(w9[i]);
+            w2[i] = (i % cs) % 2 == 0 ? h : h << 16;
+          }
+          b.dw_w2 = arena_.add_vec(w2);
+        }
         const float* w1 = need(sd, q + "se.conv_reduce.weight", {b.rd, m, 1, 1}).data;
         const float* b1 = need(sd, q + "se.conv_reduce.bias", {b.rd}).data;
         const float* w2 = need(sd, q + "se.conv_expand.weight", {m, b.rd, 1, 1}).data;
@@ -452,6 +463,15 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         run_conv<T>(p, b.c2, s);
       } else {
         const int cs = chan_stride(b.mid);
+        if (std::is_same<T, bf16_t>::value && b.stride == 1 && ir_fused_ &&
+            ir_fused_supported(nh, nw, b.c1.cs_in, cs)) {
+          const double P = (double)nh * nw;
+          launch_ir_pwdw(reinterpret_cast<const bf16_t*>(cur), nc, b.c1.cs_in, b.c1.kp,
+                         static_cast<const bf16_t*>(b.c1.w), b.c1.b,
+                         static_cast<const uint32_t*>(arena_.ptr(b.dw_w2)), static_cast<const float*>(arena_.ptr(b.dw_b)),
+                         nh, nw, cs, reinterpret_cast<bf16_t*>(M2), reinterpret_cast<bf16_t*>(se_mean),
+                         2.0 * nc * P * b.mid * (b.c1.cin + 9), 2.0 * nc * P * (b.c1.cs_in + cs), s);
+        } else {
         ConvArgs e = conv_args(b.c1);
         e.x = cur;
         e.y = M;
@@ -469,6 +489,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         {
           ProfScope ps("se_mean", 0.0, 4.0 * nc * cs * dw_pixel_blocks(nh, nw) + sizeof(T) * (double)nc * cs, s);
           launch_se_mean<T>(sums, nc, dw_pixel_blocks(nh, nw), cs, 1.0f / (float)(nh * nw), se_mean, s);
+        }
         }
         ConvArgs r1 = conv_args(b.se1);  // conv_reduce + SiLU, all images of the chunk at once
         r1.x = se_mean;

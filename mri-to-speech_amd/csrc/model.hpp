@@ -82,6 +82,7 @@ class Acoustic {
   int device() const { return device_; }
   int n_mels() const { return n_mels_; }
   int chunk = 256;
+  bool ir_fused_ = true;  // bf16: fused conv_pw + conv_dw + SE squeeze (env M2S_IR_FUSED=0 disables)
 
   size_t workspace_bytes(int B, int T, int H, int W) const;
   void forward(const float* frames, int B, int T, int H, int W, float* mel_norm, void* ws, size_t wsb, hipStream_t s);
@@ -96,6 +97,7 @@ class Acoustic {
     bool skip = false;
     PConv c1, c2;              // cn: c1 ; er: conv_exp, conv_pwl ; ir: conv_pw, conv_pwl
     size_t dw_w = 0, dw_b = 0;  // ir depthwise, tap-major (9 x cs_mid) and (cs_mid), fp32
+    size_t dw_w2 = 0;           // bf16 engines: the same taps as bf16 in the channel's dword half
     PConv se1, se2;             // ir SE: conv_reduce (mid -> rd, SiLU), conv_expand (rd -> mid, sigmoid)
   };
   template <typename T>

@@ -156,6 +156,34 @@ def test_effnet_bf16_close(ac_bf16, ac_state):
     assert cos >= 0.999, cos
 
 
+def _cos(a, b):
+    return float((a * b).sum() / np.sqrt((a ** 2).sum() * (b ** 2).sum()))
+
+
+@pytest.mark.parametrize("hw", [(256, 256), (96, 80), (67, 101)])
+def test_effnet_bf16_ir_fused_every_block(rt, ac_state, monkeypatch, hw):
+    """The fused conv_pw+conv_dw+SE-squeeze kernel (ir_fused.hip) against the unfused bf16
+    sequence and the fp32 oracle, block by block (both bf16 paths round the expanded activation
+    to bf16 at the same point, so they agree to accumulation order)."""
+    sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
+    fr = torch.from_numpy(synth.synth_frames(1, 3, hw=hw, seed=31)[0])
+    taps = []
+    effnet.effnet_features(sd, fr, taps=taps)
+    monkeypatch.setenv("M2S_IR_FUSED", "1")
+    fused = rt.AcousticEngine(ac_state[1], dtype="bf16", device=DEV)
+    monkeypatch.setenv("M2S_IR_FUSED", "0")
+    plain = rt.AcousticEngine(ac_state[1], dtype="bf16", device=DEV)
+    x = fr.to(DEV)
+    for i, ref in enumerate(taps):
+        a = fused.probe(x, i).float().cpu().numpy()
+        b = plain.probe(x, i).float().cpu().numpy()
+        assert _rel(a, b) <= 2e-2, f"block {i}: fused vs unfused rel {_rel(a, b)}"
+        assert _cos(a, ref.numpy()) >= 0.999, f"block {i}: cos vs oracle {_cos(a, ref.numpy())}"
+    ga = fused.effnet(x).cpu().numpy()
+    gb = plain.effnet(x).cpu().numpy()
+    assert _cos(ga, gb) >= 0.99999
+
+
 # ------------------------------------------------------------------------------ acoustic model / pipeline
 def test_acoustic_forward_matches_reference_wiring(ac_f32):
     g = _gold("acoustic.npz")
