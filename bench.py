@@ -47,7 +47,7 @@ def parse():
     p.add_argument("--frames", type=int, default=30, help="frames per clip")
     p.add_argument("--hw", type=int, default=256)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    p.add_argument("--chunk", type=int, default=256, help="frames per CNN pass")
+    p.add_argument("--chunk", type=int, default=1920, help="frames per CNN pass (1920 = one pass over the 64x30 step)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-profile", action="store_true")

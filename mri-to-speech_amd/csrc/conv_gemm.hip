@@ -315,7 +315,7 @@ const char* kname(int k) {
 
 template <int BM, int BN, int MT, int NT, int KIND, int XF>
 void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
-  constexpr int S = BM >= 256 ? 3 : 4;  // keep two workgroups' LDS per CU
+  constexpr int S = (BM >= 256 || BM + BN >= 384) ? 3 : 4;  // keep two workgroups' LDS per CU
   static bool attr = [] {
     M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -344,6 +344,16 @@ void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
 template <int KIND, int XF>
 void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
   const int n = a.cs_out;
+  static const int big = [] {  // M2S_GEMM_BIG=0 keeps the 128x128 tile for the long 1x1 GEMMs
+    const char* e = getenv("M2S_GEMM_BIG");
+    return e ? atoi(e) : 1;
+  }();
+  if constexpr (KIND == KIND_GEMM) if (big && a.M >= 256 * 256 && n > 128 && n <= 256 && a.kp >= 512) {
+    // long-K 1x1 GEMMs with 129..256 outputs: one 256-wide n tile reads the activations once
+    // instead of twice (b5 conv_pwl 1248 -> 208: 13.5 -> 10.0 ms per 4 steps).  A 256x128 tile
+    // for n <= 128 measured slower at every K (one wave per SIMD at 272 registers).
+    return launch_tile<128, 256, 4, 8, KIND, XF>(a, s, phases, flops, bytes);
+  }
   if (n <= 16)
     launch_tile<256, 16, 4, 1, KIND, XF>(a, s, phases, flops, bytes);
   else if (n <= 32)
@@ -377,6 +387,11 @@ void launch_conv_bf16_fast(const ConvArgs& a, hipStream_t s, double flops, doubl
   M2S_CHECK(a.kp % 32 == 0 && a.kp >= a.ntaps * a.cs_in, "conv_gemm: kp");
   M2S_CHECK(a.kind != KIND_CONV2D || a.ks == 3, "conv_gemm: 2-D kernels are 3x3 (1x1 runs as GEMM)");
   if (a.M <= 0) return;
+  static const bool halo = [] {  // M2S_CONV_HALO=0: 3x3 stride-1 convs on the implicit-GEMM path
+    const char* e = getenv("M2S_CONV_HALO");
+    return !e || atoi(e) != 0;
+  }();
+  if (halo && conv_halo_supported(a)) return launch_conv_halo(a, s, flops, bytes);
   switch (a.kind) {
     case KIND_CONV2D: launch_kind<KIND_CONV2D>(a, s, 1, flops, bytes); break;
     case KIND_CONV1D: launch_kind<KIND_CONV1D>(a, s, 1, flops, bytes); break;

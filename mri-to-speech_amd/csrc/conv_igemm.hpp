@@ -55,6 +55,10 @@ struct ConvArgs {
 template <typename T>
 void launch_conv(const ConvArgs& a, hipStream_t s, double flops = 0.0, double bytes = 0.0);
 void launch_conv_bf16_fast(const ConvArgs& a, hipStream_t s, double flops, double bytes);
+// bf16 3x3 stride-1 convs with cs_in in {32, 64}: persistent LDS-resident-weight kernel
+// (conv_halo.hip); launch_conv_bf16_fast routes them there.
+bool conv_halo_supported(const ConvArgs& a);
+void launch_conv_halo(const ConvArgs& a, hipStream_t s, double flops, double bytes);
 
 // Host-side helpers shared by the packers.
 inline int conv_tpc(int cs_in, int kc) { return cs_in < kc ? kc / cs_in : 1; }

@@ -3,9 +3,9 @@
 //   + the SE squeeze (complete per-image channel means).
 // (timm InvertedResidual conv_pw/bn1/conv_dw/bn2/se.mean; mri_acoustic_model.py:28-34.)
 //
-// One workgroup = G whole images (G*P <= 256 positions, G in {1,2,4}) x a strided set of 32-channel
-// slices of the expanded width, processed one after another (the position->tile map and the zero
-// halo are built once).  The expanded activation never leaves the CU: the unfused sequence writes
+// One workgroup = G whole images (G*P <= 256 positions, G in {1,2,4}) x one 32-channel slice of the
+// expanded width (127 VGPRs, 33 KB LDS: 4 workgroups per CU; a loop over several slices per
+// workgroup halves the occupancy and measured slower).  The expanded activation never leaves the CU: the unfused sequence writes
 // it to HBM from the GEMM and reads it back in the depthwise (2 x 416..1248 channels x P x 2 B per
 // image), which made these blocks the largest HBM consumer of the encoder (profiles/ PMC).
 // Per slice:
@@ -32,7 +32,10 @@ constexpr int CG = SL / 8;     // phase-2 channel groups (8 channels = one 16-by
 constexpr int PL = 256 / CG;   // phase-2 pixel lanes (64; 16 per wave)
 constexpr int ROWS_MAX = 400;  // haloed pixel rows per workgroup (4 x 10x10, 1 x 18x18)
 constexpr int POS_MAX = 256;   // positions per workgroup
-constexpr int SLICES_PER_WG = 4;
+#ifndef IRF_MODE
+#define IRF_MODE 0
+#endif
+constexpr int SLICES_PER_WG = 1;  // >1 (a slice loop per workgroup) measured slower: occupancy 4 -> 2
 
 __device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float acc) {
   return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x), __builtin_bit_cast(bf16x2_t, w), acc,
@@ -40,7 +43,7 @@ __device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float acc) {
 }
 
 template <int MT>
-__global__ void __launch_bounds__(256) ir_pwdw_kernel(const bf16_t* __restrict__ x, int cs_in, int kp,
+__global__ void __launch_bounds__(256, 4) ir_pwdw_kernel(const bf16_t* __restrict__ x, int cs_in, int kp,
                                                          const bf16_t* __restrict__ wpw, const float* __restrict__ bpw,
                                                          const uint32_t* __restrict__ wdw2,
                                                          const float* __restrict__ bdw, int N, int OH, int OW, int G,
@@ -53,9 +56,8 @@ __global__ void __launch_bounds__(256) ir_pwdw_kernel(const bf16_t* __restrict__
   const int g16 = lane >> 4, r16 = lane & 15;
   const int P = OH * OW, WR = OW + 2, IR = (OH + 2) * WR;
   const int n0 = blockIdx.y * G, gi = min(G, N - n0), MP = gi * P;
-  const int nsl = (cs_mid + SL - 1) / SL;
 
-  // ---- once per workgroup: position -> haloed tile row; zero the tile (halo stays zero) -------
+  // ---- position -> haloed tile row; zero the tile (the halo stays zero) ----------------------
   if (tid < G * P) {
     const int g = tid / P, p = tid - g * P, oy = p / OW, ox = p - oy * OW;
     lut[tid] = (uint16_t)(g * IR + (oy + 1) * WR + ox + 1);
@@ -73,7 +75,8 @@ __global__ void __launch_bounds__(256) ir_pwdw_kernel(const bf16_t* __restrict__
 #pragma unroll
   for (int t = 0; t < 9; ++t) off[t] = ((t / 3 - 1) * WR + (t % 3 - 1)) * MROW;
 
-  for (int sl = blockIdx.x; sl < nsl; sl += gridDim.x) {
+  {
+    const int sl = blockIdx.x;  // one slice per workgroup (grid.x = slices)
     const int c0 = sl * SL;
     // ---- phase 1: expand GEMM, positions [mw, mw + MT*16) x channels [c0, c0 + SL) ------------
     f32x4 acc[NT][MT];
@@ -102,6 +105,7 @@ __global__ void __launch_bounds__(256) ir_pwdw_kernel(const bf16_t* __restrict__
                                                                 __builtin_bit_cast(bf16x8, fb[buf][mi]), acc[ni][mi],
                                                                 0, 0, 0);
     };
+    if (!(IRF_MODE & 1)) {  // IRF_MODE: microbenchmark variants (tools/irf_bench.hip); 0 in the library
     load(0, 0);
     for (int k0 = 0;;) {
       if (k0 + 32 < kp) load(1, k0 + 32);
@@ -111,7 +115,8 @@ __global__ void __launch_bounds__(256) ir_pwdw_kernel(const bf16_t* __restrict__
       mma(1);
       if ((k0 += 32) >= kp) break;
     }
-    __syncthreads();  // lut/zeroes visible; the previous slice's phase 2 is done with the tile
+    }
+    __syncthreads();  // lut/zeroes visible
 #pragma unroll
     for (int ni = 0; ni < NT; ++ni) {
       const int cl = ni * 16 + 4 * g16;  // slice-local channel of acc[ni][.][0]
@@ -131,7 +136,7 @@ __global__ void __launch_bounds__(256) ir_pwdw_kernel(const bf16_t* __restrict__
     // ---- phase 2: depthwise 3x3 (stride 1, pad 1) from the haloed tile ------------------------
     const int c = c0 + cg * 8;
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (g < gi && c < cs_mid) {
+    if (g < gi && c < cs_mid && !(IRF_MODE & 2)) {
       uint32_t w[9][8];
       float b[8];
 #pragma unroll
@@ -174,7 +179,7 @@ __global__ void __launch_bounds__(256) ir_pwdw_kernel(const bf16_t* __restrict__
           s[2 * j + 1] += v1;
           ow[j] = pack_bf16x2(v0, v1);
         }
-        *reinterpret_cast<uint4*>(yi + (size_t)p * cs_mid) = o;
+        if (!(IRF_MODE & 4) || o.x == 0x7fc17fc1u) *reinterpret_cast<uint4*>(yi + (size_t)p * cs_mid) = o;
       }
     }
     // ---- squeeze: the wave's 16 pixel lanes (lane / CG) share cg = lane % CG; one image per wave
