@@ -59,15 +59,16 @@ struct HaloArgs {
   float act_slope;
 };
 
-template <int MTW, int NTW, int WM, int WN>
+template <int MTW, int NTW, int WM, int WN, int KC>
 __global__ void __launch_bounds__(256) conv_halo_kernel(const HaloArgs a) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int BN = WN * NTW * 16;
   constexpr int TH = WM * MTW;        // tile rows (one 16-position subtile per row)
   constexpr int HW = TW + 2;          // halo width
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nsteps = 9 * a.kc;
-  const int hrows = (TH + 2) * HW * a.kc;
+  const int nsteps = a.kp / 32;
+  // kc = 64-byte rows per pixel (cs_in / 32); kc = 0: cs_in = 16, two pixels per row
+  const int hrows = KC ? (TH + 2) * HW * KC : (TH + 2) * HW / 2;
   const int hblocks = (hrows + 15) / 16;
   char* wbuf = smem;
   char* hbuf0 = smem + nsteps * BN * ROWB;
@@ -98,12 +99,19 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(const HaloArgs a) {
     const bf16_t* xi = a.x + (size_t)img * a.H * a.W * a.cs_in;
     for (int blk = wave; blk < hblocks; blk += 4) {
       const int row = blk * 16 + lrow;
-      const int hp = a.kc == 2 ? row >> 1 : row, kc = a.kc == 2 ? row & 1 : 0;
+      int hp, coff;  // halo pixel and channel offset of this lane's 16 bytes
+      if (KC == 0) {
+        hp = 2 * row + (q >> 1);
+        coff = (q & 1) * 8;
+      } else {
+        hp = KC == 2 ? row >> 1 : row;
+        coff = (KC == 2 ? row & 1 : 0) * 32 + q * 8;
+      }
       const int hy = hp / HW, hx = hp - (hp / HW) * HW;
       const int iy = ty0 + hy, ix = tx0 + hx;
       const void* src = g_halo_zero;
       if (row < hrows && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-        src = xi + ((size_t)iy * a.W + ix) * a.cs_in + kc * 32 + q * 8;
+        src = xi + ((size_t)iy * a.W + ix) * a.cs_in + coff;
       dma16(src, hb + blk * 16 * ROWB);
     }
   };
@@ -123,7 +131,11 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(const HaloArgs a) {
       for (int mi = 0; mi < MTW; ++mi) acc[ni][mi] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     for (int st = 0; st < nsteps; ++st) {
-      const int tap = a.kc == 2 ? st >> 1 : st, kc = a.kc == 2 ? st & 1 : 0;
+      // cs_in = 16: a k-step spans taps 2st (lanes g < 2) and 2st+1; the pad tap 9 (zero
+      // weights) reads tap 0's pixel so the product stays finite
+      int tap = KC == 0 ? 2 * st + (g >> 1) : (KC == 2 ? st >> 1 : st);
+      if (tap > 8) tap = 0;
+      const int kc = KC == 2 ? st & 1 : 0;
       const int ky = tap / 3, kx = tap - (tap / 3) * 3;
       bf16x8 af[NTW], bx[MTW];
 #pragma unroll
@@ -132,14 +144,31 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(const HaloArgs a) {
 #pragma unroll
       for (int mi = 0; mi < MTW; ++mi) {
         const int ty = wm * MTW + mi;
-        const int row = ((ty + ky) * HW + r16 + kx) * a.kc + kc;
-        bx[mi] = *reinterpret_cast<const bf16x8*>(hb + swz(row, g));
+        const int p = (ty + ky) * HW + r16 + kx;
+        const int off = KC == 0 ? swz(p >> 1, ((p & 1) << 1) | (g & 1)) : swz(p * KC + kc, g);
+        bx[mi] = *reinterpret_cast<const bf16x8*>(hb + off);
       }
 #pragma unroll
       for (int ni = 0; ni < NTW; ++ni)
 #pragma unroll
         for (int mi = 0; mi < MTW; ++mi)
           acc[ni][mi] = (HALO_MODE & 1) ? acc[ni][mi] + __builtin_bit_cast(f32x4, __builtin_bit_cast(uint4, bx[mi]) ^ __builtin_bit_cast(uint4, af[ni])) : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ni], bx[mi], acc[ni][mi], 0, 0, 0);
+    }
+    // residual = this block's input (cs_in == cs_out): take it from the halo tile now, before the
+    // barrier releases the buffer to the next prefetch
+    uint2 rres[NTW][MTW];
+    const bool res_lds = KC == 0 && a.res == a.x;  // cs_in == cs_out == 16 (b0 skip)
+    if (KC == 0 && res_lds) {
+#pragma unroll
+      for (int mi = 0; mi < MTW; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NTW; ++ni) {
+          const int n4 = n0 + wn * NTW * 16 + ni * 16 + 4 * g;
+          const int p = (wm * MTW + mi + 1) * HW + r16 + 1;
+          const int off = KC == 0 ? swz(p >> 1, ((p & 1) << 1) | (n4 >> 3)) + (n4 & 7) * 2
+                                    : swz(p * KC + (n4 >> 5), (n4 & 31) >> 3) + (n4 & 7) * 2;
+          rres[ni][mi] = n4 < a.cs_in ? *reinterpret_cast<const uint2*>(hb + off) : make_uint2(0, 0);
+        }
     }
     // the next halo has landed (it had the whole K loop) and every wave is done with this one
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -166,7 +195,13 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(const HaloArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * a.act_slope;
         }
-        if (a.res) {
+        if (KC == 0 && res_lds) {
+          const uint2 u = rres[ni][mi];
+          v[0] += __uint_as_float(u.x << 16);
+          v[1] += __uint_as_float(u.x & 0xffff0000u);
+          v[2] += __uint_as_float(u.y << 16);
+          v[3] += __uint_as_float(u.y & 0xffff0000u);
+        } else if (a.res) {
           float r[4];
           ld4f(a.res + orow + n4, r);
 #pragma unroll
@@ -191,7 +226,7 @@ int num_cus() {
   return n;
 }
 
-template <int MTW, int NTW, int WM, int WN>
+template <int MTW, int NTW, int WM, int WN, int KC>
 bool launch_cfg(const ConvArgs& c, hipStream_t s, double flops, double bytes) {
   constexpr int BN = WN * NTW * 16, TH = WM * MTW;
   HaloArgs a;
@@ -203,7 +238,7 @@ bool launch_cfg(const ConvArgs& c, hipStream_t s, double flops, double bytes) {
   a.H = c.OH;
   a.W = c.OW;
   a.cs_in = c.cs_in;
-  a.kc = c.cs_in / 32;
+  a.kc = c.cs_in / 32;  // 0 for cs_in = 16
   a.kp = c.kp;
   a.n_pad = c.n_pad;
   a.cs_out = c.cs_out;
@@ -214,11 +249,12 @@ bool launch_cfg(const ConvArgs& c, hipStream_t s, double flops, double bytes) {
   a.n_tiles = ceil_div(c.cs_out, BN);
   a.act = c.act;
   a.act_slope = c.act_slope;
-  const int hblocks = ceil_div((TH + 2) * (TW + 2) * a.kc, 16);
-  const size_t lds = (size_t)9 * a.kc * BN * ROWB + 2 * (size_t)hblocks * 16 * ROWB;
+  const int hrows = a.kc ? (TH + 2) * (TW + 2) * a.kc : (TH + 2) * (TW + 2) / 2;
+  const int hblocks = ceil_div(hrows, 16);
+  const size_t lds = (size_t)(a.kp / 32) * BN * ROWB + 2 * (size_t)hblocks * 16 * ROWB;
   if (lds > 160 * 1024) return false;
   static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_halo_kernel<MTW, NTW, WM, WN>),
+    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_halo_kernel<MTW, NTW, WM, WN, KC>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     return true;
   }();
@@ -229,7 +265,7 @@ bool launch_cfg(const ConvArgs& c, hipStream_t s, double flops, double bytes) {
   char name[64];
   snprintf(name, sizeof(name), "conv_halo<%dx%d,n%d>", TH, TW, BN);
   ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((conv_halo_kernel<MTW, NTW, WM, WN>), dim3(wgs), dim3(256), lds, s, a);
+  hipLaunchKernelGGL((conv_halo_kernel<MTW, NTW, WM, WN, KC>), dim3(wgs), dim3(256), lds, s, a);
   M2S_HIP(hipGetLastError());
   return true;
 }
@@ -238,34 +274,22 @@ bool launch_cfg(const ConvArgs& c, hipStream_t s, double flops, double bytes) {
 
 bool conv_halo_supported(const ConvArgs& a) {
   return a.kind == KIND_CONV2D && a.ks == 3 && a.stride == 1 && a.ntaps == 9 && a.IH == a.OH && a.IW == a.OW &&
-         a.pad_t == 1 && a.pad_l == 1 && a.cs_in == 32 && a.kp == 9 * a.cs_in &&
+         a.pad_t == 1 && a.pad_l == 1 && ((a.cs_in == 32 && a.kp == 9 * 32) || (a.cs_in == 16 && a.kp == 10 * 16)) &&
          a.in_xform == IN_NONE && !a.accum && a.cs_out <= 256;
 }
 
 void launch_conv_halo(const ConvArgs& a, hipStream_t s, double flops, double bytes) {
   M2S_CHECK(conv_halo_supported(a), "conv_halo: unsupported conv");
-  static const int cfg = [] {  // M2S_HALO_CFG: tile experiments (0 = the per-shape default)
-    const char* e = getenv("M2S_HALO_CFG");
-    return e ? atoi(e) : 0;
-  }();
-  bool done = false;
-  switch (cfg) {
-    case 1: done = launch_cfg<2, 4, 4, 1>(a, s, flops, bytes); break;
-    case 2: done = launch_cfg<4, 4, 4, 1>(a, s, flops, bytes); break;
-    case 3: done = launch_cfg<8, 4, 2, 2>(a, s, flops, bytes); break;
-    case 4: done = launch_cfg<2, 2, 4, 1>(a, s, flops, bytes); break;
-    case 5: done = launch_cfg<4, 2, 4, 1>(a, s, flops, bytes); break;
-    case 6: done = launch_cfg<4, 4, 2, 2>(a, s, flops, bytes); break;
-    case 7: done = launch_cfg<8, 2, 4, 1>(a, s, flops, bytes); break;
-    case 8: done = launch_cfg<8, 1, 4, 1>(a, s, flops, bytes); break;
-    case 9: done = launch_cfg<2, 1, 4, 1>(a, s, flops, bytes); break;
-    default: break;
-  }
-  if (done) return;
-  if (a.cs_out <= 16)
-    done = launch_cfg<4, 1, 4, 1>(a, s, flops, bytes);  // 16x16 tiles, memory-bound b0 layers
+  // Tile shapes measured with tools/halo_bench.hip (1920 frames): 16x16 output tiles; 64-channel
+  // N tiles beat 128 (the 128-wide tile needs 1 wave/SIMD: 1.81 vs 1.28 ms on b1 conv_exp) and
+  // 32 (1.61 ms); 8x16 tiles lose to 16x16 at every width.
+  bool done;
+  if (a.cs_in == 16)
+    done = launch_cfg<4, 1, 4, 1, 0>(a, s, flops, bytes);  // b0 16 -> 16
+  else if (a.cs_out <= 16)
+    done = launch_cfg<4, 1, 4, 1, 1>(a, s, flops, bytes);  // b0 32 -> 16
   else
-    done = launch_cfg<4, 4, 4, 1>(a, s, flops, bytes);  // 16x16 x 64-channel tiles
+    done = launch_cfg<4, 4, 4, 1, 1>(a, s, flops, bytes);  // b1 32 -> 128 (two 64-wide N tiles)
   M2S_CHECK(done, "conv_halo: LDS budget");
 }
 

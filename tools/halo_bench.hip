@@ -8,8 +8,8 @@
 
 using namespace m2s;
 
-static void run(const char* name, int H, int cs_in, int cout, int act) {
-  const int N = 1920, kp = 9 * cs_in, npad = (cout + 63) / 64 * 64;
+static void run(const char* name, int H, int cs_in, int cout, int act, bool res = false) {
+  const int N = 1920, kp = (cs_in == 16 ? 10 : 9) * cs_in, npad = (cout + 63) / 64 * 64;
   std::vector<uint16_t> hx((size_t)N * H * H * cs_in), hw((size_t)npad * kp);
   for (size_t i = 0; i < hx.size(); ++i) hx[i] = 0x3c00 + (i * 7 % 64);
   for (size_t i = 0; i < hw.size(); ++i) hw[i] = 0x3a00 + (i * 5 % 64);
@@ -29,6 +29,8 @@ static void run(const char* name, int H, int cs_in, int cout, int act) {
   a.kind = KIND_CONV2D; a.M = N * H * H; a.cs_in = cs_in; a.cs_out = cout; a.n_pad = npad; a.kp = kp;
   a.ntaps = 9; a.tpc = 1; a.IH = a.IW = a.OH = a.OW = H; a.ks = 3; a.stride = 1; a.pad_t = a.pad_l = 1;
   a.act = act; a.accum_div = 1.f;
+  if (res) a.res = x;
+  if (!conv_halo_supported(a)) { std::printf("%s: not a halo shape\n", name); return; }
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
@@ -49,6 +51,7 @@ static void run(const char* name, int H, int cs_in, int cout, int act) {
 
 int main() {
   run("b0 128x128 32->16 silu", 128, 32, 16, ACT_SILU);
+  run("b0.1 128x128 16->16 silu+res", 128, 16, 16, ACT_SILU, true);
   run("b1 64x64 32->128 silu", 64, 32, 128, ACT_SILU);
   run("b2 32x32 64->224 silu", 32, 64, 224, ACT_SILU);
   run("b1 64x64 32->128 none", 64, 32, 128, ACT_NONE);
