@@ -336,7 +336,7 @@ void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
   if (detail)  // per-layer records for analysis: K x N and rows per launch
     snprintf(name, sizeof(name), "conv_gemm<%s,%dx%d> K%d N%d M%d", kname(KIND), BM, BN, a.kp, a.cs_out, a.M);
   else
-    snprintf(name, sizeof(name), "conv_gemm<bf16,%s,%dx%d>", kname(KIND), BM, BN);
+    snprintf(name, sizeof(name), "conv_gemm_kernel<%d, %d, %d, %d, %d, %d, %d>", BM, BN, MT, NT, S, KIND, XF);
   ProfScope ps(name, flops, bytes, s);
   hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF>), grid, dim3(256), lds, s, a, n_tiles, se_imgs);
 }

@@ -263,7 +263,7 @@ bool launch_cfg(const ConvArgs& c, hipStream_t s, double flops, double bytes) {
   int wgs = std::min(a.m_tiles * a.n_tiles, num_cus() * std::min(per_cu, 4));
   wgs = std::max(a.n_tiles, wgs / a.n_tiles * a.n_tiles);
   char name[64];
-  snprintf(name, sizeof(name), "conv_halo<%dx%d,n%d>", TH, TW, BN);
+  snprintf(name, sizeof(name), "conv_halo_kernel<%d, %d, %d, %d, %d>", MTW, NTW, WM, WN, KC);
   ProfScope ps(name, flops, bytes, s);
   hipLaunchKernelGGL((conv_halo_kernel<MTW, NTW, WM, WN, KC>), dim3(wgs), dim3(256), lds, s, a);
   M2S_HIP(hipGetLastError());

@@ -247,21 +247,13 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
   }
 }
 
-const char* kind_name(int k) {
-  switch (k) {
-    case KIND_CONV2D: return "conv2d";
-    case KIND_CONV1D: return "conv1d";
-    case KIND_CONVT: return "convT";
-    default: return "gemm";
-  }
-}
 
 template <typename T, int MT, int NT, int KIND>
 void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
   dim3 grid(ceil_div(a.M, 4 * MT * 16), ceil_div(a.cs_out, NT * 16), phases);
   M2S_CHECK(grid.y * NT * 16 <= a.n_pad, "conv: weight rows not padded to the N tile");
   char name[96];
-  snprintf(name, sizeof(name), "conv_igemm<%s,%s,m%dn%d>", sizeof(T) == 4 ? "f32" : "bf16", kind_name(KIND), MT, NT);
+  snprintf(name, sizeof(name), "conv_igemm_kernel<%s, %d, %d, %d>", sizeof(T) == 4 ? "float" : "unsigned short", MT, NT, KIND);
   ProfScope ps(name, flops, bytes, s);
   hipLaunchKernelGGL((conv_igemm_kernel<T, MT, NT, KIND>), grid, dim3(256), 0, s, a);
 }

@@ -35,7 +35,8 @@ __device__ __forceinline__ float act_silu(float v) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// stem: one thread = one output pixel x 32 channels.  TF-SAME pads passed from the host.
+// stem: four lanes per output pixel, 8 channels each, so one wave's stores cover 16 whole pixel
+// rows (1 KB contiguous in bf16) instead of 64 partial ones.  TF-SAME pads passed from the host.
 template <typename T>
 __global__ void __launch_bounds__(256) stem_kernel(const float* __restrict__ frames, int N, int H, int W, int OH,
                                                    int OW, int pad_t, int pad_l, const float* __restrict__ w9,
@@ -45,9 +46,10 @@ __global__ void __launch_bounds__(256) stem_kernel(const float* __restrict__ fra
   for (int i = threadIdx.x; i < 32 * 9 + 32; i += 256)
     sw[i] = i < 32 * 9 ? (i / 9 < cout ? w9[i] : 0.f) : (i - 288 < cout ? bias[i - 288] : 0.f);
   __syncthreads();
-  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  const long p = ((long)blockIdx.x * 256 + threadIdx.x) >> 2;
+  const int o0 = (threadIdx.x & 3) * 8;
   const long total = (long)N * OH * OW;
-  if (p >= total) return;
+  if (p >= total || o0 >= cs_out) return;
   const int hw = OH * OW;
   const int n = (int)(p / hw);
   const int rem = (int)(p - (long)n * hw);
@@ -60,18 +62,21 @@ __global__ void __launch_bounds__(256) stem_kernel(const float* __restrict__ fra
       const int iy = oy * 2 - pad_t + ky, ix = ox * 2 - pad_l + kx;
       in[ky * 3 + kx] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? frames[((long)n * H + iy) * W + ix] : 0.f;
     }
-  T* out = y + p * cs_out;
+  float v[8];
 #pragma unroll
-  for (int o = 0; o < 32; o += 4) {
-    float v[4];
+  for (int j = 0; j < 8; ++j) {
+    float acc = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float acc = 0.f;
-#pragma unroll
-      for (int t = 0; t < 9; ++t) acc += sw[(o + j) * 9 + t] * in[t];
-      v[j] = act_silu<T>(acc + sw[288 + o + j]);
-    }
-    if (o < cs_out) st4<T>(out + o, v[0], v[1], v[2], v[3]);
+    for (int t = 0; t < 9; ++t) acc += sw[(o0 + j) * 9 + t] * in[t];
+    v[j] = act_silu<T>(acc + sw[288 + o0 + j]);
+  }
+  T* out = y + p * cs_out + o0;
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(out) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(out + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    *reinterpret_cast<uint4*>(out) =
+        make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
   }
 }
 
@@ -256,8 +261,8 @@ void launch_add2(const float* a, const float* b, float* y, long n, hipStream_t s
 template <typename T>
 void launch_stem(const float* frames, int N, int H, int W, int OH, int OW, int pad_t, int pad_l, const float* w9,
                  const float* bias, int cout, int cs_out, T* y, hipStream_t s) {
-  M2S_CHECK(cout <= 32 && cs_out % 4 == 0, "stem: unsupported channel count");
-  hipLaunchKernelGGL(stem_kernel<T>, dim3(nblk((long)N * OH * OW)), dim3(256), 0, s, frames, N, H, W, OH, OW, pad_t,
+  M2S_CHECK(cout <= 32 && cs_out % 8 == 0 && cs_out <= 32, "stem: unsupported channel count");
+  hipLaunchKernelGGL(stem_kernel<T>, dim3(nblk(4L * N * OH * OW)), dim3(256), 0, s, frames, N, H, W, OH, OW, pad_t,
                      pad_l, w9, bias, cout, cs_out, y);
   M2S_HIP(hipGetLastError());
 }

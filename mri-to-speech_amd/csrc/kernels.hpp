@@ -42,6 +42,14 @@ void launch_gap(const T* x, int N, int P, int C, int cs, float* feats, hipStream
 void launch_lstm_step(const float* pre, const float* whh, float* hs, float* cst, int B, int T, int H,
                       int step, hipStream_t s);
 
+// The same recurrence for all T steps in ONE persistent launch (lstm_persistent.hip): W_hh resident
+// in VGPRs across 160 workgroups, a release/acquire counter barrier per step.  H = 640 only.
+// `sync` = lstm_persistent_sync_bytes() of device memory (reset by the launcher).
+bool lstm_persistent_supported(int H);
+size_t lstm_persistent_sync_bytes();
+void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync,
+                            hipStream_t s);
+
 // head: y = hs[0] + hs[1] (sum merge); out = y W^T + b.  wt (H, n_mels) transposed weight.
 void launch_mel_head(const float* hs, int rows, int H, const float* wt, const float* b, int n_mels,
                      float* out, hipStream_t s);

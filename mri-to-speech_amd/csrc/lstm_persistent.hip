@@ -1,0 +1,197 @@
+// Persistent BiLSTM recurrence: one launch for all T steps of both directions
+// (nn.LSTM(208, 640, bidirectional) in BiLSTMSumMerge, mri_acoustic_model.py:57-71; gate order
+// i, f, g, o; c' = f*c + i*g, h' = o*tanh(c'); h0 = c0 = 0).
+//
+// Layout.  Workgroup (dir, ug) owns hidden units [8 ug, 8 ug + 8) of one direction: the 32 W_hh
+// rows of their four gates stay in VGPRs for the whole launch (each of the 4 waves holds a 160-wide
+// K slice: 80 floats per lane as v_mfma_f32_32x32x2_f32 A fragments), so W_hh (6.5 MB per
+// direction, fp32) is read from HBM once per launch instead of once per step.  H = 640 gives
+// 2 x 80 = 160 co-resident workgroups (one per CU).
+// Per step: every wave loads h_{t-1} for its K slice and 32 sequences per B tile straight into B
+// fragments (lane = (k half, sequence); the K order inside the slice is permuted so a lane reads 80
+// consecutive floats), runs 80 MFMAs per B tile, the four K-slice partials are summed in LDS, and
+// 256 threads apply the cell update for (unit, sequence) pairs.  c stays in LDS; h_t goes to `hs`
+// (the layer output) and is published to the direction's other workgroups by a release/acquire
+// counter barrier (cdna_hip_programming.md Guideline 16): plain stores -> vmcnt(0) -> barrier ->
+// agent release fence -> atomic add; consumers poll relaxed, then one agent acquire fence.
+// Spins are bounded: on timeout the workgroup sets the error word and leaves, so the grid always
+// drains.  Products are exact fp32 (MFMA f32); only the summation order differs from torch.
+#include <algorithm>
+
+#include "kernels.hpp"
+
+namespace m2s {
+namespace {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int LP_H = 640;          // hidden size this kernel is built for
+constexpr int LP_U = 8;            // units per workgroup (32 gate rows = one MFMA M tile)
+constexpr int LP_KW = LP_H / 4;    // K slice per wave
+constexpr int LP_KH = LP_KW / 2;   // floats per lane per B tile (k half = lane / 32)
+constexpr int LP_BT = 2;           // 32-sequence B tiles per pass
+constexpr int LP_BMAX = 64;        // sequences per launch (c in LDS); larger batches: several launches
+constexpr unsigned LP_SPIN_MAX = 1u << 24;
+
+struct LstmSync {
+  unsigned arrive[2];  // per-direction monotonic arrival counters
+  unsigned err;        // set on a barrier timeout
+};
+
+__global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __restrict__ pre,
+                                                                 const float* __restrict__ whh, float* hs,
+                                                                 int Btot, int b0, int B, int T, LstmSync* sync) {
+  __shared__ float red[4][LP_BT][32][33];
+  __shared__ float cst[LP_U][LP_BMAX];
+  __shared__ int abort_flag;
+  const int H = LP_H;
+  const int dir = blockIdx.x / (H / LP_U), ug = blockIdx.x - dir * (H / LP_U);
+  const int nwg = H / LP_U;  // workgroups per direction
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kk = lane >> 5, l32 = lane & 31;
+  const int kbase = wave * LP_KW + kk * LP_KH;  // this lane's 80 consecutive k
+  // sequences [b0, b0 + B) of the (Btot, T, ...) tensors
+  float* hsd = hs + (size_t)dir * Btot * T * H + (size_t)b0 * T * H;
+  pre += (size_t)b0 * T * 8 * H;
+
+  // ---- W_hh rows of this workgroup -> A fragments (resident for the launch) --------------------
+  float wa[LP_KH];
+  {
+    const int r = l32, g = r / LP_U, u = ug * LP_U + (r % LP_U);
+    const float* wr = whh + ((size_t)dir * 4 * H + (size_t)g * H + u) * H + kbase;
+#pragma unroll
+    for (int s = 0; s < LP_KH; s += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(wr + s);
+      wa[s] = v.x;
+      wa[s + 1] = v.y;
+      wa[s + 2] = v.z;
+      wa[s + 3] = v.w;
+    }
+  }
+  for (int i = tid; i < LP_U * LP_BMAX; i += 256) (&cst[0][0])[i] = 0.f;
+  if (tid == 0) abort_flag = 0;
+  __syncthreads();
+
+  unsigned* arrive = &sync->arrive[dir];
+  const int nbt = (B + 31) / 32;
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? step : T - 1 - step;
+    const int tprev = dir == 0 ? t - 1 : t + 1;
+    if (step > 0) {
+      // ---- wait until every workgroup of this direction published h_{t-1} -----------------
+      if (tid == 0) {
+        const unsigned target = (unsigned)step * nwg;
+        unsigned spins = 0;
+        while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > LP_SPIN_MAX ||
+              __hip_atomic_load(&sync->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+            __hip_atomic_store(&sync->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            abort_flag = 1;
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      if (abort_flag) {  // barrier timed out: poison this workgroup's remaining outputs and leave
+        for (int st = step; st < T; ++st) {
+          const int tt = dir == 0 ? st : T - 1 - st;
+          for (int p = tid; p < LP_U * B; p += 256)
+            hsd[((size_t)(p / LP_U) * T + tt) * H + ug * LP_U + p % LP_U] = __builtin_nanf("");
+        }
+        return;
+      }
+    }
+    for (int bt0 = 0; bt0 < nbt; bt0 += LP_BT) {
+      f32x16 acc[LP_BT];
+#pragma unroll
+      for (int j = 0; j < LP_BT; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+      if (step > 0) {
+        float hb[LP_BT][LP_KH];
+#pragma unroll
+        for (int j = 0; j < LP_BT; ++j) {
+          const int b = (bt0 + j) * 32 + l32;
+          const float* hr = hsd + ((size_t)b * T + tprev) * H + kbase;
+#pragma unroll
+          for (int s = 0; s < LP_KH; s += 4) {
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (b < B) v = *reinterpret_cast<const float4*>(hr + s);
+            hb[j][s] = v.x;
+            hb[j][s + 1] = v.y;
+            hb[j][s + 2] = v.z;
+            hb[j][s + 3] = v.w;
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < LP_KH; ++s)
+#pragma unroll
+          for (int j = 0; j < LP_BT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[s], hb[j][s], acc[j], 0, 0, 0);
+      }
+      // ---- K-slice partials -> LDS: acc[i] holds row 8(i/4) + 4 kk + i%4, sequence l32 ---------
+#pragma unroll
+      for (int j = 0; j < LP_BT; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[wave][j][8 * (i / 4) + 4 * kk + (i % 4)][l32] = acc[j][i];
+      __syncthreads();
+      // ---- cell update: thread -> (unit, sequence) pairs of these B tiles ---------------------
+      for (int p = tid; p < LP_U * LP_BT * 32; p += 256) {
+        const int u = p % LP_U, bl = p / LP_U, j = bl / 32, b = bt0 * 32 + bl;
+        if (b >= B) continue;
+        float gs[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int r = g * LP_U + u;
+          gs[g] = (red[0][j][r][bl % 32] + red[1][j][r][bl % 32]) + (red[2][j][r][bl % 32] + red[3][j][r][bl % 32]);
+        }
+        const int unit = ug * LP_U + u;
+        const float* pr = pre + ((size_t)b * T + t) * 8 * H + (size_t)dir * 4 * H;
+        const float gi = sigmoid_exact(pr[unit] + gs[0]);
+        const float gf = sigmoid_exact(pr[H + unit] + gs[1]);
+        const float gg = tanhf(pr[2 * H + unit] + gs[2]);
+        const float go = sigmoid_exact(pr[3 * H + unit] + gs[3]);
+        const float c = step > 0 ? gf * cst[u][b] + gi * gg : gi * gg;
+        cst[u][b] = c;
+        hsd[((size_t)b * T + t) * H + unit] = go * tanhf(c);
+      }
+      __syncthreads();  // red reused by the next B tiles
+    }
+    // ---- publish h_t: stores drained, then one agent-scope release + arrival ------------------
+    if (step + 1 < T) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool lstm_persistent_supported(int H) { return H == LP_H; }
+
+size_t lstm_persistent_sync_bytes() { return 256; }
+
+void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync,
+                            hipStream_t s) {
+  M2S_CHECK(lstm_persistent_supported(H) && B > 0 && T > 0, "lstm_persistent: unsupported shape");
+  const int grid = 2 * (H / LP_U);
+  LstmSync* sp = static_cast<LstmSync*>(sync);
+  for (int b0 = 0; b0 < B; b0 += LP_BMAX) {  // c lives in LDS: at most LP_BMAX sequences per launch
+    int nb = std::min(LP_BMAX, B - b0);
+    M2S_HIP(hipMemsetAsync(sync, 0, lstm_persistent_sync_bytes(), s));
+    void* args[] = {(void*)&pre, (void*)&whh, (void*)&hs, (void*)&B, (void*)&b0, (void*)&nb, (void*)&T, (void*)&sp};
+    // cooperative launch: the runtime checks that all 160 workgroups are co-resident (the barrier
+    // needs it) and rejects an oversize grid instead of letting it deadlock
+    M2S_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&lstm_persistent_kernel), dim3(grid), dim3(256),
+                                       args, 0, s));
+  }
+}
+
+}  // namespace m2s

@@ -70,6 +70,13 @@ static uint16_t f2bf_host(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// Event-profiler record names = the kernels' demangled symbols as rocprofv3 prints them, so the
+// two profiles can be joined on the name.
+template <typename T>
+static std::string tname(const char* base, const char* extra = "") {
+  return std::string(base) + (std::is_same<T, bf16_t>::value ? "<unsigned short" : "<float") + extra + ">";
+}
+
 static int kc_of(int dtype) { return dtype == M2S_DT_BF16 ? Elem<bf16_t>::KC : Elem<float>::KC; }
 
 static PConv make_pconv(int kind, int cin, int cout, int ntaps, int dtype) {
@@ -373,6 +380,7 @@ size_t Acoustic::workspace_bytes(int B, int T, int H, int W) const {
   ws.take<float>(BT * 8 * hidden_);
   ws.take<float>(2 * BT * hidden_);
   ws.take<float>((size_t)2 * B * hidden_);
+  ws.take<char>(lstm_persistent_sync_bytes());
   return ws.used();
 }
 
@@ -406,7 +414,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
     same_pad(H, 3, 2, &oh, &pt);
     same_pad(W, 3, 2, &ow, &pl);
     {
-      ProfScope ps("stem", 2.0 * nc * oh * ow * EFF_STEM * 27, 4.0 * nc * H * W + sizeof(T) * (double)nc * oh * ow * 32, s);
+      ProfScope ps(tname<T>("stem_kernel"), 2.0 * nc * oh * ow * EFF_STEM * 27, 4.0 * nc * H * W + sizeof(T) * (double)nc * oh * ow * 32, s);
       launch_stem<T>(frames + (size_t)n0 * H * W, nc, H, W, oh, ow, pt, pl, static_cast<const float*>(arena_.ptr(stem_w_)),
                      static_cast<const float*>(arena_.ptr(stem_b_)), EFF_STEM, chan_stride(EFF_STEM), A, s);
     }
@@ -480,14 +488,14 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         e.act = ACT_SILU;
         run_conv<T>(e, b.c1, s);
         {
-          ProfScope ps("dwconv_se", 2.0 * nc * nh * nw * b.mid * 9,
+          ProfScope ps(b.stride == 2 ? tname<T>("dwconv_kernel", ", 2") : tname<T>("dwconv_kernel", ", 1"), 2.0 * nc * nh * nw * b.mid * 9,
                        sizeof(T) * (double)nc * (oh * ow + nh * nw) * b.mid, s);
           launch_dwconv<T>(M, nc, oh, ow, nh, nw, b.stride, qt, ql, b.mid, cs,
                            static_cast<const float*>(arena_.ptr(b.dw_w)), static_cast<const float*>(arena_.ptr(b.dw_b)),
                            M2, sums, s);
         }
         {
-          ProfScope ps("se_mean", 0.0, 4.0 * nc * cs * dw_pixel_blocks(nh, nw) + sizeof(T) * (double)nc * cs, s);
+          ProfScope ps(tname<T>("se_mean_kernel"), 0.0, 4.0 * nc * cs * dw_pixel_blocks(nh, nw) + sizeof(T) * (double)nc * cs, s);
           launch_se_mean<T>(sums, nc, dw_pixel_blocks(nh, nw), cs, 1.0f / (float)(nh * nw), se_mean, s);
         }
         }
@@ -524,7 +532,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
       }
     }
     if (stopped || !feats) continue;
-    ProfScope ps("gap", (double)nc * oh * ow * cc, sizeof(T) * (double)nc * oh * ow * cc, s);
+    ProfScope ps(tname<T>("gap_kernel"), (double)nc * oh * ow * cc, sizeof(T) * (double)nc * oh * ow * cc, s);
     launch_gap<T>(cur, nc, oh * ow, cc, chan_stride(cc), feats + (size_t)n0 * EFF_OUT, s);
   }
 }
@@ -541,12 +549,22 @@ void Acoustic::bilstm(const float* feats, int B, int T, float* y, float* mel_nor
   a.y = pre;
   a.M = (int)BT;
   run_conv<float>(a, lstm_ih_, s);
-  for (int st = 0; st < T; ++st) {
-    ProfScope ps("lstm_step", 2.0 * 2 * B * 4.0 * H * H, 4.0 * 2 * 4 * H * H, s);
-    launch_lstm_step(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, cst, B, T, H, st, s);
+  void* sync = ws.take<char>(lstm_persistent_sync_bytes());
+  const char* pe = std::getenv("M2S_LSTM_PERSISTENT");  // "0": one launch per time step
+  const bool persistent = !pe || std::strcmp(pe, "0") != 0;
+  if (persistent && lstm_persistent_supported(H)) {
+    // algorithmic bytes: W_hh of both directions once, gate pre-activations in, h out
+    ProfScope ps("lstm_persistent_kernel", 2.0 * 2 * B * 4.0 * H * H * (T - 1),
+                 4.0 * 2 * 4 * H * H + 4.0 * BT * (8.0 * H + 2.0 * H), s);
+    launch_lstm_persistent(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, s);
+  } else {
+    for (int st = 0; st < T; ++st) {
+      ProfScope ps("lstm_step_kernel", 2.0 * 2 * B * 4.0 * H * H, 4.0 * 2 * 4 * H * H, s);
+      launch_lstm_step(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, cst, B, T, H, st, s);
+    }
   }
   if (mel_norm) {
-    ProfScope ps("mel_head", 2.0 * BT * H * n_mels_, 4.0 * BT * (2 * H + n_mels_), s);
+    ProfScope ps("mel_head_kernel", 2.0 * BT * H * n_mels_, 4.0 * BT * (2 * H + n_mels_), s);
     launch_mel_head(hs, (int)BT, H, static_cast<const float*>(arena_.ptr(head_wt_)),
                     static_cast<const float*>(arena_.ptr(head_b_)), n_mels_, mel_norm, s);
   }
@@ -712,7 +730,7 @@ void Vocoder::forward_from_norm(const float* mel_norm, const float* mean, const 
   ws.take<char>((size_t)B * T * cs * (dtype_ == M2S_DT_BF16 ? 2 : 4));  // same carve as forward()
   const bool bf = dtype_ == M2S_DT_BF16;
   {
-    ProfScope ps("mel_glue", 0.0, 4.0 * B * T * nm * 4, s);
+    ProfScope ps(bf ? "mel_glue_kernel<unsigned short>" : "mel_glue_kernel<float>", 0.0, 4.0 * B * T * nm * 4, s);
     if (bf)
       launch_mel_glue<bf16_t>(mel_norm, B * T, nm, mean, std_, mel_db, mel_log, static_cast<bf16_t*>(ln_buf), cs, s);
     else
@@ -790,7 +808,7 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
       }
     }
   }
-  ProfScope ps("conv_post", 2.0 * B * L * post_c_ * 7, sizeof(T) * (double)B * L * post_c_ + 4.0 * B * L, s);
+  ProfScope ps(tname<T>("conv_post_kernel"), 2.0 * B * L * post_c_ * 7, sizeof(T) * (double)B * L * post_c_ + 4.0 * B * L, s);
   launch_conv_post<T>(S, B, L, post_c_, chan_stride(post_c_), static_cast<const float*>(arena_.ptr(post_w_)), post_b_,
                       wav, s);
 }

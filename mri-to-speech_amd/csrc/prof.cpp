@@ -42,7 +42,7 @@ Prof& P() {
 
 bool prof_on() { return P().on; }
 
-ProfScope::ProfScope(const char* name, double flops, double bytes, hipStream_t s) : s_(s) {
+ProfScope::ProfScope(const std::string& name, double flops, double bytes, hipStream_t s) : s_(s) {
   Prof& p = P();
   if (!p.on) return;
   std::lock_guard<std::mutex> g(p.mu);

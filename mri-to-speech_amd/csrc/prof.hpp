@@ -11,7 +11,7 @@ bool prof_on();
 // Brackets one kernel launch with HIP events on `s` when profiling is enabled.
 class ProfScope {
  public:
-  ProfScope(const char* name, double flops, double bytes, hipStream_t s);
+  ProfScope(const std::string& name, double flops, double bytes, hipStream_t s);
   ~ProfScope();
 
  private:

@@ -228,3 +228,23 @@ def test_pipeline_end_to_end(rt, ac_state, dtype):
     else:
         assert np.abs(got["mel_norm"] - mn.numpy()).max() <= 5e-2
         assert _snr_db(wav[:, 0].numpy(), got["wav"]) >= 20.0
+
+
+# ------------------------------------------------------------------------------ persistent BiLSTM
+@pytest.mark.parametrize("B,T", [(1, 1000), (3, 64), (70, 6)])
+def test_bilstm_persistent_long_and_wide(ac_f32, ac_state, monkeypatch, B, T):
+    """One-launch recurrence (lstm_persistent.hip) vs the oracle and vs the per-step kernel:
+    a 1000-frame clip (configs[4] length), a batch above the 64-sequence launch limit."""
+    sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
+    x = torch.from_numpy(np.random.default_rng(B * 7 + T).normal(0, 0.5, (B, T, 208)).astype(np.float32))
+    monkeypatch.setenv("M2S_LSTM_PERSISTENT", "1")
+    y, m = ac_f32.bilstm(x.to(DEV))
+    monkeypatch.setenv("M2S_LSTM_PERSISTENT", "0")
+    y_step, _ = ac_f32.bilstm(x.to(DEV))
+    ref_y = acoustic.bilstm_summerge(sd, x).numpy()
+    y = y.cpu().numpy()
+    assert np.isfinite(y).all()
+    tol = 2e-5 if T <= 64 else 1e-4  # fp32 summation order over 1000 recurrent steps
+    np.testing.assert_allclose(y, ref_y, atol=tol, rtol=0)
+    np.testing.assert_allclose(y, y_step.cpu().numpy(), atol=tol, rtol=0)
+    np.testing.assert_allclose(m.cpu().numpy(), acoustic.head(sd, torch.from_numpy(ref_y)).numpy(), atol=5 * tol, rtol=0)
