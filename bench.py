@@ -38,6 +38,23 @@ PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA peaks, MI355X_MICROA
 PEAK_HBM_GBS = 8000.0
 
 
+MFMA_KERNELS = ("conv_gemm_kernel", "conv_halo_kernel", "conv_igemm_kernel", "ir_pwdw_kernel", "lstm_persistent_kernel")
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest profiles/*pmc_traffic.json (rocprofv3
+    FETCH_SIZE x2 + WRITE_SIZE passes over the same workload, tools/gpu_pmc.sh + tools/pmc_traffic.py)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        k = json.load(fh)["kernels"].get(kernel)
+    if not k:
+        return None, None
+    return round(k["hbm_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -180,24 +197,31 @@ def main():
         stats = _native.prof_collect()
         tot_ms = sum(s["ms"] for s in stats)
         dom = max(stats, key=lambda s: s["ms"])
-        mfma = dom["name"].startswith("conv_")
-        if mfma:
+        # bound = the roof its algorithmic intensity hits first (ridge = peak FLOP/s / HBM B/s)
+        peak_tf = PEAK_TFLOPS["fp32" if args.dtype == "fp32" or "float" in dom["name"] else "bf16"]
+        ridge = peak_tf * 1e12 / (PEAK_HBM_GBS * 1e9)
+        if dom["bytes"] <= 0 or dom["flops"] / dom["bytes"] > ridge:
             achieved = dom["flops"] / (dom["ms"] * 1e-3) / 1e12
-            peak = PEAK_TFLOPS["bf16" if "bf16" in dom["name"] else "fp32"]
-            unit, bound = "TFLOP/s", "mfma"
+            peak, unit, bound = peak_tf, "TFLOP/s", "mfma"
         else:
             achieved = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9
             peak, unit, bound = PEAK_HBM_GBS, "GB/s", "hbm"
-        conv_ms = sum(s["ms"] for s in stats if s["name"].startswith("conv_") and "post" not in s["name"])
-        conv_fl = sum(s["flops"] for s in stats if s["name"].startswith("conv_") and "post" not in s["name"])
+        mm = [s for s in stats if s["name"].startswith(MFMA_KERNELS)]
+        mm_ms, mm_fl = sum(s["ms"] for s in mm), sum(s["flops"] for s in mm)
+        traffic, tsrc = pmc_traffic(dom["name"])
         result["roofline"] = {
             "bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": None,
+            "frac": round(achieved / peak, 4), "traffic": traffic,
             "kernel": dom["name"], "launches_per_step": dom["launches"] // args.steps,
             "avg_launch_us": round(1000.0 * dom["ms"] / dom["launches"], 2),
+            "algorithmic_bytes_per_launch": round(dom["bytes"] / dom["launches"]),
+            "algorithmic_flop_per_launch": round(dom["flops"] / dom["launches"]),
             "kernel_share_of_gpu_time": round(dom["ms"] / tot_ms, 3),
-            "all_conv_igemm_tflops": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2),
+            "all_mfma_kernels_tflops": round(mm_fl / (mm_ms * 1e-3) / 1e12, 2),
+            "e2e_tflops": round(3.831e9 * fps / 1e12, 2),
         }
+        if tsrc:
+            result["roofline"]["traffic_source"] = tsrc
         if rank == 0 and os.environ.get("M2S_BENCH_KERNELS"):
             for s in sorted(stats, key=lambda s: -s["ms"]):
                 print(f"# {s['name']:40s} n={s['launches']:6d} ms={s['ms']:9.3f} "
@@ -211,6 +235,9 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    # release the engines' device memory while the HIP runtime is still up
+    del pipe, ac, voc, frames, out
+    torch.cuda.synchronize(device)
 
 
 if __name__ == "__main__":

@@ -104,6 +104,12 @@ typedef struct m2s_hifigan_h {
 typedef struct m2s_vocoder m2s_vocoder;
 /* Packs a Generator state dict (weight_g/weight_v or plain weight after remove_weight_norm).
  * Strict like load_state_dict(ckpt['generator']): a missing key is M2S_E_ARG.  Synchronous. */
+/* Frame preprocessing after the host decode (replaces _preprocess_frame,
+ * run_mri_video_inference.py:34-54, except the cv2.resize): frames uint8 (n,h,w) grey
+ * (channels = 1) or (n,h,w,3) BGR (channels = 3) -> out (n,h,w) fp32, per frame z-score then
+ * min-max to [0, 1]; a constant frame gives zeros.  Device pointers, stream-ordered. */
+int m2s_preprocess_frames(const uint8_t* frames, int n, int h, int w, int channels, float* out, void* stream);
+
 int m2s_vocoder_create(const m2s_tensor* sd, int n, const m2s_hifigan_h* h, int dtype, int device, m2s_vocoder** out);
 void m2s_vocoder_destroy(m2s_vocoder* v);
 size_t m2s_vocoder_workspace_bytes(const m2s_vocoder* v, int B, int T);

@@ -153,6 +153,13 @@ int m2s_mel_glue(const float* mel_norm, int rows, int n_mels, const float* mean,
   });
 }
 
+int m2s_preprocess_frames(const uint8_t* frames, int n, int h, int w, int channels, float* out, void* stream) {
+  return guarded([&] {
+    M2S_CHECK(frames && out && n >= 0 && h > 0 && w > 0 && (channels == 1 || channels == 3), "bad argument");
+    m2s::launch_preprocess(frames, n, h, w, channels, out, S(stream));
+  });
+}
+
 int m2s_vocoder_create(const m2s_tensor* sd, int n, const m2s_hifigan_h* h, int dtype, int device, m2s_vocoder** out) {
   return guarded([&] {
     M2S_CHECK(out && h && (sd || n == 0), "null argument");

@@ -1,5 +1,7 @@
 // Non-GEMM kernels of the hot path: stem, depthwise+SE, GAP, BiLSTM recurrence, head, mel glue,
 // vocoder input/output edges.  All are HBM/latency-bound; each reads its input once.
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace m2s {
@@ -36,47 +38,54 @@ __device__ __forceinline__ float act_silu(float v) {
 
 // ---------------------------------------------------------------------------------------------
 // stem: four lanes per output pixel, 8 channels each, so one wave's stores cover 16 whole pixel
-// rows (1 KB contiguous in bf16) instead of 64 partial ones.  TF-SAME pads passed from the host.
+// rows (1 KB contiguous in bf16) instead of 64 partial ones.  A lane keeps its 8 channels' 72
+// taps + 8 biases in registers and walks pixels grid-stride (weights from LDS per pixel made the
+// kernel LDS-issue bound).  TF-SAME pads passed from the host.
 template <typename T>
 __global__ void __launch_bounds__(256) stem_kernel(const float* __restrict__ frames, int N, int H, int W, int OH,
                                                    int OW, int pad_t, int pad_l, const float* __restrict__ w9,
                                                    const float* __restrict__ bias, int cout, int cs_out,
                                                    T* __restrict__ y) {
-  __shared__ float sw[32 * 9 + 32];
-  for (int i = threadIdx.x; i < 32 * 9 + 32; i += 256)
-    sw[i] = i < 32 * 9 ? (i / 9 < cout ? w9[i] : 0.f) : (i - 288 < cout ? bias[i - 288] : 0.f);
-  __syncthreads();
-  const long p = ((long)blockIdx.x * 256 + threadIdx.x) >> 2;
   const int o0 = (threadIdx.x & 3) * 8;
-  const long total = (long)N * OH * OW;
-  if (p >= total || o0 >= cs_out) return;
-  const int hw = OH * OW;
-  const int n = (int)(p / hw);
-  const int rem = (int)(p - (long)n * hw);
-  const int oy = rem / OW, ox = rem - (rem / OW) * OW;
-  float in[9];
-#pragma unroll
-  for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int iy = oy * 2 - pad_t + ky, ix = ox * 2 - pad_l + kx;
-      in[ky * 3 + kx] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? frames[((long)n * H + iy) * W + ix] : 0.f;
-    }
-  float v[8];
+  if (o0 >= cs_out) return;
+  float w[8][9], bb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    float acc = 0.f;
+    const bool ok = o0 + j < cout;
 #pragma unroll
-    for (int t = 0; t < 9; ++t) acc += sw[(o0 + j) * 9 + t] * in[t];
-    v[j] = act_silu<T>(acc + sw[288 + o0 + j]);
+    for (int t = 0; t < 9; ++t) w[j][t] = ok ? w9[(o0 + j) * 9 + t] : 0.f;
+    bb[j] = ok ? bias[o0 + j] : 0.f;
   }
-  T* out = y + p * cs_out + o0;
-  if constexpr (sizeof(T) == 4) {
-    *reinterpret_cast<float4*>(out) = make_float4(v[0], v[1], v[2], v[3]);
-    *reinterpret_cast<float4*>(out + 4) = make_float4(v[4], v[5], v[6], v[7]);
-  } else {
-    *reinterpret_cast<uint4*>(out) =
-        make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+  const long total = (long)N * OH * OW;
+  const int hw = OH * OW;
+  for (long p = ((long)blockIdx.x * 256 + threadIdx.x) >> 2; p < total; p += (long)gridDim.x * 64) {
+    const int n = (int)(p / hw);
+    const int rem = (int)(p - (long)n * hw);
+    const int oy = rem / OW, ox = rem - (rem / OW) * OW;
+    float in[9];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int iy = oy * 2 - pad_t + ky, ix = ox * 2 - pad_l + kx;
+        in[ky * 3 + kx] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? frames[((long)n * H + iy) * W + ix] : 0.f;
+      }
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc += w[j][t] * in[t];
+      v[j] = act_silu<T>(acc + bb[j]);
+    }
+    T* out = y + p * cs_out + o0;
+    if constexpr (sizeof(T) == 4) {
+      *reinterpret_cast<float4*>(out) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(out + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      *reinterpret_cast<uint4*>(out) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                                  pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+    }
   }
 }
 
@@ -262,7 +271,8 @@ template <typename T>
 void launch_stem(const float* frames, int N, int H, int W, int OH, int OW, int pad_t, int pad_l, const float* w9,
                  const float* bias, int cout, int cs_out, T* y, hipStream_t s) {
   M2S_CHECK(cout <= 32 && cs_out % 8 == 0 && cs_out <= 32, "stem: unsupported channel count");
-  hipLaunchKernelGGL(stem_kernel<T>, dim3(nblk(4L * N * OH * OW)), dim3(256), 0, s, frames, N, H, W, OH, OW, pad_t,
+  const long blocks = std::min<long>(nblk(4L * N * OH * OW), 256L * 16);
+  hipLaunchKernelGGL(stem_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, s, frames, N, H, W, OH, OW, pad_t,
                      pad_l, w9, bias, cout, cs_out, y);
   M2S_HIP(hipGetLastError());
 }

@@ -33,6 +33,10 @@ void launch_ir_pwdw(const bf16_t* x, int N, int cs_in, int kp, const bf16_t* wpw
                     const uint32_t* wdw2, const float* bdw, int OH, int OW, int cs_mid, bf16_t* y, bf16_t* se_mean,
                     double flops, double bytes, hipStream_t s);
 
+// Decoded frames -> model input: uint8 (N,H,W) grey or (N,H,W,3) BGR -> fp32 (N,H,W) in [0, 1]
+// (_preprocess_frame, run_mri_video_inference.py:34-54, minus the host-side resize).  (preprocess.hip)
+void launch_preprocess(const uint8_t* frames, int N, int H, int W, int channels, float* out, hipStream_t s);
+
 // Global average pool: x (N,P,cs) T -> feats (N,C) fp32 (dense, row stride C).
 template <typename T>
 void launch_gap(const T* x, int N, int P, int C, int cs, float* feats, hipStream_t s);

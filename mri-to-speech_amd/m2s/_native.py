@@ -66,6 +66,7 @@ def lib():
         "m2s_effnet_probe": (i, [vp, fp, i, i, i, i, fp, C.POINTER(i), C.POINTER(i), C.POINTER(i), vp, sz, vp]),
         "m2s_bilstm_summerge": (i, [vp, fp, i, i, fp, fp, vp, sz, vp]),
         "m2s_mel_glue": (i, [fp, i, i, fp, fp, fp, fp, vp]),
+        "m2s_preprocess_frames": (i, [fp, i, i, i, i, fp, vp]),
         "m2s_vocoder_create": (i, [C.POINTER(Tensor), i, C.POINTER(HifiganH), i, i, C.POINTER(vp)]),
         "m2s_vocoder_destroy": (None, [vp]),
         "m2s_vocoder_workspace_bytes": (sz, [vp, i, i]),
@@ -95,7 +96,7 @@ def exported_symbols() -> List[str]:
     return [n for n in ("m2s_abi_version", "m2s_last_error", "m2s_device_check", "m2s_acoustic_create",
                         "m2s_acoustic_destroy", "m2s_acoustic_set_chunk", "m2s_acoustic_workspace_bytes",
                         "m2s_acoustic_forward", "m2s_effnet_forward", "m2s_effnet_probe", "m2s_bilstm_summerge",
-                        "m2s_mel_glue", "m2s_vocoder_create", "m2s_vocoder_destroy",
+                        "m2s_mel_glue", "m2s_preprocess_frames", "m2s_vocoder_create", "m2s_vocoder_destroy",
                         "m2s_vocoder_workspace_bytes", "m2s_vocoder_forward", "m2s_pipeline_workspace_bytes",
                         "m2s_pipeline_forward", "m2s_prof_enable", "m2s_prof_collect")]
 

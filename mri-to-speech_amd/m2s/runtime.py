@@ -187,6 +187,26 @@ def mel_glue(mel_norm: torch.Tensor, mean: torch.Tensor, std: torch.Tensor):
     return db, ln
 
 
+def preprocess_frames(frames: torch.Tensor) -> torch.Tensor:
+    """Decoded uint8 frames on the device, (T,H,W) grey or (T,H,W,3) BGR -> (T,H,W) fp32 in [0, 1]
+    (_preprocess_frame, run_mri_video_inference.py:34-54; resizing stays on the host)."""
+    if frames.dtype != torch.uint8:
+        raise N.M2SError(f"expected uint8 frames, got {frames.dtype}")
+    if frames.device.type != "cuda":
+        raise N.M2SError("preprocess_frames runs on the HIP device; move the decoded frames there first")
+    x = frames.contiguous()
+    if x.dim() == 4 and x.shape[-1] == 3:
+        ch = 3
+    elif x.dim() == 3:
+        ch = 1
+    else:
+        raise N.M2SError(f"expected (T,H,W) or (T,H,W,3) frames, got {tuple(x.shape)}")
+    n, h, w = x.shape[:3]
+    out = torch.empty(n, h, w, dtype=torch.float32, device=x.device)
+    N.check(N.lib().m2s_preprocess_frames(_ptr(x), n, h, w, ch, _ptr(out), _stream(x.device)))
+    return out
+
+
 class Pipeline:
     """frames -> (mel_norm, mel_db, mel_log, wav) on one stream (run_mri_video_inference.py:218-242)."""
 

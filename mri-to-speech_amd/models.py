@@ -136,9 +136,13 @@ class Generator(nn.Module):
         return self._eng
 
     def forward(self, x):
-        """(B, num_mels, T) ln-mel -> (B, 1, T * prod(upsample_rates)) waveform in [-1, 1]."""
+        """(B, num_mels, T) ln-mel -> (B, 1, T * prod(upsample_rates)) waveform in [-1, 1].
+        An unbatched (num_mels, T) mel gives (1, T * hop), as torch's unbatched conv1d chain does
+        for the reference module (inference_e2e.py:48-50 passes the stored (64, T) arrays as is)."""
         if torch.is_grad_enabled() and x.requires_grad:
             raise NotImplementedError("m2s generator has no autograd; run under torch.no_grad()")
+        if x.dim() == 2:
+            return self._engine(x.device).forward(x.unsqueeze(0), layout=0)[0]
         return self._engine(x.device).forward(x, layout=0)
 
     def remove_weight_norm(self):

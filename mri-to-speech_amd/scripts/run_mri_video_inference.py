@@ -30,7 +30,7 @@ if str(PROJECT_ROOT) not in sys.path:
 
 from env import AttrDict  # noqa: E402
 from models import Generator  # noqa: E402
-from m2s.runtime import mel_glue  # noqa: E402
+from m2s.runtime import mel_glue, preprocess_frames  # noqa: E402
 
 try:  # optional host-side decoders, exactly as the reference uses them
     import cv2  # noqa: F401
@@ -66,6 +66,50 @@ def _preprocess_frame(frame: np.ndarray, target_size=(256, 256)) -> np.ndarray:
     gray = (gray - mean) / std if std > 0 else gray - mean
     lo, hi = gray.min(), gray.max()
     return (gray - lo) / (hi - lo) if hi > lo else np.zeros_like(gray)
+
+
+def decode_video_frames(video_path: Path, target_size=(256, 256), max_frames=None) -> np.ndarray:
+    """Host half of load_video_frames: decoded uint8 frames, (T,H,W) grey or (T,H,W,3) BGR at
+    `target_size`.  Frames of another size are converted to grey and resized here (cv2, as the
+    reference does); the z-score / min-max normalisation runs on the device
+    (m2s.runtime.preprocess_frames)."""
+    if video_path.suffix.lower() == ".npy":
+        raw = np.load(video_path, allow_pickle=False)
+        if max_frames is not None:
+            raw = raw[:max_frames]
+        raw = list(raw)
+    else:
+        if cv2 is None:
+            raise RuntimeError("OpenCV is not installed; pass the frames as a .npy (T,H,W) array instead")
+        cap = cv2.VideoCapture(str(video_path))
+        if not cap.isOpened():
+            raise ValueError(f"Unable to open video: {video_path}")
+        total = int(cap.get(cv2.CAP_PROP_FRAME_COUNT))
+        if max_frames is not None:
+            total = min(total, max_frames)
+        raw = []
+        for _ in range(total):
+            ret, frame = cap.read()
+            if not ret:
+                break
+            raw.append(frame)
+        cap.release()
+    if not len(raw):
+        raise ValueError("No frames could be read from video")
+    out = []
+    for f in raw:
+        f = np.asarray(f)
+        if f.dtype != np.uint8:
+            raise ValueError(f"expected 8-bit frames, got {f.dtype}")
+        if f.shape[:2][::-1] != tuple(target_size):
+            if cv2 is None:
+                raise ValueError(f"frame size {f.shape[:2]} != {target_size} and OpenCV is not installed to resize")
+            g = cv2.cvtColor(f, cv2.COLOR_BGR2GRAY) if f.ndim == 3 else f
+            f = cv2.resize(g, target_size, interpolation=cv2.INTER_LINEAR)
+        out.append(f)
+    if len({a.shape for a in out}) != 1:
+        out = [cv2.cvtColor(a, cv2.COLOR_BGR2GRAY) if a.ndim == 3 else a for a in out]
+    return np.ascontiguousarray(np.stack(out))
 
 
 def load_video_frames(video_path: Path, target_size=(256, 256), max_frames=None) -> torch.Tensor:
@@ -242,8 +286,10 @@ def main(argv=None):
     device = torch.device("cuda")
     print(f"[INFO] Using device: {device}")
 
-    frames = load_video_frames(video_path, target_size=(256, 256), max_frames=args.max_frames)
-    frames_tensor = frames_to_tensor(frames, use_channel=True).to(device)
+    # host: decode (+ resize when needed); device: grey, z-score, min-max (libm2s preprocess kernel)
+    frames_u8 = decode_video_frames(video_path, target_size=(256, 256), max_frames=args.max_frames)
+    frames = preprocess_frames(torch.from_numpy(frames_u8).to(device))
+    frames_tensor = frames_to_tensor(frames, use_channel=True)
 
     mri_model = build_mri_model(args, device)
     with torch.no_grad():

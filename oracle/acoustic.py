@@ -10,7 +10,10 @@ TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
   against tests/golden/acoustic.npz produced by the reference module itself.
 * ``head`` restates mri_acoustic_model.py:103,135 (``nn.Linear(640, n_mels)``).
 * ``preprocess_frame`` restates scripts/run_mri_video_inference.py:34-54 for grey
-  frames already at the target size (cv2 colour conversion / resize not exercised).
+  frames already at the target size (resize not exercised).  ``bgr_to_grey`` restates the
+  cv2.cvtColor(COLOR_BGR2GRAY) call at :36 as OpenCV's published 8-bit fixed-point formula
+  (Y = (1868 B + 9617 G + 4899 R + 2^13) >> 14); cv2 is not installed, so that step is parity
+  unpinned.
 * ``denormalize_mel`` / ``mel_db_to_log`` restate run_mri_video_inference.py:160-163 and
   the inline glue at :227-233 (10**(x/10) -> clamp(min=1e-5) -> ln).
 """
@@ -79,6 +82,12 @@ def preprocess_frame(gray: np.ndarray) -> np.ndarray:
     g = (g - mean) / std if std > 0 else g - mean
     lo, hi = g.min(), g.max()
     return (g - lo) / (hi - lo) if hi > lo else np.zeros_like(g)
+
+
+def bgr_to_grey(frame: np.ndarray) -> np.ndarray:
+    """cv2.COLOR_BGR2GRAY for uint8 (H,W,3) BGR (run_mri_video_inference.py:36)."""
+    f = frame.astype(np.int64)
+    return ((1868 * f[..., 0] + 9617 * f[..., 1] + 4899 * f[..., 2] + (1 << 13)) >> 14).astype(np.uint8)
 
 
 def denormalize_mel(mel_norm: torch.Tensor, mean: np.ndarray, std: np.ndarray) -> torch.Tensor:

@@ -248,3 +248,23 @@ def test_bilstm_persistent_long_and_wide(ac_f32, ac_state, monkeypatch, B, T):
     np.testing.assert_allclose(y, ref_y, atol=tol, rtol=0)
     np.testing.assert_allclose(y, y_step.cpu().numpy(), atol=tol, rtol=0)
     np.testing.assert_allclose(m.cpu().numpy(), acoustic.head(sd, torch.from_numpy(ref_y)).numpy(), atol=5 * tol, rtol=0)
+
+
+# ------------------------------------------------------------------------------ frame preprocessing
+def test_preprocess_matches_reference_golden(rt):
+    """Device _preprocess_frame (preprocess.hip) vs the reference's own outputs (glue.npz)."""
+    g = _gold("glue.npz")
+    out = rt.preprocess_frames(torch.from_numpy(g["frames_u8"]).to(DEV)).cpu().numpy()
+    np.testing.assert_allclose(out, g["preprocessed"], atol=1e-6, rtol=0)
+
+
+@pytest.mark.parametrize("shape", [(5, 256, 256), (2, 67, 101), (3, 256, 256, 3)])
+def test_preprocess_vs_oracle_shapes_and_bgr(rt, shape):
+    rng = np.random.default_rng(len(shape) * 100 + shape[1])
+    u8 = rng.integers(0, 256, size=shape, dtype=np.uint8)
+    u8[0] = 77  # a constant frame: zeros (reference :52-53)
+    out = rt.preprocess_frames(torch.from_numpy(u8).to(DEV)).cpu().numpy()
+    grey = np.stack([acoustic.bgr_to_grey(f) for f in u8]) if len(shape) == 4 else u8
+    ref = np.stack([acoustic.preprocess_frame(f) for f in grey])
+    assert out.shape == ref.shape and not out[0].any()
+    np.testing.assert_allclose(out, ref, atol=1e-6, rtol=0)

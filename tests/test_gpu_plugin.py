@@ -113,3 +113,77 @@ def test_cli_end_to_end(tmp_path, dtype):
         np.testing.assert_allclose(res["audio"], wav, atol=2e-4, rtol=0)
     else:
         assert np.abs(mel_db - db.numpy()).max() < 1.0  # dB; mel_norm x std(<=15) amplifies bf16 error
+
+
+def _load(relpath, name):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(REPO, "mri-to-speech_amd", relpath))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_export_predicted_mels(tmp_path):
+    """scripts/export_predicted_mels.py drop-in: samples/*/mri.npy (/255 frames) -> (64, T) ln-mel
+    per sample (export_predicted_mels.py:84-99), equal-length samples batched, vs the oracle."""
+    ac_sd = synth.synth_acoustic_state(6)
+    mean, std = synth.synth_scaler()
+    ck = tmp_path / "best.pt"
+    torch.save({"model_state_dict": _t(ac_sd)}, ck)
+    (tmp_path / "scaler.json").write_text(json.dumps({"mean": mean.tolist(), "std": std.tolist(), "count_frames": 9}))
+    rng = np.random.default_rng(3)
+    lens = {"utt_a": 5, "utt_b": 3, "utt_c": 5}
+    for stem, T in lens.items():
+        d = tmp_path / "proc" / "samples" / stem
+        d.mkdir(parents=True)
+        np.save(d / "mri.npy", (rng.integers(0, 256, (T, 256, 256)) / 255.0).astype(np.float32))
+    (tmp_path / "proc" / "samples" / "utt_nomri").mkdir()
+    mod = _load(os.path.join("scripts", "export_predicted_mels.py"), "m2s_export_mels")
+    out_dir = tmp_path / "mels"
+    written = mod.main(["--processed_dir", str(tmp_path / "proc"), "--mri_checkpoint", str(ck),
+                        "--scaler_json", str(tmp_path / "scaler.json"), "--output_dir", str(out_dir),
+                        "--mri_code_dir", os.path.join(REPO, "mri-to-speech_amd", "mri2speech_code")])
+    assert sorted(p.name for p in written) == ["utt_a.npy", "utt_b.npy", "utt_c.npy"]
+    sd = _t(ac_sd)
+    for stem, T in lens.items():
+        fr = torch.from_numpy(np.load(tmp_path / "proc" / "samples" / stem / "mri.npy"))
+        f = effnet.effnet_gap(sd, fr).view(1, T, -1)
+        mn = acoustic.head(sd, acoustic.bilstm_summerge(sd, f))[0]
+        ref = acoustic.mel_db_to_log(acoustic.denormalize_mel(mn, mean, std)).t().numpy()
+        got = np.load(out_dir / f"{stem}.npy")
+        assert got.shape == (64, T) and got.dtype == np.float32
+        np.testing.assert_allclose(got, ref, atol=5e-4, rtol=0)
+    # existing outputs are kept unless --overwrite
+    assert mod.main(["--processed_dir", str(tmp_path / "proc"), "--mri_checkpoint", str(ck),
+                     "--scaler_json", str(tmp_path / "scaler.json"), "--output_dir", str(out_dir)]) == []
+
+
+def test_vocoder_only_callers(tmp_path):
+    """inference_e2e.py and mel_to_audio_synthesis.py drop-ins: (64, T) ln-mel files -> wav."""
+    from scipy.io import wavfile
+    gen_sd = synth.synth_generator_state(8)
+    ckdir = tmp_path / "cp"
+    ckdir.mkdir()
+    torch.save({"generator": _t(gen_sd)}, ckdir / "g_00000010")
+    cfg = dict(HIFIGAN_H, seed=1234, sampling_rate=11413, n_fft=1024, hop_size=420, win_size=1024)
+    (ckdir / "config.json").write_text(json.dumps(cfg))
+    mels = tmp_path / "mels"
+    mels.mkdir()
+    mel = synth.synth_mel_log(1, 64, 11, seed=2)[0]
+    np.save(mels / "utt_mel.npy", mel)
+    ref = hifigan.generator(_t(gen_sd), HIFIGAN_H, torch.from_numpy(mel)[None])[0, 0].numpy()
+
+    e2e = _load("inference_e2e.py", "m2s_inference_e2e")
+    out = e2e.main(["--input_mels_dir", str(mels), "--output_dir", str(tmp_path / "e2e"),
+                    "--checkpoint_file", str(ckdir / "g_00000010")])
+    sr, pcm = wavfile.read(out[0])
+    assert sr == 11413 and pcm.dtype == np.int16 and pcm.shape == (11 * 420,)
+    np.testing.assert_allclose(pcm.astype(np.float64), (ref * 32768.0).astype(np.int16), atol=8)
+
+    syn = _load("mel_to_audio_synthesis.py", "m2s_mel_to_audio")
+    done = syn.main(["--input", str(mels), "--checkpoint_file", str(ckdir / "g_00000010"),
+                     "--config", str(ckdir / "config.json"), "--output_dir", str(tmp_path / "syn")])
+    assert done == ["utt"]
+    stats = json.loads((tmp_path / "syn" / "utt_synthesis_stats.json").read_text())
+    assert stats["audio_shape"] == [11 * 420] and stats["sampling_rate"] == 11413
+    for f in ("utt_from_mel.wav", "mel_synthesis_results.html", "overall_synthesis_stats.json"):
+        assert (tmp_path / "syn" / f).exists(), f
