@@ -109,38 +109,65 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a, int n_
   const int nsteps = a.kp / 32;
 
   // ---- DMA roles: lane -> (row within a 16-row block, physical chunk) -------------------------
+  // Per A row the geometry is resolved once: `rbase` = element offset of the row's tap-0 input
+  // position (may lie outside the tensor) and `rmask` bit t = tap t reads inside the tensor (the
+  // TF-SAME / causal / look-ahead zero padding).  Per K step a lane then needs only its tap's
+  // uniform offset, one bit test and one add per row (the address math used to be ~40 VALU per
+  // row per step, which made VALU issue, not the MFMA, the limit of these kernels).
   const int lrow = lane >> 2;
   const int q = (lane & 3) ^ ((lane >> 4) & 3);  // logical chunk this lane fetches ((row>>2)&3 = lane>>4 & 3)
-  int rb[A_PER_WAVE], rp0[A_PER_WAVE], rp1[A_PER_WAVE];
-  bool rok[A_PER_WAVE];
+  int rbase[A_PER_WAVE];
+  uint32_t rmask[A_PER_WAVE];
   const int delta = (KIND == KIND_CONVT) ? (phase + a.ct_pad) / a.ct_u : 0;
 #pragma unroll
   for (int j = 0; j < A_PER_WAVE; ++j) {
     const int m = m0 + (wave * A_PER_WAVE + j) * 16 + lrow;
-    rok[j] = m < a.M;
-    const int mm = rok[j] ? m : 0;
+    const bool ok = m < a.M;
+    const int mm = ok ? m : 0;
+    uint32_t msk = 0;
     if constexpr (KIND == KIND_CONV2D) {
       const int hw = a.OH * a.OW;
       const int img = mm / hw, rem = mm - (mm / hw) * hw;
       const int oy = rem / a.OW, ox = rem - (rem / a.OW) * a.OW;
-      rb[j] = img;
-      rp0[j] = oy * a.stride - a.pad_t;
-      rp1[j] = ox * a.stride - a.pad_l;
+      const int iy0 = oy * a.stride - a.pad_t, ix0 = ox * a.stride - a.pad_l;
+      rbase[j] = ((img * a.IH + iy0) * a.IW + ix0) * a.cs_in;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int iy = iy0 + t / 3, ix = ix0 + t % 3;
+        msk |= (uint32_t)(iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW) << t;
+      }
     } else if constexpr (KIND == KIND_CONV1D) {
-      rb[j] = mm / a.L_out;
-      rp0[j] = mm - rb[j] * a.L_out - a.pad_left;
-      rp1[j] = 0;
+      const int b = mm / a.L_out, t0 = mm - b * a.L_out - a.pad_left;
+      rbase[j] = (b * a.L_in + t0) * a.cs_in;
+      for (int t = 0; t < a.ntaps; ++t) {
+        const int it = t0 + t * a.dil;
+        msk |= (uint32_t)(it >= 0 && it < a.L_in) << t;
+      }
     } else if constexpr (KIND == KIND_CONVT) {
-      rb[j] = mm / a.L_in;
-      rp0[j] = mm - rb[j] * a.L_in + delta;
-      rp1[j] = 0;
+      const int b = mm / a.L_in, t0 = mm - b * a.L_in + delta;
+      rbase[j] = (b * a.L_in + t0) * a.cs_in;
+      for (int t = 0; t < a.ntaps; ++t) {
+        const int it = t0 - t;
+        msk |= (uint32_t)(it >= 0 && it < a.L_in) << t;
+      }
     } else {
-      rb[j] = 0;
-      rp0[j] = mm;
-      rp1[j] = 0;
+      rbase[j] = mm * a.cs_in;
+      msk = 1u;
     }
+    rmask[j] = ok ? msk : 0u;
   }
+  // this lane's tap and channel within the current K step, and the tap's input offset
   int s_tap = (q * 8) / a.cs_in, s_c = (q * 8) % a.cs_in;
+  const int row_stride = a.IW * a.cs_in;  // CONV2D: one input row
+  auto tap_off = [&](int t) -> int {
+    if constexpr (KIND == KIND_CONV2D) return (t / 3) * row_stride + (t - (t / 3) * 3) * a.cs_in;
+    else if constexpr (KIND == KIND_CONV1D) return t * a.dil * a.cs_in;
+    else if constexpr (KIND == KIND_CONVT) return -t * a.cs_in;
+    else return 0;
+  };
+  int s_off = tap_off(s_tap) + s_c;
+  const char* zp = reinterpret_cast<const char*>(g_zero_page);
+  asm volatile("" : "+s"(zp));  // keep the zero page address in SGPRs (no per-use reload)
   const bf16_t* bsrc[B_PER_WAVE];
 #pragma unroll
   for (int j = 0; j < B_PER_WAVE; ++j) {
@@ -154,37 +181,27 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a, int n_
     char* Bs = As + BM * ROW;
 #pragma unroll
     for (int j = 0; j < A_PER_WAVE; ++j) {
-      const void* src = g_zero_page;
-      if (rok[j] && s_tap < a.ntaps) {
-        long off = -1;
-        if constexpr (KIND == KIND_CONV2D) {
-          const int ky = s_tap / 3, kx = s_tap - (s_tap / 3) * 3;
-          const int iy = rp0[j] + ky, ix = rp1[j] + kx;
-          if (iy >= 0 && iy < a.IH && ix >= 0 && ix < a.IW) off = ((long)(rb[j] * a.IH + iy) * a.IW + ix) * a.cs_in;
-        } else if constexpr (KIND == KIND_CONV1D) {
-          const int it = rp0[j] + s_tap * a.dil;
-          if (it >= 0 && it < a.L_in) off = ((long)rb[j] * a.L_in + it) * a.cs_in;
-        } else if constexpr (KIND == KIND_CONVT) {
-          const int it = rp0[j] - s_tap;
-          if (it >= 0 && it < a.L_in) off = ((long)rb[j] * a.L_in + it) * a.cs_in;
-        } else {
-          off = (long)rp0[j] * a.cs_in;
-        }
-        if (off >= 0) src = X + off + s_c;
-      }
+      const bool v = s_tap < 32 && ((rmask[j] >> s_tap) & 1u);
+      const void* src = v ? static_cast<const void*>(X + (unsigned)(rbase[j] + s_off)) : static_cast<const void*>(zp);
       dma16(src, As + (wave * A_PER_WAVE + j) * 16 * ROW);
     }
 #pragma unroll
     for (int j = 0; j < B_PER_WAVE; ++j) {
       const int blk = wave * B_PER_WAVE + j;
-      const void* src = bsrc[j] ? (const void*)(bsrc[j] + st * 32) : (const void*)g_zero_page;
+      const void* src = bsrc[j] ? (const void*)(bsrc[j] + st * 32) : (const void*)zp;
       dma16(src, blk < B_BLOCKS ? Bs + blk * 16 * ROW : As + (BM + BN) * ROW);
     }
-    s_c += 32;
-    while (s_c >= a.cs_in) {
-      s_c -= a.cs_in;
-      ++s_tap;
+    // advance one K step (32 channels): cs_in >= 32 is a multiple of 32, smaller cs_in divide 32
+    if (a.cs_in >= 32) {
+      s_c += 32;
+      if (s_c >= a.cs_in) {
+        s_c -= a.cs_in;
+        ++s_tap;
+      }
+    } else {
+      s_tap += 32 / a.cs_in;
     }
+    s_off = tap_off(s_tap) + s_c;
   };
 
   // ---- SE scale table for this workgroup's images (GEMM kind only) ---------------------------
@@ -384,6 +401,15 @@ void launch_kind(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
 
 void launch_conv_bf16_fast(const ConvArgs& a, hipStream_t s, double flops, double bytes) {
   M2S_CHECK(a.cs_in % 8 == 0 && a.cs_out % 4 == 0, "conv_gemm: channel strides");
+  M2S_CHECK(a.cs_in >= 32 ? a.cs_in % 32 == 0 : 32 % a.cs_in == 0, "conv_gemm: channel stride vs the 32-wide K step");
+  M2S_CHECK(a.ntaps <= 31, "conv_gemm: at most 31 taps");
+  {  // input element offsets are 32-bit in the kernel
+    const double in_elems = a.kind == KIND_CONV2D ? (double)(a.M / (a.OH * a.OW)) * a.IH * a.IW * a.cs_in
+                            : a.kind == KIND_CONV1D ? (double)(a.M / a.L_out) * a.L_in * a.cs_in
+                            : a.kind == KIND_CONVT  ? (double)a.M * a.cs_in
+                                                    : (double)a.M * a.cs_in;
+    M2S_CHECK(in_elems < 2147483647.0, "conv_gemm: input too large for 32-bit offsets (use a smaller chunk)");
+  }
   M2S_CHECK(a.kp % 32 == 0 && a.kp >= a.ntaps * a.cs_in, "conv_gemm: kp");
   M2S_CHECK(a.kind != KIND_CONV2D || a.ks == 3, "conv_gemm: 2-D kernels are 3x3 (1x1 runs as GEMM)");
   if (a.M <= 0) return;

@@ -182,15 +182,25 @@ void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B
                             hipStream_t s) {
   M2S_CHECK(lstm_persistent_supported(H) && B > 0 && T > 0, "lstm_persistent: unsupported shape");
   const int grid = 2 * (H / LP_U);
+  // Every workgroup must be resident (the step barrier waits on all of them).  The grid is 160
+  // workgroups at one per CU; check it against the occupancy query once.  (A plain launch has the
+  // same residency as a cooperative one, which only adds this check - and crashes rocprofv3 7.x's
+  // kernel tracer at process exit.)
+  static const int resident = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    M2S_HIP(hipGetDevice(&dev));
+    M2S_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    M2S_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&lstm_persistent_kernel),
+                                                          256, 0));
+    return cus * per_cu;
+  }();
+  M2S_CHECK(grid <= resident, "lstm_persistent: grid not co-resident on this device");
   LstmSync* sp = static_cast<LstmSync*>(sync);
   for (int b0 = 0; b0 < B; b0 += LP_BMAX) {  // c lives in LDS: at most LP_BMAX sequences per launch
-    int nb = std::min(LP_BMAX, B - b0);
+    const int nb = std::min(LP_BMAX, B - b0);
     M2S_HIP(hipMemsetAsync(sync, 0, lstm_persistent_sync_bytes(), s));
-    void* args[] = {(void*)&pre, (void*)&whh, (void*)&hs, (void*)&B, (void*)&b0, (void*)&nb, (void*)&T, (void*)&sp};
-    // cooperative launch: the runtime checks that all 160 workgroups are co-resident (the barrier
-    // needs it) and rejects an oversize grid instead of letting it deadlock
-    M2S_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&lstm_persistent_kernel), dim3(grid), dim3(256),
-                                       args, 0, s));
+    hipLaunchKernelGGL(lstm_persistent_kernel, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, b0, nb, T, sp);
+    M2S_HIP(hipGetLastError());
   }
 }
 

@@ -61,9 +61,13 @@ template <> struct Elem<bf16_t> {
   __device__ static __forceinline__ bf16_t from_f(float v) { return f2bf(v); }
 };
 
-// bf16-path activations: v_exp_f32 + v_rcp_f32 (1 ulp) instead of an IEEE divide sequence.
-__device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
-__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+// bf16-path activations: one v_exp_f32 + one v_rcp_f32 (1 ulp) instead of an IEEE divide and
+// __expf's denormal-range fix-up (a compare + select + multiply per value); e^-x underflowing to
+// 0 or overflowing to inf gives silu = x or -0 as the exact function does.  These run in every
+// conv epilogue, where VALU issue, not the MFMA, bounds the small-K layers.
+__device__ __forceinline__ float exp_neg(float x) { return __builtin_amdgcn_exp2f(x * -1.4426950408889634f); }
+__device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + exp_neg(x)); }
+__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + exp_neg(x)); }
 
 // Exact-libm variants used by the fp32 parity path (the reference runs fp32 libm on CPU).
 __device__ __forceinline__ float silu_exact(float x) { return x / (1.0f + expf(-x)); }
