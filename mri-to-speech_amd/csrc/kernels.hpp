@@ -33,6 +33,18 @@ void launch_ir_pwdw(const bf16_t* x, int N, int cs_in, int kp, const bf16_t* wpw
                     const uint32_t* wdw2, const float* bdw, int OH, int OW, int cs_mid, bf16_t* y, bf16_t* se_mean,
                     double flops, double bytes, hipStream_t s);
 
+// bf16 fused HiFi-GAN ResBlock1 (all (c1, c2) pairs of one resblock + the MRF running sum) for C in
+// {32, 64}: x (B, L, C) -> S (B, L, C) with S = x' (accum 0), S += x' (1), S = (S + x') / div (2).
+// (mrf_fused.hip)
+// w1/w2 are in fragment order: [rb1_frag_taps(C, k)][C/16][C/32][64 lanes][8] bf16, element
+// (tap t, n16, k32, lane, e) = W[n16*16 + lane%16][k32*32 + 8*(lane/16) + e][t] (zero taps past k).
+bool rb1_fused_supported(int C, int cs, int k, const int* dil, int np, int kp);
+int rb1_frag_taps(int C, int k);
+void launch_rb1_fused(const bf16_t* x, bf16_t* s, int B, int L, int C, int k, int np, const int* dil,
+                      const bf16_t* const* w1, const float* const* b1, const bf16_t* const* w2,
+                      const float* const* b2, int kp, int accum, float div, double flops, double bytes,
+                      hipStream_t st);
+
 // Decoded frames -> model input: uint8 (N,H,W) grey or (N,H,W,3) BGR -> fp32 (N,H,W) in [0, 1]
 // (_preprocess_frame, run_mri_video_inference.py:34-54, minus the host-side resize).  (preprocess.hip)
 void launch_preprocess(const uint8_t* frames, int N, int H, int W, int channels, float* out, hipStream_t s);

@@ -607,6 +607,7 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
     : h_(h), dtype_(dtype), device_(device) {
   M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16, "bad dtype");
   M2S_CHECK(h.resblock == 1 || h.resblock == 2, "resblock must be 1 or 2");
+  if (const char* e = std::getenv("M2S_MRF_FUSED")) mrf_fused_ = std::strcmp(e, "0") != 0;
   M2S_CHECK(h.n_up >= 1 && h.n_up <= 8 && h.n_kernels >= 1 && h.n_kernels <= 8, "bad generator config");
   const int c0 = h.upsample_initial_channel;
   {  // conv_pre: Conv1d(num_mels, c0, 7), no weight norm (models.py:94)
@@ -661,10 +662,31 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
                   [&](int n) { return bv.data[n]; });
         return c;
       };
+      const bool frag = dtype == M2S_DT_BF16 && h.resblock == 1 &&
+                        rb1_fused_supported(co, chan_stride(co), kk, rb.dil.data(), (int)rb.dil.size(), kk * co);
+      auto mk_frag = [&](const std::string& name) {  // fragment order of mrf_fused.hip
+        std::vector<float> wv = fold_wn(sd, name, {co, co, kk});
+        const int taps = rb1_frag_taps(co, kk), nt16 = co / 16, k32 = co / 32;
+        std::vector<uint16_t> f((size_t)taps * nt16 * k32 * 64 * 8);
+        size_t o = 0;
+        for (int t = 0; t < taps; ++t)
+          for (int nt = 0; nt < nt16; ++nt)
+            for (int kc = 0; kc < k32; ++kc)
+              for (int ln = 0; ln < 64; ++ln)
+                for (int e = 0; e < 8; ++e) {
+                  const int n = nt * 16 + (ln & 15), c = kc * 32 + 8 * (ln >> 4) + e;
+                  f[o++] = t < kk ? f2bf_host(wv[((size_t)n * co + c) * kk + t]) : 0;
+                }
+        return arena_.add_vec(f);
+      };
       for (size_t d = 0; d < rb.dil.size(); ++d) {
         if (h.resblock == 1) {
           rb.c1.push_back(mk(q + ".convs1." + std::to_string(d), rb.dil[d]));
           rb.c2.push_back(mk(q + ".convs2." + std::to_string(d), 1));
+          if (frag) {
+            rb.f1_off.push_back(mk_frag(q + ".convs1." + std::to_string(d)));
+            rb.f2_off.push_back(mk_frag(q + ".convs2." + std::to_string(d)));
+          }
         } else {
           rb.c1.push_back(mk(q + ".convs." + std::to_string(d), rb.dil[d]));
         }
@@ -688,6 +710,8 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
   for (auto& rb : rbs_) {
     for (auto& c : rb.c1) c.resolve(arena_);
     for (auto& c : rb.c2) c.resolve(arena_);
+    for (size_t o : rb.f1_off) rb.f1.push_back(static_cast<const bf16_t*>(arena_.ptr(o)));
+    for (size_t o : rb.f2_off) rb.f2.push_back(static_cast<const bf16_t*>(arena_.ptr(o)));
   }
 }
 
@@ -776,6 +800,28 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
       const RB& rb = rbs_[i * nk + j];
       const T* hcur = X;
       const int np = (int)rb.dil.size();
+      const int accum = j == 0 ? 0 : (j == nk - 1 ? 2 : 1);
+      if (std::is_same<T, bf16_t>::value && mrf_fused_ && !rb.f1.empty()) {
+        // one launch for the whole resblock + MRF sum (mrf_fused.hip)
+        const bf16_t* w1[8];
+        const bf16_t* w2[8];
+        const float* b1[8];
+        const float* b2[8];
+        double macs = 0.0;
+        for (int p = 0; p < np; ++p) {
+          w1[p] = rb.f1[p];
+          w2[p] = rb.f2[p];
+          b1[p] = rb.c1[p].b;
+          b2[p] = rb.c2[p].b;
+          macs += rb.c1[p].macs_per_row + rb.c2[p].macs_per_row;
+        }
+        const int C = rb.c1[0].cout;
+        const double rows = (double)B * L;
+        const double bytes = 2.0 * rows * C * (2 + (accum ? 1 : 0)) + 2.0 * np * 2 * C * C * rb.k;
+        launch_rb1_fused(reinterpret_cast<const bf16_t*>(X), reinterpret_cast<bf16_t*>(S), B, L, C, rb.k, np,
+                         rb.dil.data(), w1, b1, w2, b2, rb.c1[0].kp, accum, (float)nk, 2.0 * macs * rows, bytes, s);
+        continue;
+      }
       for (int p = 0; p < np; ++p) {
         const bool last = p == np - 1;
         T* out = last ? S : Hb[p & 1];

@@ -128,6 +128,7 @@ class Vocoder {
   void forward_from_norm(const float* mel_norm, const float* mean, const float* std_, int B, int T, float* mel_db,
                          float* mel_log, void* ln_buf, float* wav, Workspace& ws, hipStream_t s);
   size_t act_elems(int B, int T) const;
+  bool mrf_fused_ = true;  // bf16: fused ResBlock1 kernel for C in {32, 64} (env M2S_MRF_FUSED=0 disables)
 
  private:
   template <typename T>
@@ -136,6 +137,9 @@ class Vocoder {
     int k = 3;
     std::vector<int> dil;
     std::vector<PConv> c1, c2;  // resblock "1": c1 (dilated) + c2 ; "2": c1 only
+    // bf16 resblock "1" at C in {32, 64}: the same weights in the fused kernel's fragment order
+    std::vector<size_t> f1_off, f2_off;
+    std::vector<const bf16_t*> f1, f2;
   };
   m2s_hifigan_h h_;
   int dtype_, device_, hop_ = 1;
