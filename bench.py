@@ -184,7 +184,8 @@ def main():
         "dtype": args.dtype,
         "data": "synthetic (seeded U[0,1) frames, per-frame min-max; random-init weights of the reference architecture)",
         "rtf": round(elapsed / audio_s, 6),
-        "config": {"workload": f"e2e rtMRI->wav, {B} clips x {T} frames per GPU at {HW}x{HW} (configs[3] per-GPU share)",
+        "config": {"workload": f"e2e rtMRI->wav, {B} clips x {T} frames per GPU at {HW}x{HW} " +
+                               ("(configs[4] clip length, bf16)" if T >= 1000 else "(configs[3] per-GPU share)"),
                    "clips_per_gpu": B, "frames_per_clip": T, "global_batch_clips": B * world, "hw": HW,
                    "parallelism": f"dp{world}", "chunk": args.chunk},
     }

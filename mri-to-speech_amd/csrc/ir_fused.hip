@@ -26,7 +26,10 @@ namespace m2s {
 namespace {
 
 constexpr int SL = 32;         // expanded channels per slice
-constexpr int MROW = SL + 8;   // LDS row stride in bf16 (80 B)
+#ifndef IRF_MROW
+#define IRF_MROW (SL + 8)
+#endif
+constexpr int MROW = IRF_MROW;  // LDS row stride in bf16 (80 B)
 constexpr int NT = SL / 16;    // 16-channel MFMA subtiles
 constexpr int CG = SL / 8;     // phase-2 channel groups (8 channels = one 16-byte vector)
 constexpr int PL = 256 / CG;   // phase-2 pixel lanes (64; 16 per wave)
@@ -163,7 +166,8 @@ __global__ void __launch_bounds__(256, 4) ir_pwdw_kernel(const bf16_t* __restric
         const bf16_t* base = tile + lut[g * P + p] * MROW + cg * 8;
         uint4 in[9];
 #pragma unroll
-        for (int t = 0; t < 9; ++t) in[t] = *reinterpret_cast<const uint4*>(base + off[t]);
+        for (int t = 0; t < 9; ++t)
+          in[t] = (IRF_MODE & 16) && t ? in[0] : *reinterpret_cast<const uint4*>(base + off[t]);
         float a[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) a[j] = b[j];
@@ -172,8 +176,12 @@ __global__ void __launch_bounds__(256, 4) ir_pwdw_kernel(const bf16_t* __restric
           const uint32_t u[4] = {in[t].x, in[t].y, in[t].z, in[t].w};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            a[2 * j] = dot2(u[j], w[t][2 * j], a[2 * j]);
-            a[2 * j + 1] = dot2(u[j], w[t][2 * j + 1], a[2 * j + 1]);
+            if (IRF_MODE & 8) {  // microbenchmark: one plain add per channel pair instead of 2 dot2
+              a[2 * j] += __uint_as_float(u[j] ^ w[t][2 * j]);
+            } else {
+              a[2 * j] = dot2(u[j], w[t][2 * j], a[2 * j]);
+              a[2 * j + 1] = dot2(u[j], w[t][2 * j + 1], a[2 * j + 1]);
+            }
           }
         }
         uint4 o;
