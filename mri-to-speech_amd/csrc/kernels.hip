@@ -4,6 +4,8 @@
 
 #include "kernels.hpp"
 
+#include <type_traits>
+
 namespace m2s {
 
 namespace {
@@ -86,6 +88,46 @@ __global__ void __launch_bounds__(256) stem_kernel(const float* __restrict__ fra
       *reinterpret_cast<uint4*>(out) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
                                                   pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
     }
+  }
+}
+
+// stem, bf16 with 32 output channels: one thread per output pixel computes all 32 channels.  The
+// 288 weights and 32 biases are wave-uniform, so they come through the scalar cache as SGPR
+// operands of the FMAs (no VGPRs, no LDS), the 9 input taps are loaded once per pixel instead of
+// once per 8-channel lane group, and a lane stores its pixel's 64 bytes (a wave: 4 KB contiguous).
+__global__ void __launch_bounds__(256) stem32_kernel(const float* __restrict__ frames, int N, int H, int W, int OH,
+                                                     int OW, int pad_t, int pad_l, const float* __restrict__ w9,
+                                                     const float* __restrict__ bias, bf16_t* __restrict__ y) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  const int hw = OH * OW;
+  if (p >= (long)N * hw) return;
+  const int n = (int)(p / hw);
+  const int rem = (int)(p - (long)n * hw);
+  const int oy = rem / OW, ox = rem - (rem / OW) * OW;
+  const float* fr = frames + (long)n * H * W;
+  float in[9];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int iy = oy * 2 - pad_t + ky, ix = ox * 2 - pad_l + kx;
+      in[ky * 3 + kx] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? fr[(long)iy * W + ix] : 0.f;
+    }
+  uint4* out = reinterpret_cast<uint4*>(y + p * 32);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      float a0 = bias[q * 8 + j], a1 = bias[q * 8 + j + 1];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        a0 += w9[(q * 8 + j) * 9 + t] * in[t];
+        a1 += w9[(q * 8 + j + 1) * 9 + t] * in[t];
+      }
+      o[j / 2] = pack_bf16x2(silu(a0), silu(a1));
+    }
+    out[q] = make_uint4(o[0], o[1], o[2], o[3]);
   }
 }
 
@@ -271,6 +313,12 @@ template <typename T>
 void launch_stem(const float* frames, int N, int H, int W, int OH, int OW, int pad_t, int pad_l, const float* w9,
                  const float* bias, int cout, int cs_out, T* y, hipStream_t s) {
   M2S_CHECK(cout <= 32 && cs_out % 8 == 0 && cs_out <= 32, "stem: unsupported channel count");
+  if (std::is_same<T, bf16_t>::value && cout == 32 && cs_out == 32) {
+    hipLaunchKernelGGL(stem32_kernel, dim3((unsigned)nblk((long)N * OH * OW)), dim3(256), 0, s, frames, N, H, W, OH, OW,
+                       pad_t, pad_l, w9, bias, reinterpret_cast<bf16_t*>(y));
+    M2S_HIP(hipGetLastError());
+    return;
+  }
   const long blocks = std::min<long>(nblk(4L * N * OH * OW), 256L * 16);
   hipLaunchKernelGGL(stem_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, s, frames, N, H, W, OH, OW, pad_t,
                      pad_l, w9, bias, cout, cs_out, y);

@@ -414,7 +414,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
     same_pad(H, 3, 2, &oh, &pt);
     same_pad(W, 3, 2, &ow, &pl);
     {
-      ProfScope ps(tname<T>("stem_kernel"), 2.0 * nc * oh * ow * EFF_STEM * 27, 4.0 * nc * H * W + sizeof(T) * (double)nc * oh * ow * 32, s);
+      ProfScope ps(std::is_same<T, bf16_t>::value ? std::string("stem32_kernel") : tname<T>("stem_kernel"), 2.0 * nc * oh * ow * EFF_STEM * 27, 4.0 * nc * H * W + sizeof(T) * (double)nc * oh * ow * 32, s);
       launch_stem<T>(frames + (size_t)n0 * H * W, nc, H, W, oh, ow, pt, pl, static_cast<const float*>(arena_.ptr(stem_w_)),
                      static_cast<const float*>(arena_.ptr(stem_b_)), EFF_STEM, chan_stride(EFF_STEM), A, s);
     }
