@@ -45,6 +45,13 @@ void launch_rb1_fused(const bf16_t* x, bf16_t* s, int B, int L, int C, int k, in
                       const float* const* b2, int kp, int accum, float div, double flops, double bytes,
                       hipStream_t st);
 
+// bf16 conv_stem + bn1 + SiLU + blocks.0.0 (3x3 32->16 + SiLU) + blocks.0.1 (3x3 16->16 + SiLU + skip)
+// in one kernel: frames (N,H,W) fp32 -> y (N,OH,OW,16).  w0/w1: packed conv rows (kp 288 / 160).
+// (stem_b0.hip)
+void launch_stem_b0(const float* frames, int N, int H, int W, int OH, int OW, int pad_t, int pad_l, const float* w9,
+                    const float* b9, const bf16_t* w0, const float* b0, int kp0, const bf16_t* w1, const float* b1,
+                    int kp1, bf16_t* y, double flops, double bytes, hipStream_t s);
+
 // Decoded frames -> model input: uint8 (N,H,W) grey or (N,H,W,3) BGR -> fp32 (N,H,W) in [0, 1]
 // (_preprocess_frame, run_mri_video_inference.py:34-54, minus the host-side resize).  (preprocess.hip)
 void launch_preprocess(const uint8_t* frames, int N, int H, int W, int channels, float* out, hipStream_t s);

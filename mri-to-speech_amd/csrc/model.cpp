@@ -202,6 +202,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16, "bad dtype");
   M2S_CHECK(n_mels > 0 && hidden > 0 && hidden % 8 == 0, "bad n_mels / rnn_hidden");
   if (const char* e = std::getenv("M2S_IR_FUSED")) ir_fused_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
   const std::string P = "cnn.backbone.";
   {  // stem: fold repeat(1,3,1,1) by summing the 3 input channels; then BN
     const float* w = need(sd, P + "conv_stem.weight", {EFF_STEM, 3, 3, 3}).data;
@@ -413,15 +414,30 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
     int oh, ow, pt, pl;
     same_pad(H, 3, 2, &oh, &pt);
     same_pad(W, 3, 2, &ow, &pl);
-    {
-      ProfScope ps(std::is_same<T, bf16_t>::value ? std::string("stem32_kernel") : tname<T>("stem_kernel"), 2.0 * nc * oh * ow * EFF_STEM * 27, 4.0 * nc * H * W + sizeof(T) * (double)nc * oh * ow * 32, s);
-      launch_stem<T>(frames + (size_t)n0 * H * W, nc, H, W, oh, ow, pt, pl, static_cast<const float*>(arena_.ptr(stem_w_)),
-                     static_cast<const float*>(arena_.ptr(stem_b_)), EFF_STEM, chan_stride(EFF_STEM), A, s);
-    }
+    // stem + blocks.0 (two 3x3 ConvBnAct at stride 1: 32 -> 16, 16 -> 16 + skip) in one kernel
+    const bool front = std::is_same<T, bf16_t>::value && stem_fused_ && !(probe && stop_after >= 0 && stop_after < 2) &&
+                       blocks_.size() >= 2 && blocks_[0].type == 0 && blocks_[0].stride == 1 && !blocks_[0].skip &&
+                       blocks_[0].cout == 16 && blocks_[0].c1.cs_in == 32 && blocks_[0].c1.kp == 288 &&
+                       blocks_[1].type == 0 && blocks_[1].stride == 1 && blocks_[1].skip && blocks_[1].cout == 16 &&
+                       blocks_[1].c1.cs_in == 16 && blocks_[1].c1.kp == 160 && chan_stride(16) == 16;
     T* cur = A;
     T* nxt = Bb;
     int cc = EFF_STEM;
     int bi = 0;
+    if (front) {
+      const double px = (double)nc * oh * ow;
+      launch_stem_b0(frames + (size_t)n0 * H * W, nc, H, W, oh, ow, pt, pl, static_cast<const float*>(arena_.ptr(stem_w_)),
+                     static_cast<const float*>(arena_.ptr(stem_b_)), static_cast<const bf16_t*>(blocks_[0].c1.w),
+                     blocks_[0].c1.b, blocks_[0].c1.kp, static_cast<const bf16_t*>(blocks_[1].c1.w), blocks_[1].c1.b,
+                     blocks_[1].c1.kp, reinterpret_cast<bf16_t*>(A),
+                     2.0 * px * (EFF_STEM * 9 + 16 * 9 * 32 + 16 * 9 * 16), 4.0 * nc * H * W + 2.0 * px * 16, s);
+      cc = 16;
+      bi = 2;
+    } else {
+      ProfScope ps(std::is_same<T, bf16_t>::value ? std::string("stem32_kernel") : tname<T>("stem_kernel"), 2.0 * nc * oh * ow * EFF_STEM * 27, 4.0 * nc * H * W + sizeof(T) * (double)nc * oh * ow * 32, s);
+      launch_stem<T>(frames + (size_t)n0 * H * W, nc, H, W, oh, ow, pt, pl, static_cast<const float*>(arena_.ptr(stem_w_)),
+                     static_cast<const float*>(arena_.ptr(stem_b_)), EFF_STEM, chan_stride(EFF_STEM), A, s);
+    }
     auto tap = [&](int done) {
       if (stop_after == done && probe) {
         launch_unpad<T>(cur, (long)nc * oh * ow, cc, chan_stride(cc), probe + (size_t)n0 * oh * ow * cc, s);
@@ -434,9 +450,10 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
       }
       return false;
     };
-    if (tap(0)) continue;
+    if (tap(bi)) continue;  // bi = 0, or 2 after the fused front
     bool stopped = false;
-    for (const Block& b : blocks_) {
+    for (size_t k = front ? 2 : 0; k < blocks_.size(); ++k) {
+      const Block& b = blocks_[k];
       int nh, nw, qt, ql;
       same_pad(oh, 3, b.stride, &nh, &qt);
       same_pad(ow, 3, b.stride, &nw, &ql);

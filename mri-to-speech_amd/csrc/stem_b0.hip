@@ -1,0 +1,232 @@
+// Fused encoder front (bf16): conv_stem 3x3/s2 (TF-SAME) + bn1 + SiLU  ->  blocks.0.0 ConvBnAct 3x3
+// 32->16 + SiLU  ->  blocks.0.1 ConvBnAct 3x3 16->16 + SiLU + skip, for one 16 x TH output tile per
+// workgroup (timm tf_efficientnetv2_b2 conv_stem/bn1/blocks.0; mri_acoustic_model.py:28-46 builds it).
+//
+// Unfused, the stem writes its 32-channel map (2 MB per 256x256 frame in bf16), blocks.0.0 reads it
+// back and writes 16 channels, blocks.0.1 reads those twice (conv + skip) and writes again: ~8.5 GB
+// of HBM traffic per 1920 frames.  Here only the fp32 frame is read and the blocks.0.1 output
+// written (1.5 GB); the two intermediate maps live in LDS with the halos the next 3x3 needs:
+//   S = stem output on (TH+4) x 20 pixels (32 ch), A = blocks.0.0 output on (TH+2) x 18 (16 ch).
+// Pixels outside the image are stored as exact zeros: they are the next conv's zero padding.
+//
+//   phase 1  stem on VALU in fp32 (one thread per S pixel, 32 channels, weights as scalar operands)
+//   phase 2  blocks.0.0 on MFMA 16x16x32 bf16: weights (16 x 288) resident in VGPRs as 9 A
+//            fragments, B = 16 A-pixels x 32 channels of one tap from S
+//   phase 3  blocks.0.1 likewise (16 x 160: two taps of 16 channels per K step), + skip from A.
+// Both LDS images are planar ([16-byte chunk][pixel]) so a B-fragment read of 16 consecutive
+// pixels is bank-conflict free at any tap offset (see mrf_fused.hip).
+#include <algorithm>
+#include <cstdio>
+
+#include "kernels.hpp"
+#include "prof.hpp"
+
+namespace m2s {
+namespace {
+
+constexpr int SB_TW = 16;           // output tile width (one MFMA position subtile per tile row)
+constexpr int SB_SW = SB_TW + 4;    // S row width
+constexpr int SB_AW = SB_TW + 2;    // A row width
+
+struct StemB0Args {
+  const float* frames;  // (N, H, W) fp32
+  const float* w9;      // stem [32][9] (grey repeat folded), BN folded
+  const float* b9;      // [32]
+  const bf16_t* w0;     // blocks.0.0 packed [>=16][kp0 = 288]
+  const float* b0;
+  const bf16_t* w1;     // blocks.0.1 packed [>=16][kp1 = 160]
+  const float* b1;
+  bf16_t* y;            // (N, OH, OW, 16)
+  int N, H, W, OH, OW, pad_t, pad_l, kp0, kp1, tiles_x, tiles_y;
+};
+
+template <int TH>
+__global__ void __launch_bounds__(256, 4) stem_b0_kernel(const StemB0Args a) {
+  constexpr int SH = TH + 4, AH = TH + 2;
+  constexpr int SPIX = SH * SB_SW, APIX = AH * SB_AW;
+  constexpr int APIX_PAD = (APIX + 15) / 16 * 16;
+  constexpr int SPLANE = (SPIX * 16 + 255) / 256 * 256;      // bytes per S plane (4 planes)
+  constexpr int APLANE = (APIX_PAD * 16 + 255) / 256 * 256;  // bytes per A plane (2 planes)
+  constexpr int ASUB = APIX_PAD / 16;                         // A position subtiles
+  constexpr int AMS = (ASUB + 3) / 4;                         // ... per wave, at most
+  constexpr int OMS = TH / 4;                                 // output subtiles (rows) per wave
+  __shared__ __attribute__((aligned(16))) char sS[4 * SPLANE];
+  __shared__ __attribute__((aligned(16))) char sA[2 * APLANE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int tpi = a.tiles_x * a.tiles_y;
+  const int n = blockIdx.x / tpi, tr = blockIdx.x - n * tpi;
+  const int ty0 = (tr / a.tiles_x) * TH, tx0 = (tr - (tr / a.tiles_x) * a.tiles_x) * SB_TW;
+
+  // ---- phase 1: stem (fp32 VALU) -> S -------------------------------------------------------
+  // threads [0, SPIX/2) take S pixels i and i + SPIX/2: straight-line code, so every weight is one
+  // scalar load feeding two FMAs and nothing keeps the 288 weights live in registers
+  const float* fr = a.frames + (size_t)n * a.H * a.W;
+  static_assert(SPIX % 2 == 0 && SPIX / 2 <= 256, "stem tile");
+  if (tid < SPIX / 2) {
+    float in[2][9];
+    bool ok[2];
+    int pix[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = tid + h * (SPIX / 2);
+      pix[h] = i;
+      const int sy = i / SB_SW, sx = i - (i / SB_SW) * SB_SW;
+      const int oy = ty0 - 2 + sy, ox = tx0 - 2 + sx;  // stem output pixel
+      ok[h] = oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int iy = oy * 2 - a.pad_t + ky, ix = ox * 2 - a.pad_l + kx;
+          in[h][ky * 3 + kx] =
+              (ok[h] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) ? fr[(size_t)iy * a.W + ix] : 0.f;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t v[2][4];
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const float bj0 = a.b9[q * 8 + j], bj1 = a.b9[q * 8 + j + 1];
+        float a0 = bj0, a1 = bj1, c0 = bj0, c1 = bj1;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const float w0 = a.w9[(q * 8 + j) * 9 + t], w1 = a.w9[(q * 8 + j + 1) * 9 + t];
+          a0 += w0 * in[0][t];
+          a1 += w1 * in[0][t];
+          c0 += w0 * in[1][t];
+          c1 += w1 * in[1][t];
+        }
+        v[0][j / 2] = ok[0] ? pack_bf16x2(silu(a0), silu(a1)) : 0u;
+        v[1][j / 2] = ok[1] ? pack_bf16x2(silu(c0), silu(c1)) : 0u;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        *reinterpret_cast<uint4*>(sS + q * SPLANE + pix[h] * 16) = make_uint4(v[h][0], v[h][1], v[h][2], v[h][3]);
+    }
+  }
+  // resident weights of both convs (A fragments), in flight across the barrier
+  bf16x8 wf0[9], wf1[5];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wf0[t] = *reinterpret_cast<const bf16x8*>(a.w0 + (size_t)r16 * a.kp0 + t * 32 + 8 * g);
+#pragma unroll
+  for (int t = 0; t < 5; ++t) wf1[t] = *reinterpret_cast<const bf16x8*>(a.w1 + (size_t)r16 * a.kp1 + t * 32 + 8 * g);
+  __syncthreads();
+
+  // ---- phase 2: blocks.0.0 (32 -> 16) on MFMA -> A --------------------------------------------
+  {
+    int sbase[AMS];
+#pragma unroll
+    for (int i = 0; i < AMS; ++i) {
+      const int pa = min(16 * (wave + 4 * i) + r16, APIX - 1);
+      const int ay = pa / SB_AW, ax = pa - (pa / SB_AW) * SB_AW;
+      sbase[i] = (ay * SB_SW + ax) * 16 + g * SPLANE;
+    }
+    f32x4 acc[AMS];
+#pragma unroll
+    for (int i = 0; i < AMS; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int toff = ((t / 3) * SB_SW + (t % 3)) * 16;
+#pragma unroll
+      for (int i = 0; i < AMS; ++i) {
+        if (wave + 4 * i < ASUB) {
+          const bf16x8 b = *reinterpret_cast<const bf16x8*>(sS + sbase[i] + toff);
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[t], b, acc[i], 0, 0, 0);
+        }
+      }
+    }
+    const float4 bb = *reinterpret_cast<const float4*>(a.b0 + 4 * g);
+#pragma unroll
+    for (int i = 0; i < AMS; ++i) {
+      const int pa = 16 * (wave + 4 * i) + r16;
+      if (wave + 4 * i >= ASUB || pa >= APIX) continue;
+      const int ay = pa / SB_AW, ax = pa - (pa / SB_AW) * SB_AW;
+      const int oy = ty0 - 1 + ay, ox = tx0 - 1 + ax;
+      uint2 u = make_uint2(0u, 0u);
+      if (oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW) {
+        u.x = pack_bf16x2(silu(acc[i][0] + bb.x), silu(acc[i][1] + bb.y));
+        u.y = pack_bf16x2(silu(acc[i][2] + bb.z), silu(acc[i][3] + bb.w));
+      }
+      *reinterpret_cast<uint2*>(sA + (g >> 1) * APLANE + pa * 16 + (g & 1) * 8) = u;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 3: blocks.0.1 (16 -> 16) + skip on MFMA -> y -------------------------------------
+  {
+    // K step st covers taps 2st (lanes g < 2) and 2st + 1 (g >= 2), 16 channels each; the pad tap 9
+    // (zero weights) reads tap 0's pixel so the product stays finite
+    int toff[5];
+#pragma unroll
+    for (int st = 0; st < 5; ++st) {
+      int t = 2 * st + (g >> 1);
+      if (t > 8) t = 0;
+      toff[st] = ((t / 3) * SB_AW + (t % 3)) * 16 + (g & 1) * APLANE;
+    }
+    f32x4 acc[OMS];
+#pragma unroll
+    for (int i = 0; i < OMS; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < 5; ++st)
+#pragma unroll
+      for (int i = 0; i < OMS; ++i) {
+        const int row = wave + 4 * i;  // output tile row = subtile
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(sA + (row * SB_AW + r16) * 16 + toff[st]);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[st], b, acc[i], 0, 0, 0);
+      }
+    const float4 bb = *reinterpret_cast<const float4*>(a.b1 + 4 * g);
+    const int ox = tx0 + r16;
+#pragma unroll
+    for (int i = 0; i < OMS; ++i) {
+      const int row = wave + 4 * i, oy = ty0 + row;
+      if (oy >= a.OH || ox >= a.OW) continue;
+      const uint2 r = *reinterpret_cast<const uint2*>(sA + (g >> 1) * APLANE + ((row + 1) * SB_AW + r16 + 1) * 16 +
+                                                      (g & 1) * 8);
+      const float v0 = silu(acc[i][0] + bb.x) + __uint_as_float(r.x << 16);
+      const float v1 = silu(acc[i][1] + bb.y) + __uint_as_float(r.x & 0xffff0000u);
+      const float v2 = silu(acc[i][2] + bb.z) + __uint_as_float(r.y << 16);
+      const float v3 = silu(acc[i][3] + bb.w) + __uint_as_float(r.y & 0xffff0000u);
+      *reinterpret_cast<uint2*>(a.y + (((size_t)n * a.OH + oy) * a.OW + ox) * 16 + 4 * g) =
+          make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+    }
+  }
+}
+
+}  // namespace
+
+void launch_stem_b0(const float* frames, int N, int H, int W, int OH, int OW, int pad_t, int pad_l, const float* w9,
+                    const float* b9, const bf16_t* w0, const float* b0, int kp0, const bf16_t* w1, const float* b1,
+                    int kp1, bf16_t* y, double flops, double bytes, hipStream_t s) {
+  M2S_CHECK(kp0 == 288 && kp1 == 160 && N > 0 && OH > 0 && OW > 0, "stem_b0: unsupported shape");
+  constexpr int TH = 16;
+  StemB0Args a;
+  a.frames = frames;
+  a.w9 = w9;
+  a.b9 = b9;
+  a.w0 = w0;
+  a.b0 = b0;
+  a.w1 = w1;
+  a.b1 = b1;
+  a.y = y;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.OH = OH;
+  a.OW = OW;
+  a.pad_t = pad_t;
+  a.pad_l = pad_l;
+  a.kp0 = kp0;
+  a.kp1 = kp1;
+  a.tiles_x = ceil_div(OW, SB_TW);
+  a.tiles_y = ceil_div(OH, TH);
+  M2S_CHECK((double)N * a.tiles_x * a.tiles_y < 2147483647.0, "stem_b0: grid");
+  ProfScope ps("stem_b0_kernel<16>", flops, bytes, s);
+  hipLaunchKernelGGL(stem_b0_kernel<TH>, dim3(N * a.tiles_x * a.tiles_y), dim3(256), 0, s, a);
+  M2S_HIP(hipGetLastError());
+}
+
+}  // namespace m2s

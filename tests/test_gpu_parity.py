@@ -203,6 +203,29 @@ def test_effnet_bf16_ir_fused_every_block(rt, ac_state, monkeypatch, hw):
     assert _cos(ga, gb) >= 0.99999
 
 
+@pytest.mark.parametrize("hw", [(256, 256), (96, 80), (67, 101)])
+def test_effnet_bf16_stem_b0_fused(rt, ac_state, monkeypatch, hw):
+    """The fused stem + blocks.0 kernel (stem_b0.hip) against the separate stem / 3x3 conv launches
+    and the fp32 oracle: the blocks.0 output (probe 2), every later block, the pooled features;
+    odd sizes exercise the TF-SAME bottom/right stem pad and the partial 16 x 16 tiles."""
+    sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
+    fr = torch.from_numpy(synth.synth_frames(1, 2, hw=hw, seed=47)[0])
+    taps = []
+    effnet.effnet_features(sd, fr, taps=taps)
+    monkeypatch.setenv("M2S_STEM_FUSED", "1")
+    fused = rt.AcousticEngine(ac_state[1], dtype="bf16", device=DEV)
+    monkeypatch.setenv("M2S_STEM_FUSED", "0")
+    plain = rt.AcousticEngine(ac_state[1], dtype="bf16", device=DEV)
+    x = fr.to(DEV)
+    for i in (2, 3, 6, len(taps) - 1):
+        a = fused.probe(x, i).float().cpu().numpy()
+        b = plain.probe(x, i).float().cpu().numpy()
+        assert np.isfinite(a).all()
+        assert _rel(a, b) <= 2e-2, f"block {i}: fused vs unfused rel {_rel(a, b)}"
+        assert _cos(a, taps[i].numpy()) >= 0.999, f"block {i}: cos vs oracle {_cos(a, taps[i].numpy())}"
+    assert _cos(fused.effnet(x).cpu().numpy(), plain.effnet(x).cpu().numpy()) >= 0.99999
+
+
 # ------------------------------------------------------------------------------ acoustic model / pipeline
 def test_acoustic_forward_matches_reference_wiring(ac_f32):
     g = _gold("acoustic.npz")
