@@ -56,6 +56,8 @@ __global__ void __launch_bounds__(256, 4) ir_pwdw_kernel(const bf16_t* __restric
   __shared__ __attribute__((aligned(16))) bf16_t tile[ROWS_MAX * MROW];
   __shared__ uint16_t lut[POS_MAX];
   __shared__ float red[4][SL];
+  __shared__ uint4 wdw_lds[9][SL / 4];  // this slice's depthwise taps (bf16 in their dword halves)
+  __shared__ float4 bdw_lds[SL / 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g16 = lane >> 4, r16 = lane & 15;
   const int P = OH * OW, WR = OW + 2, IR = (OH + 2) * WR;
@@ -67,6 +69,15 @@ __global__ void __launch_bounds__(256, 4) ir_pwdw_kernel(const bf16_t* __restric
   const int grp = wid / nsl, sl = wid - grp * nsl;
   const int n0 = grp * G, gi = min(G, N - n0), MP = gi * P;
 
+  // the slice's depthwise weights and biases, staged once: every pixel lane of a channel group
+  // needs the same 9 x 8 taps, and loading them per lane from L1/L2 (80 KB per workgroup) cost
+  // more than the whole depthwise
+  if (tid < 9 * (SL / 4)) {
+    const int t = tid / (SL / 4), k = tid - t * (SL / 4), c = sl * SL + 4 * k;
+    wdw_lds[t][k] = c < cs_mid ? *reinterpret_cast<const uint4*>(wdw2 + (size_t)t * cs_mid + c) : make_uint4(0, 0, 0, 0);
+    if (t == 0) bdw_lds[k] = c < cs_mid ? *reinterpret_cast<const float4*>(bdw + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
   // ---- position -> haloed tile row; zero the tile (the halo stays zero) ----------------------
   if (tid < G * P) {
     const int g = tid / P, p = tid - g * P, oy = p / OW, ox = p - oy * OW;
@@ -74,7 +85,8 @@ __global__ void __launch_bounds__(256, 4) ir_pwdw_kernel(const bf16_t* __restric
   }
   {
     uint4* t4 = reinterpret_cast<uint4*>(tile);
-    for (int i = tid; i < G * IR * (MROW / 8); i += 256) t4[i] = make_uint4(0, 0, 0, 0);
+    if (!(IRF_MODE & 64))
+      for (int i = tid; i < G * IR * (MROW / 8); i += 256) t4[i] = make_uint4(0, 0, 0, 0);
   }
 
   const bf16_t* xi = x + (size_t)n0 * P * cs_in;
@@ -150,14 +162,12 @@ __global__ void __launch_bounds__(256, 4) ir_pwdw_kernel(const bf16_t* __restric
       float b[8];
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const uint4 lo = *reinterpret_cast<const uint4*>(wdw2 + (size_t)t * cs_mid + c);
-        const uint4 hi = *reinterpret_cast<const uint4*>(wdw2 + (size_t)t * cs_mid + c + 4);
+        const uint4 lo = wdw_lds[t][2 * cg], hi = wdw_lds[t][2 * cg + 1];
         w[t][0] = lo.x; w[t][1] = lo.y; w[t][2] = lo.z; w[t][3] = lo.w;
         w[t][4] = hi.x; w[t][5] = hi.y; w[t][6] = hi.z; w[t][7] = hi.w;
       }
       {
-        const float4 lo = *reinterpret_cast<const float4*>(bdw + c);
-        const float4 hi = *reinterpret_cast<const float4*>(bdw + c + 4);
+        const float4 lo = bdw_lds[2 * cg], hi = bdw_lds[2 * cg + 1];
         b[0] = lo.x; b[1] = lo.y; b[2] = lo.z; b[3] = lo.w;
         b[4] = hi.x; b[5] = hi.y; b[6] = hi.z; b[7] = hi.w;
       }
@@ -188,7 +198,8 @@ __global__ void __launch_bounds__(256, 4) ir_pwdw_kernel(const bf16_t* __restric
         uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float v0 = silu(a[2 * j]), v1 = silu(a[2 * j + 1]);
+          const float v0 = (IRF_MODE & 32) ? a[2 * j] : silu(a[2 * j]);
+          const float v1 = (IRF_MODE & 32) ? a[2 * j + 1] : silu(a[2 * j + 1]);
           s[2 * j] += v0;
           s[2 * j + 1] += v1;
           ow[j] = pack_bf16x2(v0, v1);
