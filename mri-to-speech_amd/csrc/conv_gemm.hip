@@ -79,7 +79,7 @@ constexpr int ROW = 64;  // bytes per LDS row = 32 bf16 = one k-step
 __device__ __forceinline__ int swz(int row, int chunk) { return row * ROW + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
 template <int BM, int BN, int MT, int NT, int S, int KIND, int XF>
-__global__ void __launch_bounds__(256) conv_gemm_kernel(const ConvArgs a, int n_tiles, int se_imgs) {
+__global__ void __launch_bounds__(256, (BN >= 256 ? 2 : 1)) conv_gemm_kernel(const ConvArgs a, int n_tiles, int se_imgs) {
   constexpr int WN = BN / (NT * 16);
   constexpr int WM = 4 / WN;
   static_assert(WM * WN == 4 && WM * MT * 16 == BM, "bad tile");
@@ -332,7 +332,8 @@ const char* kname(int k) {
 
 template <int BM, int BN, int MT, int NT, int KIND, int XF>
 void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
-  constexpr int S = (BM >= 256 || BM + BN >= 384) ? 3 : 4;  // keep two workgroups' LDS per CU
+  // keep two workgroups' LDS per CU (128 x 256: the SE gate table too, and 256 registers a wave)
+  constexpr int S = BN >= 256 ? 2 : ((BM >= 256 || BM + BN >= 384) ? 3 : 4);
   static bool attr = [] {
     M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
