@@ -366,9 +366,10 @@ void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, 
     const char* e = getenv("M2S_GEMM_BIG");
     return e ? atoi(e) : 1;
   }();
-  if constexpr (KIND == KIND_GEMM) if (big && a.M >= 256 * 256 && n > 128 && n <= 256 && a.kp >= 512) {
-    // long-K 1x1 GEMMs with 129..256 outputs: one 256-wide n tile reads the activations once
-    // instead of twice (b5 conv_pwl 1248 -> 208: 13.5 -> 10.0 ms per 4 steps).  A 256x128 tile
+  if constexpr (KIND == KIND_GEMM || KIND == KIND_CONV2D) if (big && a.M >= 256 * 256 && n > 128 && n <= 256 && a.kp >= 512) {
+    // long-K 1x1 GEMMs and 3x3 convs with 129..256 outputs: one 256-wide n tile reads (gathers)
+    // the activations once instead of twice (b5 conv_pwl 1248 -> 208: 13.5 -> 10.0 ms per 4 steps;
+    // b2 conv_exp 3x3 56 -> 224: 1.10 -> 0.91 ms per launch).  A 256x128 tile
     // for n <= 128 measured slower at every K (one wave per SIMD at 272 registers).
     return launch_tile<128, 256, 4, 8, KIND, XF>(a, s, phases, flops, bytes);
   }
