@@ -52,6 +52,12 @@ void launch_stem_b0(const float* frames, int N, int H, int W, int OH, int OW, in
                     const float* b9, const bf16_t* w0, const float* b0, int kp0, const bf16_t* w1, const float* b1,
                     int kp1, bf16_t* y, double flops, double bytes, hipStream_t s);
 
+// bf16 SqueezeExcite excitation: gate (N, cs_mid) = sigmoid(W2 · SiLU(W1 · mean + b1) + b2), mean (N, cs_mid)
+// from the squeeze; w1 packed [>= rd][kp1], w2 packed [>= mid][kp2].  (se_excite.hip)
+bool se_excite_supported(int rd, int kp2, int cs_mid);
+void launch_se_excite(const bf16_t* mean, int N, int mid, int cs_mid, const bf16_t* w1, int kp1, const float* b1,
+                      int rd, const bf16_t* w2, int kp2, const float* b2, bf16_t* gate, hipStream_t s);
+
 // Decoded frames -> model input: uint8 (N,H,W) grey or (N,H,W,3) BGR -> fp32 (N,H,W) in [0, 1]
 // (_preprocess_frame, run_mri_video_inference.py:34-54, minus the host-side resize).  (preprocess.hip)
 void launch_preprocess(const uint8_t* frames, int N, int H, int W, int channels, float* out, hipStream_t s);

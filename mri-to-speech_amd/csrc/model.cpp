@@ -203,6 +203,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   M2S_CHECK(n_mels > 0 && hidden > 0 && hidden % 8 == 0, "bad n_mels / rnn_hidden");
   if (const char* e = std::getenv("M2S_IR_FUSED")) ir_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_SE_FUSED")) se_fused_ = std::strcmp(e, "0") != 0;
   const std::string P = "cnn.backbone.";
   {  // stem: fold repeat(1,3,1,1) by summing the 3 input channels; then BN
     const float* w = need(sd, P + "conv_stem.weight", {EFF_STEM, 3, 3, 3}).data;
@@ -516,6 +517,11 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
           launch_se_mean<T>(sums, nc, dw_pixel_blocks(nh, nw), cs, 1.0f / (float)(nh * nw), se_mean, s);
         }
         }
+        if (std::is_same<T, bf16_t>::value && se_fused_ && se_excite_supported(b.rd, b.se2.kp, cs)) {
+          launch_se_excite(reinterpret_cast<const bf16_t*>(se_mean), nc, b.mid, cs, static_cast<const bf16_t*>(b.se1.w),
+                           b.se1.kp, b.se1.b, b.rd, static_cast<const bf16_t*>(b.se2.w), b.se2.kp, b.se2.b,
+                           reinterpret_cast<bf16_t*>(scale), s);
+        } else {
         ConvArgs r1 = conv_args(b.se1);  // conv_reduce + SiLU, all images of the chunk at once
         r1.x = se_mean;
         r1.y = se_hid;
@@ -528,6 +534,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         r2.M = nc;
         r2.act = ACT_SIGMOID;
         run_conv<T>(r2, b.se2, s);
+        }
         ConvArgs p = conv_args(b.c2);
         p.x = M2;
         p.y = nxt;

@@ -84,6 +84,7 @@ class Acoustic {
   int chunk = 256;
   bool ir_fused_ = true;  // bf16: fused conv_pw + conv_dw + SE squeeze (env M2S_IR_FUSED=0 disables)
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
+  bool se_fused_ = true;    // bf16: SE excitation in one kernel (env M2S_SE_FUSED=0: two GEMMs)
 
   size_t workspace_bytes(int B, int T, int H, int W) const;
   void forward(const float* frames, int B, int T, int H, int W, float* mel_norm, void* ws, size_t wsb, hipStream_t s);

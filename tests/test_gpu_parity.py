@@ -203,21 +203,23 @@ def test_effnet_bf16_ir_fused_every_block(rt, ac_state, monkeypatch, hw):
     assert _cos(ga, gb) >= 0.99999
 
 
+@pytest.mark.parametrize("env,blocks", [("M2S_STEM_FUSED", (2, 3, 6, -1)), ("M2S_SE_FUSED", (9, 14, 20, -1))])
 @pytest.mark.parametrize("hw", [(256, 256), (96, 80), (67, 101)])
-def test_effnet_bf16_stem_b0_fused(rt, ac_state, monkeypatch, hw):
-    """The fused stem + blocks.0 kernel (stem_b0.hip) against the separate stem / 3x3 conv launches
-    and the fp32 oracle: the blocks.0 output (probe 2), every later block, the pooled features;
-    odd sizes exercise the TF-SAME bottom/right stem pad and the partial 16 x 16 tiles."""
+def test_effnet_bf16_fused_kernels_vs_unfused(rt, ac_state, monkeypatch, hw, env, blocks):
+    """The fused stem + blocks.0 kernel (stem_b0.hip) and the one-kernel SE excitation
+    (se_excite.hip) against the separate launches they replace and the fp32 oracle, block by block
+    and on the pooled features; odd sizes exercise the TF-SAME bottom/right stem pad and partial
+    16 x 16 tiles, and a 3-frame batch a partial 8-image SE group."""
     sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
-    fr = torch.from_numpy(synth.synth_frames(1, 2, hw=hw, seed=47)[0])
+    fr = torch.from_numpy(synth.synth_frames(1, 3, hw=hw, seed=47)[0])
     taps = []
     effnet.effnet_features(sd, fr, taps=taps)
-    monkeypatch.setenv("M2S_STEM_FUSED", "1")
+    monkeypatch.setenv(env, "1")
     fused = rt.AcousticEngine(ac_state[1], dtype="bf16", device=DEV)
-    monkeypatch.setenv("M2S_STEM_FUSED", "0")
+    monkeypatch.setenv(env, "0")
     plain = rt.AcousticEngine(ac_state[1], dtype="bf16", device=DEV)
     x = fr.to(DEV)
-    for i in (2, 3, 6, len(taps) - 1):
+    for i in [b if b >= 0 else len(taps) - 1 for b in blocks]:
         a = fused.probe(x, i).float().cpu().numpy()
         b = plain.probe(x, i).float().cpu().numpy()
         assert np.isfinite(a).all()
