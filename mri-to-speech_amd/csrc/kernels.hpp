@@ -58,6 +58,12 @@ bool se_excite_supported(int rd, int kp2, int cs_mid);
 void launch_se_excite(const bf16_t* mean, int N, int mid, int cs_mid, const bf16_t* w1, int kp1, const float* b1,
                       int rd, const bf16_t* w2, int kp2, const float* b2, bf16_t* gate, hipStream_t s);
 
+// bf16 EdgeResidual (stride 1, skip) 32 -> 128 -> 32: conv_exp 3x3 + SiLU, conv_pwl 1x1, + x in one
+// persistent kernel; x, y (N,H,W,32); wexp / wpwl in the kernel's fragment orders.  (er_fused.hip)
+bool er_fused_supported(int H, int W, int cin, int mid, int cout, int kp_exp, int kp_pwl);
+void launch_er_fused(const bf16_t* x, int N, int H, int W, const bf16_t* wexp, const float* bexp, const bf16_t* wpwl,
+                     const float* bpwl, bf16_t* y, double flops, double bytes, hipStream_t s);
+
 // Decoded frames -> model input: uint8 (N,H,W) grey or (N,H,W,3) BGR -> fp32 (N,H,W) in [0, 1]
 // (_preprocess_frame, run_mri_video_inference.py:34-54, minus the host-side resize).  (preprocess.hip)
 void launch_preprocess(const uint8_t* frames, int N, int H, int W, int channels, float* out, hipStream_t s);

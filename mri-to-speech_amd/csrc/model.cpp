@@ -204,6 +204,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_IR_FUSED")) ir_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_FUSED")) se_fused_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_ER_FUSED")) er_fused_ = std::strcmp(e, "0") != 0;
   const std::string P = "cnn.backbone.";
   {  // stem: fold repeat(1,3,1,1) by summing the 3 input channels; then BN
     const float* w = need(sd, P + "conv_stem.weight", {EFF_STEM, 3, 3, 3}).data;
@@ -249,6 +250,33 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
         b.mid = make_divisible(cin * (double)sdf.exp);
         conv2d_kxk(b.c1, q + "conv_exp.weight", cin, b.mid, fold_bn(sd, q + "bn1", b.mid));
         conv1x1(b.c2, q + "conv_pwl.weight", b.mid, b.cout, fold_bn(sd, q + "bn2", b.cout));
+        if (dtype == M2S_DT_BF16 && b.stride == 1 && b.skip && k == 3 &&
+            er_fused_supported(64, 64, cin, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
+          // er_fused.hip operand orders: conv_exp [tap][n16][lane][8] (lane = (k8 group, row));
+          // conv_pwl [n16][k-step][lane][8] with the k-slot permutation of the kernel's header
+          const float* we = need(sd, q + "conv_exp.weight", {b.mid, cin, 3, 3}).data;
+          const float* wq = need(sd, q + "conv_pwl.weight", {b.cout, b.mid, 1, 1}).data;
+          const BN e1 = fold_bn(sd, q + "bn1", b.mid), e2 = fold_bn(sd, q + "bn2", b.cout);
+          std::vector<uint16_t> fe((size_t)9 * 8 * 64 * 8), fp((size_t)2 * 4 * 64 * 8);
+          for (int t = 0; t < 9; ++t)
+            for (int nt = 0; nt < 8; ++nt)
+              for (int ln = 0; ln < 64; ++ln)
+                for (int e = 0; e < 8; ++e) {
+                  const int n = nt * 16 + (ln & 15), c = 8 * (ln >> 4) + e;
+                  fe[(((size_t)t * 8 + nt) * 64 + ln) * 8 + e] = f2bf_host(we[((size_t)n * cin + c) * 9 + t] * e1.a[n]);
+                }
+          for (int on = 0; on < 2; ++on)
+            for (int ks = 0; ks < 4; ++ks)
+              for (int ln = 0; ln < 64; ++ln)
+                for (int e = 0; e < 8; ++e) {
+                  const int n = on * 16 + (ln & 15), g4 = 4 * (ln >> 4);
+                  const int c = 32 * ks + (e < 4 ? g4 + e : 16 + g4 + e - 4);
+                  fp[(((size_t)on * 4 + ks) * 64 + ln) * 8 + e] = f2bf_host(wq[(size_t)n * b.mid + c] * e2.a[n]);
+                }
+          b.er_wexp = arena_.add_vec(fe);
+          b.er_wpwl = arena_.add_vec(fp);
+          b.er_frag = true;
+        }
       } else {
         b.mid = make_divisible(cin * (double)sdf.exp);
         b.rd = (int)std::lround(b.mid * (sdf.se / sdf.exp));
@@ -476,6 +504,13 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         a.act = ACT_SILU;
         a.res = b.skip ? cur : nullptr;
         run_conv<T>(a, b.c1, s);
+      } else if (b.type == 1 && std::is_same<T, bf16_t>::value && er_fused_ && b.er_frag &&
+                 er_fused_supported(nh, nw, b.cin, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
+        const double px = (double)nc * nh * nw;
+        launch_er_fused(reinterpret_cast<const bf16_t*>(cur), nc, nh, nw,
+                        static_cast<const bf16_t*>(arena_.ptr(b.er_wexp)), b.c1.b,
+                        static_cast<const bf16_t*>(arena_.ptr(b.er_wpwl)), b.c2.b, reinterpret_cast<bf16_t*>(nxt),
+                        2.0 * px * b.mid * (9.0 * b.cin + b.cout), 2.0 * px * (2.0 * b.cin) + 2.0 * (9.0 * 32 * 128 + 128 * 32), s);
       } else if (b.type == 1) {
         ConvArgs a = a2d(b.c1, cur, M);
         a.act = ACT_SILU;

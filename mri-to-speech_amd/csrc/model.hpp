@@ -85,6 +85,7 @@ class Acoustic {
   bool ir_fused_ = true;  // bf16: fused conv_pw + conv_dw + SE squeeze (env M2S_IR_FUSED=0 disables)
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
   bool se_fused_ = true;    // bf16: SE excitation in one kernel (env M2S_SE_FUSED=0: two GEMMs)
+  bool er_fused_ = true;    // bf16: EdgeResidual 32->128->32 in one kernel (env M2S_ER_FUSED=0 disables)
 
   size_t workspace_bytes(int B, int T, int H, int W) const;
   void forward(const float* frames, int B, int T, int H, int W, float* mel_norm, void* ws, size_t wsb, hipStream_t s);
@@ -101,6 +102,8 @@ class Acoustic {
     size_t dw_w = 0, dw_b = 0;  // ir depthwise, tap-major (9 x cs_mid) and (cs_mid), fp32
     size_t dw_w2 = 0;           // bf16 engines: the same taps as bf16 in the channel's dword half
     PConv se1, se2;             // ir SE: conv_reduce (mid -> rd, SiLU), conv_expand (rd -> mid, sigmoid)
+    size_t er_wexp = 0, er_wpwl = 0;  // bf16 er 32 -> 128 -> 32 stride 1: fused-kernel fragment orders
+    bool er_frag = false;
   };
   template <typename T>
   void effnet_t(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe, int* probe_dims,
