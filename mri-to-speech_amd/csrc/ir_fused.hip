@@ -25,7 +25,10 @@
 namespace m2s {
 namespace {
 
-constexpr int SL = 32;         // expanded channels per slice
+#ifndef IRF_SL
+#define IRF_SL 32
+#endif
+constexpr int SL = IRF_SL;         // expanded channels per slice
 #ifndef IRF_MROW
 #define IRF_MROW (SL + 8)
 #endif
@@ -47,7 +50,7 @@ __device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float acc) {
 }
 
 template <int MT, int G>
-__global__ void __launch_bounds__(256, 4) ir_pwdw_kernel(const bf16_t* __restrict__ x, int cs_in, int kp,
+__global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : 2)) ir_pwdw_kernel(const bf16_t* __restrict__ x, int cs_in, int kp,
                                                          const bf16_t* __restrict__ wpw, const float* __restrict__ bpw,
                                                          const uint32_t* __restrict__ wdw2,
                                                          const float* __restrict__ bdw, int N, int OH, int OW,

@@ -64,6 +64,14 @@ bool er_fused_supported(int H, int W, int cin, int mid, int cout, int kp_exp, in
 void launch_er_fused(const bf16_t* x, int N, int H, int W, const bf16_t* wexp, const float* bexp, const bf16_t* wpwl,
                      const float* bpwl, bf16_t* y, double flops, double bytes, hipStream_t s);
 
+// bf16 EdgeResidual (stride 1, skip) 56 -> 224 -> 56 (channel strides 64 / 224 / 64): same fusion with the
+// weights streamed through an LDS ring; wst = er2_stage_elems() bf16 in the kernel's stage order.
+// (er2_fused.hip)
+bool er2_fused_supported(int H, int W, int cs_in, int mid, int cout, int kp_exp, int kp_pwl);
+int er2_stage_elems();
+void launch_er2_fused(const bf16_t* x, int N, int H, int W, const bf16_t* wst, const float* bexp, const float* bpwl,
+                      bf16_t* y, double flops, double bytes, hipStream_t s);
+
 // Decoded frames -> model input: uint8 (N,H,W) grey or (N,H,W,3) BGR -> fp32 (N,H,W) in [0, 1]
 // (_preprocess_frame, run_mri_video_inference.py:34-54, minus the host-side resize).  (preprocess.hip)
 void launch_preprocess(const uint8_t* frames, int N, int H, int W, int channels, float* out, hipStream_t s);

@@ -276,6 +276,33 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
           b.er_wexp = arena_.add_vec(fe);
           b.er_wpwl = arena_.add_vec(fp);
           b.er_frag = true;
+        } else if (dtype == M2S_DT_BF16 && b.stride == 1 && b.skip && k == 3 &&
+                   er2_fused_supported(32, 32, b.c1.cs_in, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
+          // er2_fused.hip stage stream [20][16 pieces][lane][8]: stages 0..17 = conv_exp k-step s (tap
+          // s / 2, input channels 32 (s % 2) ..), piece = n16; stages 18 / 19 = conv_pwl k-steps 0..3 /
+          // 4..6, piece = local k-step * 4 + n16, with er_fused.hip's k-slot permutation
+          const float* we = need(sd, q + "conv_exp.weight", {b.mid, cin, 3, 3}).data;
+          const float* wq = need(sd, q + "conv_pwl.weight", {b.cout, b.mid, 1, 1}).data;
+          const BN e1 = fold_bn(sd, q + "bn1", b.mid), e2 = fold_bn(sd, q + "bn2", b.cout);
+          std::vector<uint16_t> st((size_t)er2_stage_elems(), 0);
+          for (int sg = 0; sg < 20; ++sg)
+            for (int pc = 0; pc < 16; ++pc)
+              for (int ln = 0; ln < 64; ++ln)
+                for (int e = 0; e < 8; ++e) {
+                  const int row = ln & 15, g8 = ln >> 4;
+                  float v = 0.f;
+                  if (sg < 18) {
+                    const int n = 16 * pc + row, c = (sg & 1) * 32 + 8 * g8 + e, t = sg >> 1;
+                    if (pc < 14 && c < cin) v = we[((size_t)n * cin + c) * 9 + t] * e1.a[n];
+                  } else {
+                    const int kk = pc >> 2, n = 16 * (pc & 3) + row, ks = (sg == 18 ? 0 : 4) + kk;
+                    const int c = 32 * ks + (e < 4 ? 4 * g8 + e : 16 + 4 * g8 + e - 4);
+                    if ((sg == 18 || kk < 3) && n < b.cout) v = wq[(size_t)n * b.mid + c] * e2.a[n];
+                  }
+                  st[(((size_t)sg * 16 + pc) * 64 + ln) * 8 + e] = f2bf_host(v);
+                }
+          b.er_wexp = arena_.add_vec(st);
+          b.er_frag = true;
         }
       } else {
         b.mid = make_divisible(cin * (double)sdf.exp);
@@ -511,6 +538,12 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                         static_cast<const bf16_t*>(arena_.ptr(b.er_wexp)), b.c1.b,
                         static_cast<const bf16_t*>(arena_.ptr(b.er_wpwl)), b.c2.b, reinterpret_cast<bf16_t*>(nxt),
                         2.0 * px * b.mid * (9.0 * b.cin + b.cout), 2.0 * px * (2.0 * b.cin) + 2.0 * (9.0 * 32 * 128 + 128 * 32), s);
+      } else if (b.type == 1 && std::is_same<T, bf16_t>::value && er_fused_ && b.er_frag &&
+                 er2_fused_supported(nh, nw, b.c1.cs_in, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
+        const double px = (double)nc * nh * nw;
+        launch_er2_fused(reinterpret_cast<const bf16_t*>(cur), nc, nh, nw, static_cast<const bf16_t*>(arena_.ptr(b.er_wexp)),
+                         b.c1.b, b.c2.b, reinterpret_cast<bf16_t*>(nxt), 2.0 * px * b.mid * (9.0 * b.cin + b.cout),
+                         2.0 * px * (2.0 * b.c1.cs_in) + 2.0 * er2_stage_elems(), s);
       } else if (b.type == 1) {
         ConvArgs a = a2d(b.c1, cur, M);
         a.act = ACT_SILU;
