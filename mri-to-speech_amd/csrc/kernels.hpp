@@ -72,6 +72,15 @@ int er2_stage_elems();
 void launch_er2_fused(const bf16_t* x, int N, int H, int W, const bf16_t* wst, const float* bexp, const float* bpwl,
                       bf16_t* y, double flops, double bytes, hipStream_t s);
 
+// bf16 whole InvertedResidual (stride 1, 16x16 maps, channel strides 128 / <= 736 / 128): conv_pw + SiLU,
+// conv_dw + SiLU, SqueezeExcite, conv_pwl (+ skip) in one kernel; wst = (cs_mid / 32) stages of
+// ir_block_stage_bytes() in the kernel's order; w1 / w2 / b1 / b2 the packed SE convs.  (ir_block.hip)
+bool ir_block_supported(int H, int W, int cs_in, int cs_mid, int cs_out, int rd, int kp1, int kp2);
+int ir_block_stage_bytes();
+void launch_ir_block(const bf16_t* x, int N, const bf16_t* wst, int mid, int cs_mid, const bf16_t* w1, int kp1,
+                     const float* b1, int rd, const bf16_t* w2, int kp2, const float* b2, const float* bpwl, bool skip,
+                     bf16_t* y, double flops, double bytes, hipStream_t s);
+
 // Decoded frames -> model input: uint8 (N,H,W) grey or (N,H,W,3) BGR -> fp32 (N,H,W) in [0, 1]
 // (_preprocess_frame, run_mri_video_inference.py:34-54, minus the host-side resize).  (preprocess.hip)
 void launch_preprocess(const uint8_t* frames, int N, int H, int W, int channels, float* out, hipStream_t s);

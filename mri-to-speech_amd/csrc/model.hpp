@@ -85,6 +85,7 @@ class Acoustic {
   bool ir_fused_ = true;  // bf16: fused conv_pw + conv_dw + SE squeeze (env M2S_IR_FUSED=0 disables)
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
   bool se_fused_ = true;    // bf16: SE excitation in one kernel (env M2S_SE_FUSED=0: two GEMMs)
+  bool ir_block_ = false;   // bf16: whole InvertedResidual at 16x16 in one kernel (opt-in: env M2S_IR_BLOCK=1)
   bool er_fused_ = true;    // bf16: EdgeResidual 32->128->32 in one kernel (env M2S_ER_FUSED=0 disables)
 
   size_t workspace_bytes(int B, int T, int H, int W) const;
@@ -104,6 +105,8 @@ class Acoustic {
     PConv se1, se2;             // ir SE: conv_reduce (mid -> rd, SiLU), conv_expand (rd -> mid, sigmoid)
     size_t er_wexp = 0, er_wpwl = 0;  // bf16 er 32 -> 128 -> 32 stride 1: fused-kernel fragment orders
     bool er_frag = false;
+    size_t ib_w = 0;  // bf16 ir stride 1 at 16x16: ir_block.hip stage stream
+    bool ib = false;
   };
   template <typename T>
   void effnet_t(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe, int* probe_dims,
