@@ -38,7 +38,9 @@ PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA peaks, MI355X_MICROA
 PEAK_HBM_GBS = 8000.0
 
 
-MFMA_KERNELS = ("conv_gemm_kernel", "conv_halo_kernel", "conv_igemm_kernel", "ir_pwdw_kernel", "lstm_persistent_kernel")
+MFMA_KERNELS = ("conv_gemm_kernel", "conv_halo_kernel", "conv_igemm_kernel", "ir_pwdw_kernel", "lstm_persistent_kernel",
+                "rb1_fused_kernel", "stem_b0_kernel", "se_excite_kernel", "er_fused_kernel", "er2_fused_kernel",
+                "ir_block_kernel")
 
 
 def pmc_traffic(kernel):

@@ -79,7 +79,7 @@ constexpr int ROW = 64;  // bytes per LDS row = 32 bf16 = one k-step
 __device__ __forceinline__ int swz(int row, int chunk) { return row * ROW + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
 template <int BM, int BN, int MT, int NT, int S, int KIND, int XF>
-__global__ void __launch_bounds__(256, (BN >= 256 ? 2 : 1)) conv_gemm_kernel(const ConvArgs a, int n_tiles, int se_imgs) {
+__global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 2 : 1)) conv_gemm_kernel(const ConvArgs a, int n_tiles, int se_imgs) {
   constexpr int WN = BN / (NT * 16);
   constexpr int WM = 4 / WN;
   static_assert(WM * WN == 4 && WM * MT * 16 == BM, "bad tile");
@@ -333,7 +333,7 @@ const char* kname(int k) {
 template <int BM, int BN, int MT, int NT, int KIND, int XF>
 void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
   // keep two workgroups' LDS per CU (128 x 256: the SE gate table too, and 256 registers a wave)
-  constexpr int S = BN >= 256 ? 2 : ((BM >= 256 || BM + BN >= 384) ? 3 : 4);
+  constexpr int S = (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
   static bool attr = [] {
     M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -372,6 +372,15 @@ void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, 
     // b2 conv_exp 3x3 56 -> 224: 1.10 -> 0.91 ms per launch).  A 256x128 tile
     // for n <= 128 measured slower at every K (one wave per SIMD at 272 registers).
     return launch_tile<128, 256, 4, 8, KIND, XF>(a, s, phases, flops, bytes);
+  }
+  static const int tall = [] {  // M2S_GEMM_TALL=0 keeps the 128x128 tile for long-K GEMMs with n <= 128
+    const char* e = getenv("M2S_GEMM_TALL");
+    return e ? atoi(e) : 1;
+  }();
+  if constexpr (KIND == KIND_GEMM) if (tall && a.M >= 256 * 256 && n > 64 && n <= 128 && a.kp >= 384) {
+    // 256 rows x 128 outputs at two waves per SIMD: the weight tile (K x 128) is re-read from L2
+    // once per 256 rows instead of per 128 (the SE-scaled conv_pwl of blocks.3/4: K 416..736)
+    return launch_tile<256, 128, 8, 4, KIND, XF>(a, s, phases, flops, bytes);
   }
   if (n <= 16)
     launch_tile<256, 16, 4, 1, KIND, XF>(a, s, phases, flops, bytes);

@@ -3,7 +3,7 @@
 OUT=gpurun_out/ibpmc
 mkdir -p $OUT
 export TMPDIR=/tmp
-cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES --kernel-include-regex "ir_block|er2_fused" --output-format csv -d /root/repo/$OUT -o pmc -- python3 /root/repo/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-profile > /root/repo/$OUT/log 2>&1
+cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES --kernel-include-regex "${IBPMC_RE:-ir_block|er2_fused}" --output-format csv -d /root/repo/$OUT -o pmc -- python3 /root/repo/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-profile > /root/repo/$OUT/log 2>&1
 rc=$?
 cd /root/repo && python3 - <<'P'
 import csv, glob, collections
