@@ -72,6 +72,16 @@ int er2_stage_elems();
 void launch_er2_fused(const bf16_t* x, int N, int H, int W, const bf16_t* wst, const float* bexp, const float* bpwl,
                       bf16_t* y, double flops, double bytes, hipStream_t s);
 
+// bf16 stride-2 EdgeResidual (no skip), (cs_in, mid, cs_out) in {(16, 64, 32), (32, 128, 64)}: conv_exp
+// 3x3/s2 TF-SAME + SiLU -> conv_pwl; x (N,H,W,cs_in) -> y (N,OH,OW,cs_out); wexp ers2_exp_elems() bf16 in
+// the kernel's fragment order, wpwl [cs_out/16][mid/32][64][8] with er_fused.hip's K permutation.
+// (ers2_fused.hip)
+bool ers2_fused_supported(int OH, int OW, int cs_in, int mid, int cs_out, int kp_exp, int kp_pwl);
+int ers2_exp_elems(int cs_in, int mid);
+void launch_ers2_fused(const bf16_t* x, int N, int H, int W, int OH, int OW, int pad_t, int pad_l, int cs_in, int mid,
+                       int cs_out, const bf16_t* wexp, const float* bexp, const bf16_t* wpwl, const float* bpwl,
+                       bf16_t* y, double flops, double bytes, hipStream_t s);
+
 // bf16 whole InvertedResidual (stride 1, 16x16 maps, channel strides 128 / <= 736 / 128): conv_pw + SiLU,
 // conv_dw + SiLU, SqueezeExcite, conv_pwl (+ skip) in one kernel; wst = (cs_mid / 32) stages of
 // ir_block_stage_bytes() in the kernel's order; w1 / w2 / b1 / b2 the packed SE convs.  (ir_block.hip)

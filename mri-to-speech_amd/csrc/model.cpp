@@ -304,6 +304,36 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
                 }
           b.er_wexp = arena_.add_vec(st);
           b.er_frag = true;
+        } else if (dtype == M2S_DT_BF16 && b.stride == 2 && k == 3 &&
+                   ers2_fused_supported(8, 16, b.c1.cs_in, b.mid, chan_stride(b.cout), b.c1.kp, b.c2.kp)) {
+          // ers2_fused.hip: conv_exp [k-step][n16][lane][8] (CIN 16: lane groups 0-1 tap 2s, 2-3 tap
+          // 2s + 1; CIN 32: tap s), conv_pwl [n16][k-step][lane][8] with the permuted K
+          const int csi = b.c1.cs_in, cso = chan_stride(b.cout), ks_n = (9 * csi + 31) / 32;
+          const float* we = need(sd, q + "conv_exp.weight", {b.mid, cin, 3, 3}).data;
+          const float* wq = need(sd, q + "conv_pwl.weight", {b.cout, b.mid, 1, 1}).data;
+          const BN e1 = fold_bn(sd, q + "bn1", b.mid), e2 = fold_bn(sd, q + "bn2", b.cout);
+          std::vector<uint16_t> fe((size_t)ers2_exp_elems(csi, b.mid), 0), fp((size_t)cso * b.mid, 0);
+          for (int s2 = 0; s2 < ks_n; ++s2)
+            for (int nt = 0; nt < b.mid / 16; ++nt)
+              for (int ln = 0; ln < 64; ++ln)
+                for (int e = 0; e < 8; ++e) {
+                  const int g8 = ln >> 4, n = nt * 16 + (ln & 15);
+                  const int t = csi == 16 ? 2 * s2 + (g8 >> 1) : s2, c = csi == 16 ? 8 * (g8 & 1) + e : 8 * g8 + e;
+                  const float v = t < 9 && c < cin ? we[((size_t)n * cin + c) * 9 + t] * e1.a[n] : 0.f;
+                  fe[(((size_t)s2 * (b.mid / 16) + nt) * 64 + ln) * 8 + e] = f2bf_host(v);
+                }
+          for (int on = 0; on < cso / 16; ++on)
+            for (int ks = 0; ks < b.mid / 32; ++ks)
+              for (int ln = 0; ln < 64; ++ln)
+                for (int e = 0; e < 8; ++e) {
+                  const int n = on * 16 + (ln & 15), g4 = 4 * (ln >> 4);
+                  const int c = 32 * ks + (e < 4 ? g4 + e : 16 + g4 + e - 4);
+                  const float v = n < b.cout ? wq[(size_t)n * b.mid + c] * e2.a[n] : 0.f;
+                  fp[(((size_t)on * (b.mid / 32) + ks) * 64 + ln) * 8 + e] = f2bf_host(v);
+                }
+          b.er_wexp = arena_.add_vec(fe);
+          b.er_wpwl = arena_.add_vec(fp);
+          b.er_frag = true;
         }
       } else {
         b.mid = make_divisible(cin * (double)sdf.exp);
@@ -587,6 +617,14 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         launch_er2_fused(reinterpret_cast<const bf16_t*>(cur), nc, nh, nw, static_cast<const bf16_t*>(arena_.ptr(b.er_wexp)),
                          b.c1.b, b.c2.b, reinterpret_cast<bf16_t*>(nxt), 2.0 * px * b.mid * (9.0 * b.cin + b.cout),
                          2.0 * px * (2.0 * b.c1.cs_in) + 2.0 * er2_stage_elems(), s);
+      } else if (b.type == 1 && std::is_same<T, bf16_t>::value && er_fused_ && b.er_frag && b.stride == 2 &&
+                 ers2_fused_supported(nh, nw, b.c1.cs_in, b.mid, chan_stride(b.cout), b.c1.kp, b.c2.kp)) {
+        const double px = (double)nc * nh * nw;
+        launch_ers2_fused(reinterpret_cast<const bf16_t*>(cur), nc, oh, ow, nh, nw, qt, ql, b.c1.cs_in, b.mid,
+                          chan_stride(b.cout), static_cast<const bf16_t*>(arena_.ptr(b.er_wexp)), b.c1.b,
+                          static_cast<const bf16_t*>(arena_.ptr(b.er_wpwl)), b.c2.b, reinterpret_cast<bf16_t*>(nxt),
+                          2.0 * px * b.mid * (9.0 * b.cin + b.cout),
+                          2.0 * ((double)nc * oh * ow * b.c1.cs_in + px * chan_stride(b.cout)), s);
       } else if (b.type == 1) {
         ConvArgs a = a2d(b.c1, cur, M);
         a.act = ACT_SILU;

@@ -204,11 +204,12 @@ def test_effnet_bf16_ir_fused_every_block(rt, ac_state, monkeypatch, hw):
 
 
 @pytest.mark.parametrize("env,blocks", [("M2S_STEM_FUSED", (2, 3, 6, -1)), ("M2S_SE_FUSED", (9, 14, 20, -1)),
-                                        ("M2S_ER_FUSED", (4, 5, 6, 7, 8, -1)), ("M2S_IR_BLOCK", (10, 12, 13, 18, -1))])
+                                        ("M2S_ER_FUSED", (3, 4, 5, 6, 7, 8, -1)), ("M2S_IR_BLOCK", (10, 12, 13, 18, -1))])
 @pytest.mark.parametrize("hw", [(256, 256), (96, 80), (67, 101)])
 def test_effnet_bf16_fused_kernels_vs_unfused(rt, ac_state, monkeypatch, hw, env, blocks):
     """The fused stem + blocks.0 kernel (stem_b0.hip), the one-kernel SE excitation (se_excite.hip)
-    the fused EdgeResidual (er_fused.hip / er2_fused.hip: blocks.1.1/.2 at 64x64, blocks.2.1/.2 at 32x32)
+    the fused EdgeResidual (er_fused.hip / er2_fused.hip: blocks.1.1/.2 at 64x64, blocks.2.1/.2 at 32x32;
+    ers2_fused.hip: the stride-2 blocks.1.0 / blocks.2.0)
     and the whole-InvertedResidual kernel (ir_block.hip: blocks.3.1-3, blocks.4.* at 16x16; 96x80 and 67x101 give maps
     that are not multiples of 16, where the unfused path must take over) against the separate
     launches they replace and the fp32 oracle, block by block
