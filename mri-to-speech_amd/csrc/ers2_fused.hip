@@ -9,7 +9,7 @@
 // [8-channel chunk][parity][row][column / 2] with 17-pixel rows, so the 16 pixels of a B-fragment read
 // (input columns 2 x + kx) are 16 consecutive 16-byte slots: conflict-free at every tap.  With
 // CIN = 16 a 32-deep k-step covers two taps (lane groups 0-1: tap 2s, 2-3: tap 2s + 1).
-// Persistent workgroups (one per CU, 8 waves): conv_exp's weights are DMA'd into LDS once, the next
+// Persistent workgroups (8 waves; one per CU, two for blocks.1.0): conv_exp's weights are DMA'd into LDS once, the next
 // tile's halo lands in the second buffer while the current tile computes, conv_pwl's weights and the
 // biases stay in VGPRs.
 #include <algorithm>
@@ -48,7 +48,7 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 template <int CIN, int MID, int CO>
-__global__ void __launch_bounds__(512, 1) ers2_fused_kernel(const Es2Args a) {
+__global__ void __launch_bounds__(512, (CIN == 16 ? 2 : 1)) ers2_fused_kernel(const Es2Args a) {
   constexpr int NCH = CIN / 8;             // input chunks
   constexpr int KS = (9 * CIN + 31) / 32;  // conv_exp k-steps
   constexpr int NT = MID / 16;             // conv_exp n16 tiles
@@ -175,7 +175,8 @@ void launch_cfg(const Es2Args& a, double flops, double bytes, hipStream_t s) {
     M2S_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev));
     return v > 0 ? v : 256;
   }();
-  const int grid = std::min(a.N * a.tiles_x * a.tiles_y, cus);
+  // CIN 16: 60 KB of LDS and < 128 VGPRs, so two workgroups per CU
+  const int grid = std::min(a.N * a.tiles_x * a.tiles_y, (CIN == 16 ? 2 : 1) * cus);
   char name[64];
   snprintf(name, sizeof(name), "ers2_fused_kernel<%d, %d, %d>", CIN, MID, CO);
   ProfScope ps(name, flops, bytes, s);
