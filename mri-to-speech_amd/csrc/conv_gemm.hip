@@ -47,23 +47,28 @@ __device__ __forceinline__ bf16x8 lrelu_frag(bf16x8 v, float slope) {
 // SE scales come from an LDS table.  Read through inline asm (loads + wait in ONE statement,
 // cdna_hip_programming.md §5.7 form (i)): a plain ds_read there makes hipcc assume it may alias
 // the in-flight LDS-DMA and drain the whole pipeline with vmcnt(0) every step.
-__device__ __forceinline__ bf16x8 scale_frag(bf16x8 v, const float* s) {
-  uint4 u = __builtin_bit_cast(uint4, v);
-  uint32_t w[4] = {u.x, u.y, u.z, u.w};
+__device__ __forceinline__ void load_scales(const float* s, float* sc) {
   float4 s0, s1;
   const uint32_t addr = (uint32_t)(uintptr_t)s;
   asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
                : "=&v"(s0), "=&v"(s1)
                : "v"(addr)
                : "memory");
-  const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+  sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+}
+__device__ __forceinline__ bf16x8 scale_with(bf16x8 v, const float* sc) {
+  uint4 u = __builtin_bit_cast(uint4, v);
+  uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float lo = __uint_as_float(w[j] << 16) * sc[2 * j];
-    const float hi = __uint_as_float(w[j] & 0xffff0000u) * sc[2 * j + 1];
-    w[j] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
-  }
+  for (int j = 0; j < 4; ++j)
+    w[j] = pack_bf16x2(__uint_as_float(w[j] << 16) * sc[2 * j], __uint_as_float(w[j] & 0xffff0000u) * sc[2 * j + 1]);
   return __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3]));
+}
+__device__ __forceinline__ bf16x8 scale_frag(bf16x8 v, const float* s) {
+  float sc[8];
+  load_scales(s, sc);
+  return scale_with(v, sc);
 }
 
 __device__ __forceinline__ void ld4f(const bf16_t* p, float* v) {
@@ -215,6 +220,10 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
                       : 0.f;
     }
   }
+  // SE scale on the weight fragments when the tile is one image (its k-scales are shared by every
+  // row): NT fragments and one table read per k-step instead of MT fragments and MT reads
+  bool one_img = false;
+  if constexpr (XF == IN_SE_SCALE) one_img = img0 == (min(m0 + BM, a.M) - 1) / a.OH;
   int frow_img[MT];
 #pragma unroll
   for (int mi = 0; mi < MT; ++mi) {
@@ -257,8 +266,15 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi) bx[mi] = lrelu_frag(bx[mi], a.in_slope);
     } else if constexpr (XF == IN_SE_SCALE) {
+      if (one_img) {  // the whole tile is one image: scale the NT weight fragments, one table read
+        float sc[8];
+        load_scales(se_tab + st * 32 + g * 8, sc);
 #pragma unroll
-      for (int mi = 0; mi < MT; ++mi) bx[mi] = scale_frag(bx[mi], se_tab + frow_img[mi] * a.cs_in + st * 32 + g * 8);
+        for (int ni = 0; ni < NT; ++ni) af[ni] = scale_with(af[ni], sc);
+      } else {
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi) bx[mi] = scale_frag(bx[mi], se_tab + frow_img[mi] * a.cs_in + st * 32 + g * 8);
+      }
     }
 #pragma unroll
     for (int ni = 0; ni < NT; ++ni)
@@ -362,14 +378,16 @@ void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
 template <int KIND, int XF>
 void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
   const int n = a.cs_out;
-  static const int big = [] {  // M2S_GEMM_BIG=0 keeps the 128x128 tile for the long 1x1 GEMMs
-    const char* e = getenv("M2S_GEMM_BIG");
-    return e ? atoi(e) : 1;
+  static const int big = [] {  // M2S_GEMM_BIG=0 keeps the 128x128 tile for the long 1x1 GEMMs,
+    const char* e = getenv("M2S_GEMM_BIG");  // 1 limits the 128x256 tile to n <= 256 and kp >= 512
+    return e ? atoi(e) : 2;
   }();
-  if constexpr (KIND == KIND_GEMM || KIND == KIND_CONV2D) if (big && a.M >= 256 * 256 && n > 128 && n <= 256 && a.kp >= 512) {
+  if constexpr (KIND == KIND_GEMM || KIND == KIND_CONV2D) if (big && a.M >= 256 * 256 && n > 128 &&
+                                                               ((n <= 256 && a.kp >= 512) || (KIND == KIND_GEMM && big > 1))) {
     // long-K 1x1 GEMMs and 3x3 convs with 129..256 outputs: one 256-wide n tile reads (gathers)
     // the activations once instead of twice (b5 conv_pwl 1248 -> 208: 13.5 -> 10.0 ms per 4 steps;
-    // b2 conv_exp 3x3 56 -> 224: 1.10 -> 0.91 ms per launch).  A 256x128 tile
+    // b2 conv_exp 3x3 56 -> 224: 1.10 -> 0.91 ms per launch); also every wide 1x1 GEMM (the
+    // stride-2 IR expansions K 64 / 128 -> 224 / 736: 526 -> 457 us per launch).  A 256x128 tile
     // for n <= 128 measured slower at every K (one wave per SIMD at 272 registers).
     return launch_tile<128, 256, 4, 8, KIND, XF>(a, s, phases, flops, bytes);
   }
