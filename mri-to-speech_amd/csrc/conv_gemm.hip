@@ -395,7 +395,8 @@ void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, 
     const char* e = getenv("M2S_GEMM_TALL");
     return e ? atoi(e) : 1;
   }();
-  if constexpr (KIND == KIND_GEMM) if (tall && a.M >= 256 * 256 && n > 64 && n <= 128 && a.kp >= 384) {
+  if constexpr (KIND == KIND_GEMM || KIND == KIND_CONV1D)
+    if (tall && a.M >= 256 * 256 && n > 64 && n <= 128 && a.kp >= 384 && (KIND == KIND_GEMM || tall > 1)) {
     // 256 rows x 128 outputs at two waves per SIMD: the weight tile (K x 128) is re-read from L2
     // once per 256 rows instead of per 128 (the SE-scaled conv_pwl of blocks.3/4: K 416..736)
     return launch_tile<256, 128, 8, 4, KIND, XF>(a, s, phases, flops, bytes);
