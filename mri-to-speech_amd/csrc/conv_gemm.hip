@@ -401,6 +401,16 @@ void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, 
     // once per 256 rows instead of per 128 (the SE-scaled conv_pwl of blocks.3/4: K 416..736)
     return launch_tile<256, 128, 8, 4, KIND, XF>(a, s, phases, flops, bytes);
   }
+  static const int smallm = [] {  // M2S_GEMM_SMALLM=0 keeps 128-row tiles for short-M, wide, long-K convs
+    const char* e = getenv("M2S_GEMM_SMALLM");  // (measured 10 % slower: off by default)
+    return e ? atoi(e) : 0;
+  }();
+  if constexpr (KIND == KIND_CONV1D)
+    if (smallm && a.M <= 32768 && n >= 128 && n % 128 == 0 && a.kp >= 512) {
+      // the vocoder's first MRF stage (M = 64 clips x 300, N = 256, K up to 2816): 128-row tiles
+      // give ~300 workgroups for 256 CUs; 64-row tiles double the parallelism
+      return launch_tile<64, 128, 4, 2, KIND, XF>(a, s, phases, flops, bytes);
+    }
   if (n <= 16)
     launch_tile<256, 16, 4, 1, KIND, XF>(a, s, phases, flops, bytes);
   else if (n <= 32)

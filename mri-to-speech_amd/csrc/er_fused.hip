@@ -44,6 +44,15 @@ struct ErArgs {
 __device__ __forceinline__ void dma16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, lds_wave_base, 16, 0, 0);
 }
+// An LDS read the compiler does not see: an ordinary ds_read after an LDS-DMA (the next tile's halo)
+// gets a conservative s_waitcnt vmcnt(0), which would also wait for this tile's stores.
+__device__ __forceinline__ uint2 lds_u2(const void* p) {
+  uint2 r;
+  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(r)
+               : "v"((uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p));
+  return r;
+}
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -98,8 +107,9 @@ __global__ void __launch_bounds__(512, 1) er_fused_kernel(const ErArgs a) {
   for (int it = 0, tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
     char* hb = hbuf + (it & 1) * ER_BUF;
     if (it > 0) {
-      wait_vm<4>();     // this tile's halo landed (the 4 younger ops are the last tile's stores)
-      __syncthreads();  // ... for every wave; and every wave is done with the other buffer
+      wait_vm<4>();  // this tile's halo landed (the 4 younger ops are the last tile's stores)
+      __builtin_amdgcn_s_barrier();  // ... for every wave; every wave is done with the other buffer
+      asm volatile("" ::: "memory");  // (a raw barrier: __syncthreads would also wait for the stores)
     }
     if (tile + (int)gridDim.x < ntiles) issue_halo(tile + gridDim.x, hbuf + ((it + 1) & 1) * ER_BUF);
 
@@ -148,8 +158,7 @@ __global__ void __launch_bounds__(512, 1) er_fused_kernel(const ErArgs a) {
 #pragma unroll
       for (int on = 0; on < 2; ++on) {
         const int c4 = on * 16 + 4 * g;
-        const uint2 r = *reinterpret_cast<const uint2*>(hb + (c4 >> 3) * ER_PLANE + ((ry + 1) * ER_HW + r16 + 1) * 16 +
-                                                        (c4 & 7) * 2);
+        const uint2 r = lds_u2(hb + (c4 >> 3) * ER_PLANE + ((ry + 1) * ER_HW + r16 + 1) * 16 + (c4 & 7) * 2);
         const float v0 = o[on][0] + bp[on].x + __uint_as_float(r.x << 16);
         const float v1 = o[on][1] + bp[on].y + __uint_as_float(r.x & 0xffff0000u);
         const float v2 = o[on][2] + bp[on].z + __uint_as_float(r.y << 16);
