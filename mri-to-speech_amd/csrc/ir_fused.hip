@@ -18,6 +18,8 @@
 //            dwords (no unpacking), SiLU, one v_cvt_pk_bf16_f32 per channel pair, 16-byte stores.
 //   squeeze: per-lane channel sums -> fixed xor-shuffle tree within each wave -> per-wave partials
 //            in LDS -> the image's waves added in order -> SE mean (deterministic).
+#include <type_traits>
+
 #include "conv_igemm.hpp"
 #include "kernels.hpp"
 #include "prof.hpp"
@@ -49,13 +51,16 @@ __device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float acc) {
                                          false);
 }
 
-template <int MT, int G>
-__global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : 2)) ir_pwdw_kernel(const bf16_t* __restrict__ x, int cs_in, int kp,
+// S = depthwise stride.  OH x OW is the conv_pw (input) map; with S = 2 the depthwise writes the
+// SOH x SOW map, TF-SAME with top / left pads pad_t / pad_l (the stride-2 blocks.5.0 at 16x16).
+template <int MT, int G, int S>
+__device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int cs_in, int kp,
                                                          const bf16_t* __restrict__ wpw, const float* __restrict__ bpw,
                                                          const uint32_t* __restrict__ wdw2,
                                                          const float* __restrict__ bdw, int N, int OH, int OW,
                                                          int cs_mid, bf16_t* __restrict__ y,
-                                                         bf16_t* __restrict__ se_mean) {
+                                                         bf16_t* __restrict__ se_mean, int SOH, int SOW, int pad_t,
+                                                         int pad_l) {
   __shared__ __attribute__((aligned(16))) bf16_t tile[ROWS_MAX * MROW];
   __shared__ uint16_t lut[POS_MAX];
   __shared__ float red[4][SL];
@@ -64,6 +69,7 @@ __global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : 2)) ir_pwdw_kernel(co
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g16 = lane >> 4, r16 = lane & 15;
   const int P = OH * OW, WR = OW + 2, IR = (OH + 2) * WR;
+  const int PO = S == 1 ? P : SOH * SOW;  // depthwise output pixels per image
   // XCD-aware: the workgroups of one image group (its slices) are consecutive in `wid` and share
   // blockIdx % 8, i.e. one XCD, so the image is fetched into one L2 instead of eight.
   const int nsl = (cs_mid + SL - 1) / SL;
@@ -129,7 +135,35 @@ __global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : 2)) ir_pwdw_kernel(co
                                                                 __builtin_bit_cast(bf16x8, fb[buf][mi]), acc[ni][mi],
                                                                 0, 0, 0);
     };
-    if (!(IRF_MODE & 1)) {  // IRF_MODE: microbenchmark variants (tools/irf_bench.hip); 0 in the library
+    // the K loop fully unrolled for the block widths of the backbone (kp = cs_in = 128 / 224): loads
+    // from clamped addresses (no exec-masked branch; positions past MP feed only discarded output
+    // columns), and sched_barriers pin the one-step prefetch ahead of the MFMAs it must overlap.  The
+    // generic loop below made every k-step wait for its own loads (conditional loads end in vmcnt(0)).
+    auto load_u = [&](int buf, int k0) {
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni)
+        fa[buf][ni] = *reinterpret_cast<const uint4*>(wpw + (size_t)(c0 + ni * 16 + r16) * kp + k0 + 8 * g16);
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+        fb[buf][mi] = *reinterpret_cast<const uint4*>(xi + (size_t)min(mw + mi * 16 + r16, MP - 1) * cs_in + k0 + 8 * g16);
+    };
+    auto unrolled = [&](auto ksn_c) {
+      constexpr int KSN = decltype(ksn_c)::value;
+      load_u(0, 0);
+#pragma unroll
+      for (int ks = 0; ks < KSN; ++ks) {
+        if (ks + 1 < KSN) load_u((ks + 1) & 1, (ks + 1) * 32);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(ks & 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    if (IRF_MODE & 1) {  // IRF_MODE: microbenchmark variants (tools/irf_bench.hip); 0 in the library
+    } else if (kp == 128 && cs_in == 128) {
+      unrolled(std::integral_constant<int, 4>());
+    } else if (kp == 224 && cs_in == 224) {
+      unrolled(std::integral_constant<int, 7>());
+    } else {
     load(0, 0);
     for (int k0 = 0;;) {
       if (k0 + 32 < kp) load(1, k0 + 32);
@@ -174,9 +208,16 @@ __global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : 2)) ir_pwdw_kernel(co
         b[0] = lo.x; b[1] = lo.y; b[2] = lo.z; b[3] = lo.w;
         b[4] = hi.x; b[5] = hi.y; b[6] = hi.z; b[7] = hi.w;
       }
-      bf16_t* yi = y + (size_t)(n0 + g) * P * cs_mid + c;
-      for (int p = q; p < P; p += lpi) {
-        const bf16_t* base = tile + lut[g * P + p] * MROW + cg * 8;
+      bf16_t* yi = y + (size_t)(n0 + g) * PO * cs_mid + c;
+      for (int p = q; p < PO; p += lpi) {
+        int trow;  // haloed tile row of the tap-(1, 1) input pixel
+        if constexpr (S == 1) {
+          trow = lut[g * P + p];
+        } else {
+          const int oy = p / SOW, ox = p - (p / SOW) * SOW;
+          trow = g * IR + (S * oy - pad_t + 2) * WR + S * ox - pad_l + 2;
+        }
+        const bf16_t* base = tile + trow * MROW + cg * 8;
         uint4 in[9];
 #pragma unroll
         for (int t = 0; t < 9; ++t)
@@ -225,10 +266,26 @@ __global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : 2)) ir_pwdw_kernel(co
       if (gg < gi && c0 + cl < cs_mid) {
         float t = 0.f;
         for (int wv = gg * wpi; wv < (gg + 1) * wpi; ++wv) t += red[wv][cl];
-        se_mean[(size_t)(n0 + gg) * cs_mid + c0 + cl] = f2bf(t / (float)P);
+        se_mean[(size_t)(n0 + gg) * cs_mid + c0 + cl] = f2bf(t / (float)PO);
       }
     }
   }
+}
+
+template <int MT, int G>
+__global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : 2))
+    ir_pwdw_kernel(const bf16_t* __restrict__ x, int cs_in, int kp, const bf16_t* __restrict__ wpw,
+                   const float* __restrict__ bpw, const uint32_t* __restrict__ wdw2, const float* __restrict__ bdw, int N,
+                   int OH, int OW, int cs_mid, bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean) {
+  ir_pwdw_body<MT, G, 1>(x, cs_in, kp, wpw, bpw, wdw2, bdw, N, OH, OW, cs_mid, y, se_mean, OH, OW, 1, 1);
+}
+
+__global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : 2))
+    ir_pwdw_s2_kernel(const bf16_t* __restrict__ x, int cs_in, int kp, const bf16_t* __restrict__ wpw,
+                      const float* __restrict__ bpw, const uint32_t* __restrict__ wdw2, const float* __restrict__ bdw,
+                      int N, int IH, int IW, int cs_mid, bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, int OH,
+                      int OW, int pad_t, int pad_l) {
+  ir_pwdw_body<4, 1, 2>(x, cs_in, kp, wpw, bpw, wdw2, bdw, N, IH, IW, cs_mid, y, se_mean, OH, OW, pad_t, pad_l);
 }
 
 int ir_group(int OH, int OW) {
@@ -267,6 +324,24 @@ void launch_ir_pwdw(const bf16_t* x, int N, int cs_in, int kp, const bf16_t* wpw
   M2S_IRF(4, 1) M2S_IRF(4, 2) M2S_IRF(4, 4)
 #undef M2S_IRF
   M2S_CHECK(false, "ir_pwdw: no variant for this shape");
+}
+
+bool ir_fused_s2_supported(int IH, int IW, int cs_in, int cs_mid) {
+  return IH * IW <= 256 && IH * IW > 192 && (IH + 2) * (IW + 2) <= ROWS_MAX && cs_mid % 8 == 0 && cs_in > 0;
+}
+
+void launch_ir_pwdw_s2(const bf16_t* x, int N, int cs_in, int kp, const bf16_t* wpw, const float* bpw,
+                       const uint32_t* wdw2, const float* bdw, int IH, int IW, int OH, int OW, int pad_t, int pad_l,
+                       int cs_mid, bf16_t* y, bf16_t* se_mean, double flops, double bytes, hipStream_t s) {
+  M2S_CHECK(ir_fused_s2_supported(IH, IW, cs_in, cs_mid) && kp % 32 == 0 && kp >= cs_in, "ir_pwdw_s2: unsupported shape");
+  M2S_CHECK(OH == (IH + 1) / 2 && OW == (IW + 1) / 2 && OH * OW <= 64 && pad_t >= 0 && pad_t <= 1 && pad_l >= 0 &&
+                pad_l <= 1,
+            "ir_pwdw_s2: geometry");
+  const dim3 grid(ceil_div(cs_mid, SL) * N);
+  ProfScope ps("ir_pwdw_s2_kernel", flops, bytes, s);
+  hipLaunchKernelGGL(ir_pwdw_s2_kernel, grid, dim3(256), 0, s, x, cs_in, kp, wpw, bpw, wdw2, bdw, N, IH, IW, cs_mid, y,
+                     se_mean, OH, OW, pad_t, pad_l);
+  M2S_HIP(hipGetLastError());
 }
 
 }  // namespace m2s

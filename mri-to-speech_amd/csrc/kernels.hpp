@@ -33,6 +33,13 @@ void launch_ir_pwdw(const bf16_t* x, int N, int cs_in, int kp, const bf16_t* wpw
                     const uint32_t* wdw2, const float* bdw, int OH, int OW, int cs_mid, bf16_t* y, bf16_t* se_mean,
                     double flops, double bytes, hipStream_t s);
 
+// The same for a stride-2 depthwise (TF-SAME, top / left pads pad_t / pad_l) on an IH x IW <= 256-pixel
+// conv_pw map: y (N, OH*OW, cs_mid), se_mean over the OH x OW output.  (ir_fused.hip)
+bool ir_fused_s2_supported(int IH, int IW, int cs_in, int cs_mid);
+void launch_ir_pwdw_s2(const bf16_t* x, int N, int cs_in, int kp, const bf16_t* wpw, const float* bpw,
+                       const uint32_t* wdw2, const float* bdw, int IH, int IW, int OH, int OW, int pad_t, int pad_l,
+                       int cs_mid, bf16_t* y, bf16_t* se_mean, double flops, double bytes, hipStream_t s);
+
 // bf16 fused HiFi-GAN ResBlock1 (all (c1, c2) pairs of one resblock + the MRF running sum) for C in
 // {32, 64}: x (B, L, C) -> S (B, L, C) with S = x' (accum 0), S += x' (1), S = (S + x') / div (2).
 // (mrf_fused.hip)

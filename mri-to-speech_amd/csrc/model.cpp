@@ -657,6 +657,14 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                          static_cast<const uint32_t*>(arena_.ptr(b.dw_w2)), static_cast<const float*>(arena_.ptr(b.dw_b)),
                          nh, nw, cs, reinterpret_cast<bf16_t*>(M2), reinterpret_cast<bf16_t*>(se_mean),
                          2.0 * nc * P * b.mid * (b.c1.cin + 9), 2.0 * nc * P * (b.c1.cs_in + cs), s);
+        } else if (std::is_same<T, bf16_t>::value && b.stride == 2 && ir_fused_ &&
+                   ir_fused_s2_supported(oh, ow, b.c1.cs_in, cs) && nh * nw <= 64) {
+          const double Pi = (double)oh * ow, Po = (double)nh * nw;
+          launch_ir_pwdw_s2(reinterpret_cast<const bf16_t*>(cur), nc, b.c1.cs_in, b.c1.kp,
+                            static_cast<const bf16_t*>(b.c1.w), b.c1.b,
+                            static_cast<const uint32_t*>(arena_.ptr(b.dw_w2)), static_cast<const float*>(arena_.ptr(b.dw_b)),
+                            oh, ow, nh, nw, qt, ql, cs, reinterpret_cast<bf16_t*>(M2), reinterpret_cast<bf16_t*>(se_mean),
+                            2.0 * nc * b.mid * (Pi * b.c1.cin + Po * 9), 2.0 * nc * (Pi * b.c1.cs_in + Po * cs), s);
         } else {
         ConvArgs e = conv_args(b.c1);
         e.x = cur;

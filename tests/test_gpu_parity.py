@@ -203,7 +203,7 @@ def test_effnet_bf16_ir_fused_every_block(rt, ac_state, monkeypatch, hw):
     assert _cos(ga, gb) >= 0.99999
 
 
-@pytest.mark.parametrize("env,blocks", [("M2S_STEM_FUSED", (2, 3, 6, -1)), ("M2S_SE_FUSED", (9, 14, 20, -1)),
+@pytest.mark.parametrize("env,blocks", [("M2S_STEM_FUSED", (2, 3, 6, -1)), ("M2S_SE_FUSED", (9, 14, 20, -1)), ("M2S_IR_FUSED", (9, 10, 18, 19, -1)),
                                         ("M2S_ER_FUSED", (3, 4, 5, 6, 7, 8, -1)), ("M2S_IR_BLOCK", (10, 12, 13, 18, -1))])
 @pytest.mark.parametrize("hw", [(256, 256), (96, 80), (67, 101)])
 def test_effnet_bf16_fused_kernels_vs_unfused(rt, ac_state, monkeypatch, hw, env, blocks):
