@@ -30,6 +30,9 @@ namespace {
 #ifndef IRF_SL
 #define IRF_SL 32
 #endif
+#ifndef IRF_OCC
+#define IRF_OCC 2  // workgroups per CU for IRF_SL != 32 (microbenchmark builds)
+#endif
 constexpr int SL = IRF_SL;         // expanded channels per slice
 #ifndef IRF_MROW
 #define IRF_MROW (SL + 8)
@@ -273,14 +276,14 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
 }
 
 template <int MT, int G>
-__global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : 2))
+__global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : IRF_OCC))
     ir_pwdw_kernel(const bf16_t* __restrict__ x, int cs_in, int kp, const bf16_t* __restrict__ wpw,
                    const float* __restrict__ bpw, const uint32_t* __restrict__ wdw2, const float* __restrict__ bdw, int N,
                    int OH, int OW, int cs_mid, bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean) {
   ir_pwdw_body<MT, G, 1>(x, cs_in, kp, wpw, bpw, wdw2, bdw, N, OH, OW, cs_mid, y, se_mean, OH, OW, 1, 1);
 }
 
-__global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : 2))
+__global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : IRF_OCC))
     ir_pwdw_s2_kernel(const bf16_t* __restrict__ x, int cs_in, int kp, const bf16_t* __restrict__ wpw,
                       const float* __restrict__ bpw, const uint32_t* __restrict__ wdw2, const float* __restrict__ bdw,
                       int N, int IH, int IW, int cs_mid, bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, int OH,
