@@ -179,7 +179,7 @@ def _cos(a, b):
     return float((a * b).sum() / np.sqrt((a ** 2).sum() * (b ** 2).sum()))
 
 
-@pytest.mark.parametrize("hw", [(256, 256), (96, 80), (67, 101)])
+@pytest.mark.parametrize("hw", [(256, 256), (256, 128), (96, 80), (67, 101)])
 def test_effnet_bf16_ir_fused_every_block(rt, ac_state, monkeypatch, hw):
     """The fused conv_pw+conv_dw+SE-squeeze kernel (ir_fused.hip) against the unfused bf16
     sequence and the fp32 oracle, block by block (both bf16 paths round the expanded activation
