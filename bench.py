@@ -34,7 +34,7 @@ from m2s.config import HIFIGAN_H  # noqa: E402
 
 HOP = 420
 SR = 11413
-PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA peaks, MI355X_MICROARCH.md
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "bf16x3": 2500.0 / 3}  # dense MFMA peaks, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
 
 
@@ -65,7 +65,7 @@ def parse():
     p.add_argument("--clips", type=int, default=64, help="clips per GPU")
     p.add_argument("--frames", type=int, default=30, help="frames per clip")
     p.add_argument("--hw", type=int, default=256)
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "bf16x3"])
     p.add_argument("--chunk", type=int, default=1920, help="frames per CNN pass (1920 = one pass over the 64x30 step)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -201,7 +201,7 @@ def main():
         tot_ms = sum(s["ms"] for s in stats)
         dom = max(stats, key=lambda s: s["ms"])
         # bound = the roof its algorithmic intensity hits first (ridge = peak FLOP/s / HBM B/s)
-        peak_tf = PEAK_TFLOPS["fp32" if args.dtype == "fp32" or "float" in dom["name"] else "bf16"]
+        peak_tf = PEAK_TFLOPS["fp32" if args.dtype == "fp32" or "float" in dom["name"] else args.dtype]
         ridge = peak_tf * 1e12 / (PEAK_HBM_GBS * 1e9)
         if dom["bytes"] <= 0 or dom["flops"] / dom["bytes"] > ridge:
             achieved = dom["flops"] / (dom["ms"] * 1e-3) / 1e12

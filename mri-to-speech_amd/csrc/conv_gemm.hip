@@ -71,6 +71,40 @@ __device__ __forceinline__ bf16x8 scale_frag(bf16x8 v, const float* s) {
   return scale_with(v, sc);
 }
 
+// Split-fp32 fragments (SP = 1): hi/lo pairs of 8 values.  An input transform computes in fp32 on
+// hi + lo and re-splits the result, so the transformed operand keeps 17 significant bits.
+__device__ __forceinline__ void resplit_frag(const float* v, bf16x8& h, bf16x8& l) {
+  uint2 h0, h1, l0, l1;
+  split4(v, h0, l0);
+  split4(v + 4, h1, l1);
+  h = __builtin_bit_cast(bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+  l = __builtin_bit_cast(bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+}
+__device__ __forceinline__ void frag_sum(bf16x8 h, bf16x8 l, float* v) {
+  const uint4 a = __builtin_bit_cast(uint4, h), b = __builtin_bit_cast(uint4, l);
+  unpack_bf16x4(make_uint2(a.x, a.y), v);
+  unpack_bf16x4(make_uint2(a.z, a.w), v + 4);
+  float w[8];
+  unpack_bf16x4(make_uint2(b.x, b.y), w);
+  unpack_bf16x4(make_uint2(b.z, b.w), w + 4);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] += w[j];
+}
+__device__ __forceinline__ void lrelu_split(bf16x8& h, bf16x8& l, float slope) {
+  float v[8];
+  frag_sum(h, l, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * slope;
+  resplit_frag(v, h, l);
+}
+__device__ __forceinline__ void scale_split(bf16x8& h, bf16x8& l, const float* sc) {
+  float v[8];
+  frag_sum(h, l, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] *= sc[j];
+  resplit_frag(v, h, l);
+}
+
 __device__ __forceinline__ void ld4f(const bf16_t* p, float* v) {
   const uint2 u = *reinterpret_cast<const uint2*>(p);
   v[0] = __uint_as_float(u.x << 16);
@@ -83,16 +117,20 @@ constexpr int ROW = 64;  // bytes per LDS row = 32 bf16 = one k-step
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * ROW + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
-template <int BM, int BN, int MT, int NT, int S, int KIND, int XF>
+// SP = 1: split-fp32 operands (m2s_common.hpp sp_t): every activation and weight row is [hi | lo],
+// each K step DMAs both halves into two planes of the slot and runs the three MFMA terms
+// hi*hi + hi*lo + lo*hi (the dropped lo*lo term is below 2^-16 of the product).
+template <int BM, int BN, int MT, int NT, int S, int KIND, int XF, int SP>
 __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 2 : 1)) conv_gemm_kernel(const ConvArgs a, int n_tiles, int se_imgs) {
   constexpr int WN = BN / (NT * 16);
   constexpr int WM = 4 / WN;
   static_assert(WM * WN == 4 && WM * MT * 16 == BM, "bad tile");
+  constexpr int R = SP ? 2 : 1;                    // planes per operand row
   constexpr int A_PER_WAVE = BM / 64;              // 16-row DMA blocks per wave for A
   constexpr int B_BLOCKS = BN / 16;                // 16-row DMA blocks for B
   constexpr int B_PER_WAVE = (B_BLOCKS + 3) / 4;   // waves >= B_BLOCKS issue into a scratch block
-  constexpr int SLOT = (BM + BN + 16) * ROW;       // +16 rows: scratch for surplus B DMAs
-  constexpr int PER_STAGE = A_PER_WAVE + B_PER_WAVE;
+  constexpr int SLOT = (R * (BM + BN) + 16) * ROW; // +16 rows: scratch for surplus B DMAs
+  constexpr int PER_STAGE = R * (A_PER_WAVE + B_PER_WAVE);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* se_tab = reinterpret_cast<float*>(smem + S * SLOT);
 
@@ -110,7 +148,8 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
   const int phase = blockIdx.z;
 
   const bf16_t* __restrict__ X = static_cast<const bf16_t*>(a.x);
-  const bf16_t* __restrict__ W = static_cast<const bf16_t*>(a.w) + (size_t)phase * a.n_pad * a.kp;
+  const bf16_t* __restrict__ W = static_cast<const bf16_t*>(a.w) + (size_t)phase * a.n_pad * a.kp * R;
+  const int xs = a.cs_in * R;  // elements per input position
   const int nsteps = a.kp / 32;
 
   // ---- DMA roles: lane -> (row within a 16-row block, physical chunk) -------------------------
@@ -135,7 +174,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
       const int img = mm / hw, rem = mm - (mm / hw) * hw;
       const int oy = rem / a.OW, ox = rem - (rem / a.OW) * a.OW;
       const int iy0 = oy * a.stride - a.pad_t, ix0 = ox * a.stride - a.pad_l;
-      rbase[j] = ((img * a.IH + iy0) * a.IW + ix0) * a.cs_in;
+      rbase[j] = ((img * a.IH + iy0) * a.IW + ix0) * xs;
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int iy = iy0 + t / 3, ix = ix0 + t % 3;
@@ -143,31 +182,31 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
       }
     } else if constexpr (KIND == KIND_CONV1D) {
       const int b = mm / a.L_out, t0 = mm - b * a.L_out - a.pad_left;
-      rbase[j] = (b * a.L_in + t0) * a.cs_in;
+      rbase[j] = (b * a.L_in + t0) * xs;
       for (int t = 0; t < a.ntaps; ++t) {
         const int it = t0 + t * a.dil;
         msk |= (uint32_t)(it >= 0 && it < a.L_in) << t;
       }
     } else if constexpr (KIND == KIND_CONVT) {
       const int b = mm / a.L_in, t0 = mm - b * a.L_in + delta;
-      rbase[j] = (b * a.L_in + t0) * a.cs_in;
+      rbase[j] = (b * a.L_in + t0) * xs;
       for (int t = 0; t < a.ntaps; ++t) {
         const int it = t0 - t;
         msk |= (uint32_t)(it >= 0 && it < a.L_in) << t;
       }
     } else {
-      rbase[j] = mm * a.cs_in;
+      rbase[j] = mm * xs;
       msk = 1u;
     }
     rmask[j] = ok ? msk : 0u;
   }
   // this lane's tap and channel within the current K step, and the tap's input offset
   int s_tap = (q * 8) / a.cs_in, s_c = (q * 8) % a.cs_in;
-  const int row_stride = a.IW * a.cs_in;  // CONV2D: one input row
+  const int row_stride = a.IW * xs;  // CONV2D: one input row
   auto tap_off = [&](int t) -> int {
-    if constexpr (KIND == KIND_CONV2D) return (t / 3) * row_stride + (t - (t / 3) * 3) * a.cs_in;
-    else if constexpr (KIND == KIND_CONV1D) return t * a.dil * a.cs_in;
-    else if constexpr (KIND == KIND_CONVT) return -t * a.cs_in;
+    if constexpr (KIND == KIND_CONV2D) return (t / 3) * row_stride + (t - (t / 3) * 3) * xs;
+    else if constexpr (KIND == KIND_CONV1D) return t * a.dil * xs;
+    else if constexpr (KIND == KIND_CONVT) return -t * xs;
     else return 0;
   };
   int s_off = tap_off(s_tap) + s_c;
@@ -178,23 +217,29 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
   for (int j = 0; j < B_PER_WAVE; ++j) {
     const int blk = wave * B_PER_WAVE + j;
     const int n = n0 + blk * 16 + lrow;
-    bsrc[j] = (blk < B_BLOCKS && n < a.n_pad) ? W + (size_t)n * a.kp + q * 8 : nullptr;
+    bsrc[j] = (blk < B_BLOCKS && n < a.n_pad) ? W + (size_t)n * a.kp * R + q * 8 : nullptr;
   }
 
   auto issue = [&](int st, int slot) {
     char* As = smem + slot * SLOT;
-    char* Bs = As + BM * ROW;
+    char* Bs = As + R * BM * ROW;
 #pragma unroll
     for (int j = 0; j < A_PER_WAVE; ++j) {
       const bool v = s_tap < 32 && ((rmask[j] >> s_tap) & 1u);
-      const void* src = v ? static_cast<const void*>(X + (unsigned)(rbase[j] + s_off)) : static_cast<const void*>(zp);
-      dma16(src, As + (wave * A_PER_WAVE + j) * 16 * ROW);
+      const bf16_t* src = X + (unsigned)(rbase[j] + s_off);
+      dma16(v ? static_cast<const void*>(src) : static_cast<const void*>(zp), As + (wave * A_PER_WAVE + j) * 16 * ROW);
+      if constexpr (SP)
+        dma16(v ? static_cast<const void*>(src + a.cs_in) : static_cast<const void*>(zp),
+              As + (BM + (wave * A_PER_WAVE + j) * 16) * ROW);
     }
 #pragma unroll
     for (int j = 0; j < B_PER_WAVE; ++j) {
       const int blk = wave * B_PER_WAVE + j;
       const void* src = bsrc[j] ? (const void*)(bsrc[j] + st * 32) : (const void*)zp;
-      dma16(src, blk < B_BLOCKS ? Bs + blk * 16 * ROW : As + (BM + BN) * ROW);
+      dma16(src, blk < B_BLOCKS ? Bs + blk * 16 * ROW : As + R * (BM + BN) * ROW);
+      if constexpr (SP)
+        dma16(bsrc[j] ? (const void*)(bsrc[j] + st * 32 + a.kp) : (const void*)zp,
+              blk < B_BLOCKS ? Bs + (BN + blk * 16) * ROW : As + R * (BM + BN) * ROW);
     }
     // advance one K step (32 channels): cs_in >= 32 is a multiple of 32, smaller cs_in divide 32
     if (a.cs_in >= 32) {
@@ -215,9 +260,8 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
     img0 = m0 / a.OH;
     for (int i = tid; i < se_imgs * a.cs_in; i += 256) {
       const int im = i / a.cs_in, c = i - (i / a.cs_in) * a.cs_in;
-      se_tab[i] = (img0 + im) * a.OH < a.M
-                      ? bf2f(static_cast<const bf16_t*>(a.in_scale)[(size_t)(img0 + im) * a.cs_in + c])
-                      : 0.f;
+      const bf16_t* g = static_cast<const bf16_t*>(a.in_scale) + (size_t)(img0 + im) * xs + c;
+      se_tab[i] = (img0 + im) * a.OH < a.M ? (SP ? bf2f(g[0]) + bf2f(g[a.cs_in]) : bf2f(g[0])) : 0.f;
     }
   }
   // SE scale on the weight fragments when the tile is one image (its k-scales are shared by every
@@ -254,7 +298,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
     if (st + S - 1 < nsteps) issue(st + S - 1, (st + S - 1) % S);
 
     const char* As = smem + (st % S) * SLOT;
-    const char* Bs = As + BM * ROW;
+    const char* Bs = As + R * BM * ROW;
     bf16x8 af[NT], bx[MT];
 #pragma unroll
     for (int ni = 0; ni < NT; ++ni)
@@ -262,6 +306,42 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi)
       bx[mi] = *reinterpret_cast<const bf16x8*>(As + swz(wm * MT * 16 + mi * 16 + r16, g));
+    if constexpr (SP) {
+      bf16x8 afl[NT], bxl[MT];
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni)
+        afl[ni] = *reinterpret_cast<const bf16x8*>(Bs + BN * ROW + swz(wn * NT * 16 + ni * 16 + r16, g));
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+        bxl[mi] = *reinterpret_cast<const bf16x8*>(As + BM * ROW + swz(wm * MT * 16 + mi * 16 + r16, g));
+      if constexpr (XF == IN_LRELU) {
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi) lrelu_split(bx[mi], bxl[mi], a.in_slope);
+      } else if constexpr (XF == IN_SE_SCALE) {
+        if (one_img) {
+          float sc[8];
+          load_scales(se_tab + st * 32 + g * 8, sc);
+#pragma unroll
+          for (int ni = 0; ni < NT; ++ni) scale_split(af[ni], afl[ni], sc);
+        } else {
+#pragma unroll
+          for (int mi = 0; mi < MT; ++mi) {
+            float sc[8];
+            load_scales(se_tab + frow_img[mi] * a.cs_in + st * 32 + g * 8, sc);
+            scale_split(bx[mi], bxl[mi], sc);
+          }
+        }
+      }
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi) {
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl[ni], bx[mi], acc[ni][mi], 0, 0, 0);
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ni], bxl[mi], acc[ni][mi], 0, 0, 0);
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ni], bx[mi], acc[ni][mi], 0, 0, 0);
+        }
+      continue;
+    }
     if constexpr (XF == IN_LRELU) {
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi) bx[mi] = lrelu_frag(bx[mi], a.in_slope);
@@ -285,18 +365,19 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
 
   // ---- epilogue: 4 consecutive channels of one position per lane ------------------------------
   bf16_t* __restrict__ Y = static_cast<bf16_t*>(a.y);
-  const bf16_t* __restrict__ R = static_cast<const bf16_t*>(a.res);
+  const bf16_t* __restrict__ Rs = static_cast<const bf16_t*>(a.res);
 #pragma unroll
   for (int mi = 0; mi < MT; ++mi) {
     const int m = m0 + wm * MT * 16 + mi * 16 + r16;
     if (m >= a.M) continue;
-    long orow;
+    long orow;  // output position
     if constexpr (KIND == KIND_CONVT) {
       const int b = m / a.L_in, qq = m - (m / a.L_in) * a.L_in;
-      orow = ((long)b * a.L_out + (long)qq * a.ct_u + phase) * a.cs_out;
+      orow = (long)b * a.L_out + (long)qq * a.ct_u + phase;
     } else {
-      orow = (long)m * a.cs_out;
+      orow = m;
     }
+    orow *= (long)a.cs_out * R;
 #pragma unroll
     for (int ni = 0; ni < NT; ++ni) {
       const int n4 = n0 + wn * NT * 16 + ni * 16 + 4 * g;
@@ -313,15 +394,27 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = sigmoidf_(v[j]);
       }
-      if (R) {
+      if (Rs) {
         float r[4];
-        ld4f(R + orow + n4, r);
+        ld4f(Rs + orow + n4, r);
+        if constexpr (SP) {
+          float rl[4];
+          ld4f(Rs + orow + a.cs_out + n4, rl);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r[j] += rl[j];
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] += r[j];
       }
       if (a.accum) {
         float p[4];
         ld4f(Y + orow + n4, p);
+        if constexpr (SP) {
+          float pl[4];
+          ld4f(Y + orow + a.cs_out + n4, pl);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) p[j] += pl[j];
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = p[j] + v[j];
         if (a.accum == 2) {
@@ -329,10 +422,17 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
           for (int j = 0; j < 4; ++j) v[j] = v[j] / a.accum_div;
         }
       }
-      uint2 u;
-      u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      *reinterpret_cast<uint2*>(Y + orow + n4) = u;
+      if constexpr (SP) {
+        uint2 hi, lo;
+        split4(v, hi, lo);
+        *reinterpret_cast<uint2*>(Y + orow + n4) = hi;
+        *reinterpret_cast<uint2*>(Y + orow + a.cs_out + n4) = lo;
+      } else {
+        uint2 u;
+        u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(Y + orow + n4) = u;
+      }
     }
   }
 }
@@ -346,12 +446,14 @@ const char* kname(int k) {
   }
 }
 
-template <int BM, int BN, int MT, int NT, int KIND, int XF>
+template <int BM, int BN, int MT, int NT, int KIND, int XF, int SP>
 void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
-  // keep two workgroups' LDS per CU (128 x 256: the SE gate table too, and 256 registers a wave)
-  constexpr int S = (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
+  // keep two workgroups' LDS per CU (128 x 256: the SE gate table too, and 256 registers a wave);
+  // split operands double the slot, so they run two stages
+  constexpr int S = SP ? 2 : (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
+  constexpr int R = SP ? 2 : 1;
   static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF>),
+    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF, SP>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     return true;
   }();
@@ -362,22 +464,31 @@ void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
     M2S_CHECK(KIND == KIND_GEMM && a.OH > 0, "SE scale needs the GEMM kind with OH = rows per image");
     se_imgs = (BM + a.OH - 1) / a.OH + 1;
   }
-  const size_t lds = (size_t)S * (BM + BN + 16) * ROW + (size_t)se_imgs * a.cs_in * sizeof(float);
+  const size_t lds = (size_t)S * (R * (BM + BN) + 16) * ROW + (size_t)se_imgs * a.cs_in * sizeof(float);
   M2S_CHECK(lds <= 160 * 1024, "conv_gemm: LDS budget");
   dim3 grid(m_tiles * n_tiles, 1, phases);
   char name[96];
   static const bool detail = getenv("M2S_PROF_DETAIL") != nullptr;
   if (detail)  // per-layer records for analysis: K x N and rows per launch
-    snprintf(name, sizeof(name), "conv_gemm<%s,%dx%d> K%d N%d M%d", kname(KIND), BM, BN, a.kp, a.cs_out, a.M);
+    snprintf(name, sizeof(name), "conv_gemm<%s,%dx%d%s> K%d N%d M%d", kname(KIND), BM, BN, SP ? ",x3" : "", a.kp, a.cs_out, a.M);
   else
-    snprintf(name, sizeof(name), "conv_gemm_kernel<%d, %d, %d, %d, %d, %d, %d>", BM, BN, MT, NT, S, KIND, XF);
+    snprintf(name, sizeof(name), "conv_gemm_kernel<%d, %d, %d, %d, %d, %d, %d, %d>", BM, BN, MT, NT, S, KIND, XF, SP);
   ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF>), grid, dim3(256), lds, s, a, n_tiles, se_imgs);
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF, SP>), grid, dim3(256), lds, s, a, n_tiles, se_imgs);
 }
 
-template <int KIND, int XF>
+template <int KIND, int XF, int SP>
 void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
   const int n = a.cs_out;
+  if constexpr (SP) {  // split operands: 16/32/64-wide tiles for narrow outputs, else 128 x 128
+    if (n <= 16)
+      return launch_tile<256, 16, 4, 1, KIND, XF, 1>(a, s, phases, flops, bytes);
+    if (n <= 32)
+      return launch_tile<256, 32, 4, 2, KIND, XF, 1>(a, s, phases, flops, bytes);
+    if (n <= 64 || (n % 128 != 0 && ceil_div(n, 64) * 64 < ceil_div(n, 128) * 128))
+      return launch_tile<256, 64, 4, 4, KIND, XF, 1>(a, s, phases, flops, bytes);
+    return launch_tile<128, 128, 4, 4, KIND, XF, 1>(a, s, phases, flops, bytes);
+  } else {
   static const int big = [] {  // M2S_GEMM_BIG=0 keeps the 128x128 tile for the long 1x1 GEMMs,
     const char* e = getenv("M2S_GEMM_BIG");  // 1 limits the 128x256 tile to n <= 256 and kp >= 512
     return e ? atoi(e) : 2;
@@ -389,7 +500,7 @@ void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, 
     // b2 conv_exp 3x3 56 -> 224: 1.10 -> 0.91 ms per launch); also every wide 1x1 GEMM (the
     // stride-2 IR expansions K 64 / 128 -> 224 / 736: 526 -> 457 us per launch).  A 256x128 tile
     // for n <= 128 measured slower at every K (one wave per SIMD at 272 registers).
-    return launch_tile<128, 256, 4, 8, KIND, XF>(a, s, phases, flops, bytes);
+    return launch_tile<128, 256, 4, 8, KIND, XF, 0>(a, s, phases, flops, bytes);
   }
   static const int tall = [] {  // M2S_GEMM_TALL=0 keeps the 128x128 tile for long-K GEMMs with n <= 128
     const char* e = getenv("M2S_GEMM_TALL");
@@ -399,7 +510,7 @@ void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, 
     if (tall && a.M >= 256 * 256 && n > 64 && n <= 128 && a.kp >= 384 && (KIND == KIND_GEMM || tall > 1)) {
     // 256 rows x 128 outputs at two waves per SIMD: the weight tile (K x 128) is re-read from L2
     // once per 256 rows instead of per 128 (the SE-scaled conv_pwl of blocks.3/4: K 416..736)
-    return launch_tile<256, 128, 8, 4, KIND, XF>(a, s, phases, flops, bytes);
+    return launch_tile<256, 128, 8, 4, KIND, XF, 0>(a, s, phases, flops, bytes);
   }
   static const int smallm = [] {  // M2S_GEMM_SMALLM=0 keeps 128-row tiles for short-M, wide, long-K convs
     const char* e = getenv("M2S_GEMM_SMALLM");  // (measured 10 % slower: off by default)
@@ -409,29 +520,30 @@ void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, 
     if (smallm && a.M <= 32768 && n >= 128 && n % 128 == 0 && a.kp >= 512) {
       // the vocoder's first MRF stage (M = 64 clips x 300, N = 256, K up to 2816): 128-row tiles
       // give ~300 workgroups for 256 CUs; 64-row tiles double the parallelism
-      return launch_tile<64, 128, 4, 2, KIND, XF>(a, s, phases, flops, bytes);
+      return launch_tile<64, 128, 4, 2, KIND, XF, 0>(a, s, phases, flops, bytes);
     }
   if (n <= 16)
-    launch_tile<256, 16, 4, 1, KIND, XF>(a, s, phases, flops, bytes);
+    launch_tile<256, 16, 4, 1, KIND, XF, 0>(a, s, phases, flops, bytes);
   else if (n <= 32)
-    launch_tile<256, 32, 4, 2, KIND, XF>(a, s, phases, flops, bytes);
+    launch_tile<256, 32, 4, 2, KIND, XF, 0>(a, s, phases, flops, bytes);
   else if (n <= 64 || (n % 128 != 0 && ceil_div(n, 64) * 64 < ceil_div(n, 128) * 128))
-    launch_tile<256, 64, 4, 4, KIND, XF>(a, s, phases, flops, bytes);
+    launch_tile<256, 64, 4, 4, KIND, XF, 0>(a, s, phases, flops, bytes);
   else
-    launch_tile<128, 128, 4, 4, KIND, XF>(a, s, phases, flops, bytes);
+    launch_tile<128, 128, 4, 4, KIND, XF, 0>(a, s, phases, flops, bytes);
+  }
 }
 
 // Only the (kind, input transform) pairs the hot path uses are instantiated.
-template <int KIND>
+template <int KIND, int SP>
 void launch_kind(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
   if (a.in_xform == IN_NONE) {
-    launch_kind_xf<KIND, IN_NONE>(a, s, phases, flops, bytes);
+    launch_kind_xf<KIND, IN_NONE, SP>(a, s, phases, flops, bytes);
   } else if constexpr (KIND == KIND_CONV1D || KIND == KIND_CONVT) {
     M2S_CHECK(a.in_xform == IN_LRELU, "conv_gemm: 1-D kinds take LeakyReLU inputs only");
-    launch_kind_xf<KIND, IN_LRELU>(a, s, phases, flops, bytes);
+    launch_kind_xf<KIND, IN_LRELU, SP>(a, s, phases, flops, bytes);
   } else if constexpr (KIND == KIND_GEMM) {
     M2S_CHECK(a.in_xform == IN_SE_SCALE, "conv_gemm: GEMM kind takes SE-scaled inputs only");
-    launch_kind_xf<KIND, IN_SE_SCALE>(a, s, phases, flops, bytes);
+    launch_kind_xf<KIND, IN_SE_SCALE, SP>(a, s, phases, flops, bytes);
   } else {
     M2S_CHECK(false, "conv_gemm: 2-D convs take untransformed inputs");
   }
@@ -439,7 +551,7 @@ void launch_kind(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
 
 }  // namespace
 
-void launch_conv_bf16_fast(const ConvArgs& a, hipStream_t s, double flops, double bytes) {
+void launch_conv_gemm(const ConvArgs& a, bool split, hipStream_t s, double flops, double bytes) {
   M2S_CHECK(a.cs_in % 8 == 0 && a.cs_out % 4 == 0, "conv_gemm: channel strides");
   M2S_CHECK(a.cs_in >= 32 ? a.cs_in % 32 == 0 : 32 % a.cs_in == 0, "conv_gemm: channel stride vs the 32-wide K step");
   M2S_CHECK(a.ntaps <= 31, "conv_gemm: at most 31 taps");
@@ -448,7 +560,7 @@ void launch_conv_bf16_fast(const ConvArgs& a, hipStream_t s, double flops, doubl
                             : a.kind == KIND_CONV1D ? (double)(a.M / a.L_out) * a.L_in * a.cs_in
                             : a.kind == KIND_CONVT  ? (double)a.M * a.cs_in
                                                     : (double)a.M * a.cs_in;
-    M2S_CHECK(in_elems < 2147483647.0, "conv_gemm: input too large for 32-bit offsets (use a smaller chunk)");
+    M2S_CHECK(in_elems * (split ? 2 : 1) < 2147483647.0, "conv_gemm: input too large for 32-bit offsets (use a smaller chunk)");
   }
   M2S_CHECK(a.kp % 32 == 0 && a.kp >= a.ntaps * a.cs_in, "conv_gemm: kp");
   M2S_CHECK(a.kind != KIND_CONV2D || a.ks == 3, "conv_gemm: 2-D kernels are 3x3 (1x1 runs as GEMM)");
@@ -457,12 +569,23 @@ void launch_conv_bf16_fast(const ConvArgs& a, hipStream_t s, double flops, doubl
     const char* e = getenv("M2S_CONV_HALO");
     return !e || atoi(e) != 0;
   }();
+  if (split) {
+    switch (a.kind) {
+      case KIND_CONV2D: launch_kind<KIND_CONV2D, 1>(a, s, 1, flops, bytes); break;
+      case KIND_CONV1D: launch_kind<KIND_CONV1D, 1>(a, s, 1, flops, bytes); break;
+      case KIND_CONVT: launch_kind<KIND_CONVT, 1>(a, s, a.ct_u, flops, bytes); break;
+      case KIND_GEMM: launch_kind<KIND_GEMM, 1>(a, s, 1, flops, bytes); break;
+      default: M2S_CHECK(false, "conv_gemm: bad kind");
+    }
+    M2S_HIP(hipGetLastError());
+    return;
+  }
   if (halo && conv_halo_supported(a)) return launch_conv_halo(a, s, flops, bytes);
   switch (a.kind) {
-    case KIND_CONV2D: launch_kind<KIND_CONV2D>(a, s, 1, flops, bytes); break;
-    case KIND_CONV1D: launch_kind<KIND_CONV1D>(a, s, 1, flops, bytes); break;
-    case KIND_CONVT: launch_kind<KIND_CONVT>(a, s, a.ct_u, flops, bytes); break;
-    case KIND_GEMM: launch_kind<KIND_GEMM>(a, s, 1, flops, bytes); break;
+    case KIND_CONV2D: launch_kind<KIND_CONV2D, 0>(a, s, 1, flops, bytes); break;
+    case KIND_CONV1D: launch_kind<KIND_CONV1D, 0>(a, s, 1, flops, bytes); break;
+    case KIND_CONVT: launch_kind<KIND_CONVT, 0>(a, s, a.ct_u, flops, bytes); break;
+    case KIND_GEMM: launch_kind<KIND_GEMM, 0>(a, s, 1, flops, bytes); break;
     default: M2S_CHECK(false, "conv_gemm: bad kind");
   }
   M2S_HIP(hipGetLastError());

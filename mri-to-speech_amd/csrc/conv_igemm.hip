@@ -272,13 +272,17 @@ void launch_kind(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
 
 template <typename T>
 void launch_conv(const ConvArgs& a, hipStream_t s, double flops, double bytes) {
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (std::is_same<T, sp_t>::value) {  // split fp32: three-term bf16 MFMA (conv_gemm.hip)
+    M2S_CHECK(a.kind != KIND_CONV2D || a.ks == 3, "conv: split 2-D convs are 3x3");
+    launch_conv_gemm(a, true, s, flops, bytes);
+    return;
+  } else if constexpr (sizeof(T) == 2) {
     static const bool v1 = [] {
       const char* e = getenv("M2S_CONV_IMPL");
       return e && std::string(e) == "v1";
     }();
     if (!v1 && (a.kind != KIND_CONV2D || a.ks == 3)) {
-      launch_conv_bf16_fast(a, s, flops, bytes);
+      launch_conv_gemm(a, false, s, flops, bytes);
       return;
     }
   }
@@ -300,5 +304,6 @@ void launch_conv(const ConvArgs& a, hipStream_t s, double flops, double bytes) {
 
 template void launch_conv<float>(const ConvArgs&, hipStream_t, double, double);
 template void launch_conv<bf16_t>(const ConvArgs&, hipStream_t, double, double);
+template void launch_conv<sp_t>(const ConvArgs&, hipStream_t, double, double);
 
 }  // namespace m2s

@@ -50,13 +50,14 @@ struct ConvArgs {
 };
 
 // flops / bytes: algorithmic work of this launch, recorded by the profiler (m2s_prof_*).
-// bf16 runs the LDS-DMA pipelined kernel (conv_gemm.hip) unless M2S_CONV_IMPL=v1; fp32 (the
-// parity path) runs the direct-load kernel of conv_igemm.hip.
+// bf16 and split fp32 (sp_t) run the LDS-DMA pipelined kernel (conv_gemm.hip); fp32 (the exact
+// f32-MFMA parity path) runs the direct-load kernel of conv_igemm.hip.
 template <typename T>
 void launch_conv(const ConvArgs& a, hipStream_t s, double flops = 0.0, double bytes = 0.0);
-void launch_conv_bf16_fast(const ConvArgs& a, hipStream_t s, double flops, double bytes);
+// split: x, w, res, y and in_scale hold [hi | lo] rows (m2s_common.hpp sp_t); w rows are 2 * kp long
+void launch_conv_gemm(const ConvArgs& a, bool split, hipStream_t s, double flops, double bytes);
 // bf16 3x3 stride-1 convs with cs_in in {32, 64}: persistent LDS-resident-weight kernel
-// (conv_halo.hip); launch_conv_bf16_fast routes them there.
+// (conv_halo.hip); launch_conv_gemm routes them there.
 bool conv_halo_supported(const ConvArgs& a);
 void launch_conv_halo(const ConvArgs& a, hipStream_t s, double flops, double bytes);
 

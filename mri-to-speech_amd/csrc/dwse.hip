@@ -68,15 +68,17 @@ __global__ void __launch_bounds__(256) dwconv_kernel(const T* __restrict__ x, in
         }
         g_cur = g;
       }
-      const T* xn = x + (long)n * IH * IW * cs + c0;
+      constexpr int R = Elem<T>::R;
+      const T* xn = x + (long)n * IH * IW * cs * R + c0;
       const int oy = p / OW, ox = p - (p / OW) * OW;
-      uint4 in[9];
+      uint4 in[9], inl[9];
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int iy = oy * S - pad_t + t / 3, ix = ox * S - pad_l + t % 3;
-        in[t] = (iy >= 0 && iy < IH && ix >= 0 && ix < IW)
-                    ? *reinterpret_cast<const uint4*>(xn + ((long)iy * IW + ix) * cs)
-                    : make_uint4(0, 0, 0, 0);
+        const bool ok = iy >= 0 && iy < IH && ix >= 0 && ix < IW;
+        in[t] = ok ? *reinterpret_cast<const uint4*>(xn + ((long)iy * IW + ix) * cs * R) : make_uint4(0, 0, 0, 0);
+        if constexpr (R == 2)  // split storage: the lo half of the same 8 channels, cs elements on
+          inl[t] = ok ? *reinterpret_cast<const uint4*>(xn + ((long)iy * IW + ix) * cs * R + cs) : make_uint4(0, 0, 0, 0);
       }
       float acc[8];
 #pragma unroll
@@ -100,6 +102,14 @@ __global__ void __launch_bounds__(256) dwconv_kernel(const T* __restrict__ x, in
             v[2 * j] = __uint_as_float(u[j] << 16);
             v[2 * j + 1] = __uint_as_float(u[j] & 0xffff0000u);
           }
+          if constexpr (R == 2) {
+            const uint32_t l[4] = {inl[t].x, inl[t].y, inl[t].z, inl[t].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              v[2 * j] += __uint_as_float(l[j] << 16);
+              v[2 * j + 1] += __uint_as_float(l[j] & 0xffff0000u);
+            }
+          }
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += w[t][j] * v[j];
@@ -110,7 +120,9 @@ __global__ void __launch_bounds__(256) dwconv_kernel(const T* __restrict__ x, in
         s[j] += acc[j];
       }
       T* o = y + ((long)n * P + p) * cs + c0;
-      if constexpr (sizeof(T) == 4) {
+      if constexpr (R == 2) {
+        act_st8<T>(y, (long)n * P + p, cs, c0, acc);
+      } else if constexpr (sizeof(T) == 4) {
         *reinterpret_cast<float4*>(o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
         *reinterpret_cast<float4*>(o + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
       } else {
@@ -148,7 +160,7 @@ __global__ void __launch_bounds__(256) se_mean_kernel(const float* __restrict__ 
   const int c = (int)(i - n * cs);
   float acc = 0.f;
   for (int q = 0; q < npb; ++q) acc += psum[(n * npb + q) * cs + c];
-  mean[i] = Elem<T>::from_f(acc * inv_count);
+  act_st<T>(mean, n, cs, c, acc * inv_count);
 }
 
 int dw_group(int OH, int OW) {
@@ -190,5 +202,8 @@ template void launch_dwconv<bf16_t>(const bf16_t*, int, int, int, int, int, int,
                                     const float*, bf16_t*, float*, hipStream_t);
 template void launch_se_mean<float>(const float*, int, int, int, float, float*, hipStream_t);
 template void launch_se_mean<bf16_t>(const float*, int, int, int, float, bf16_t*, hipStream_t);
+template void launch_dwconv<sp_t>(const sp_t*, int, int, int, int, int, int, int, int, int, int, const float*,
+                                  const float*, sp_t*, float*, hipStream_t);
+template void launch_se_mean<sp_t>(const float*, int, int, int, float, sp_t*, hipStream_t);
 
 }  // namespace m2s

@@ -11,29 +11,6 @@ namespace m2s {
 namespace {
 
 template <typename T>
-__device__ __forceinline__ void st4(T* p, float a, float b, float c, float d) {
-  if constexpr (sizeof(T) == 4) {
-    *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
-  } else {
-    uint2 u;
-    u.x = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
-    u.y = (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16);
-    *reinterpret_cast<uint2*>(p) = u;
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ float4 ld4(const T* p) {
-  if constexpr (sizeof(T) == 4) {
-    return *reinterpret_cast<const float4*>(p);
-  } else {
-    uint2 u = *reinterpret_cast<const uint2*>(p);
-    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
-  }
-}
-
-template <typename T>
 __device__ __forceinline__ float act_silu(float v) {
   return sizeof(T) == 4 ? silu_exact(v) : silu(v);
 }
@@ -80,14 +57,7 @@ __global__ void __launch_bounds__(256) stem_kernel(const float* __restrict__ fra
       for (int t = 0; t < 9; ++t) acc += w[j][t] * in[t];
       v[j] = act_silu<T>(acc + bb[j]);
     }
-    T* out = y + p * cs_out + o0;
-    if constexpr (sizeof(T) == 4) {
-      *reinterpret_cast<float4*>(out) = make_float4(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<float4*>(out + 4) = make_float4(v[4], v[5], v[6], v[7]);
-    } else {
-      *reinterpret_cast<uint4*>(out) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
-                                                  pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
-    }
+    act_st8<T>(y, p, cs_out, o0, v);
   }
 }
 
@@ -138,9 +108,8 @@ __global__ void __launch_bounds__(256) gap_kernel(const T* __restrict__ x, int N
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)N * C) return;
   const int n = (int)(i / C), c = (int)(i - (long)(i / C) * C);
-  const T* p = x + (long)n * P * cs + c;
   float acc = 0.f;
-  for (int k = 0; k < P; ++k) acc += Elem<T>::to_f(p[(long)k * cs]);
+  for (int k = 0; k < P; ++k) acc += act_ld<T>(x, (long)n * P + k, cs, c);
   feats[i] = acc / (float)P;
 }
 
@@ -227,7 +196,7 @@ __global__ void __launch_bounds__(256) mel_glue_kernel(const float* __restrict__
   if (i >= (long)rows * cs) return;
   const int r = (int)(i / cs), n = (int)(i - (long)(i / cs) * cs);
   if (n >= n_mels) {
-    if (ln_t) ln_t[i] = Elem<T>::from_f(0.f);
+    if (ln_t) act_st<T>(ln_t, r, cs, n, 0.f);
     return;
   }
   const long o = (long)r * n_mels + n;
@@ -239,7 +208,7 @@ __global__ void __launch_bounds__(256) mel_glue_kernel(const float* __restrict__
     const float l = logf(fmaxf(p, 1e-5f));
     if (db) db[o] = d;
     if (ln) ln[o] = l;
-    if (ln_t) ln_t[i] = Elem<T>::from_f(l);
+    if (ln_t) act_st<T>(ln_t, r, cs, n, l);
   }
 }
 
@@ -253,7 +222,7 @@ __global__ void __launch_bounds__(256) mel_to_nlc_kernel(const float* __restrict
   const int b = (int)(bt / Tn), t = (int)(bt - (long)b * Tn);
   float v = 0.f;
   if (c < C) v = layout == 0 ? mel[((long)b * C + c) * Tn + t] : mel[bt * C + c];
-  y[i] = Elem<T>::from_f(v);
+  act_st<T>(y, bt, cs, c, v);
 }
 
 template <typename T>
@@ -266,14 +235,12 @@ __global__ void __launch_bounds__(256) conv_post_kernel(const T* __restrict__ x,
   float acc = 0.f;
   for (int j = 0; j < 7; ++j) {
     if (t + j >= L) break;  // right zero pad of 6 (models.py:127)
-    const T* row = x + ((long)b * L + t + j) * cs;
     for (int c = 0; c < C; c += 4) {
-      const float4 v = ld4<T>(row + c);
+      float v[4];
+      act_ld4<T>(x, (long)b * L + t + j, cs, c, v);
       const float* wj = w + j * C + c;
-      acc += wj[0] * (v.x > 0.f ? v.x : 0.01f * v.x);
-      acc += wj[1] * (v.y > 0.f ? v.y : 0.01f * v.y);
-      acc += wj[2] * (v.z > 0.f ? v.z : 0.01f * v.z);
-      acc += wj[3] * (v.w > 0.f ? v.w : 0.01f * v.w);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc += wj[e] * (v[e] > 0.f ? v[e] : 0.01f * v[e]);
     }
   }
   wav[i] = tanhf(acc + bias);
@@ -291,7 +258,7 @@ __global__ void __launch_bounds__(256) unpad_kernel(const T* __restrict__ x, lon
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= rows * C) return;
   const long r = i / C;
-  y[i] = Elem<T>::to_f(x[r * cs + (i - r * C)]);
+  y[i] = act_ld<T>(x, r, cs, (int)(i - r * C));
 }
 
 inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
@@ -380,5 +347,6 @@ void launch_conv_post(const T* x, int B, int L, int C, int cs, const float* w, f
   template void launch_unpad<T>(const T*, long, int, int, float*, hipStream_t);
 M2S_INST(float)
 M2S_INST(bf16_t)
+M2S_INST(sp_t)
 
 }  // namespace m2s

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 
 namespace m2s {
 
@@ -47,19 +48,114 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{a, b}), bf16x2_t));
 }
 
+// Split-fp32 ("bf16x3") storage: an fp32 value v is kept as the bf16 pair hi = bf16(v),
+// lo = bf16(v - hi) (17 significant bits, relative error <= 2^-17), so a product of two such
+// values is three exact bf16 MFMA terms hi*hi + hi*lo + lo*hi accumulated in fp32.  A channel-last
+// tensor with channel stride cs stores every position as [hi: cs][lo: cs] bf16 (4 bytes per
+// channel, the footprint of fp32): a DMA of the hi chunk and one of the lo chunk at +cs.
+struct sp_t {
+  uint16_t v;
+};
+
 template <typename T> struct Elem;
 template <> struct Elem<float> {
   static constexpr int VEC = 4;  // elements per 16-byte lane load
   static constexpr int KC = 16;  // K covered by one 16-byte load set (4 x mfma 16x16x4 f32)
+  static constexpr int R = 1;    // planes per position
   __device__ static __forceinline__ float to_f(float v) { return v; }
   __device__ static __forceinline__ float from_f(float v) { return v; }
 };
 template <> struct Elem<bf16_t> {
   static constexpr int VEC = 8;
   static constexpr int KC = 32;  // one mfma 16x16x32 bf16
+  static constexpr int R = 1;
   __device__ static __forceinline__ float to_f(bf16_t v) { return bf2f(v); }
   __device__ static __forceinline__ bf16_t from_f(float v) { return f2bf(v); }
 };
+template <> struct Elem<sp_t> {
+  static constexpr int VEC = 8;
+  static constexpr int KC = 32;
+  static constexpr int R = 2;  // [hi cs][lo cs] per position
+};
+
+// Element access by (position p, channel c) for the three storage types.
+template <typename T>
+__device__ __forceinline__ float act_ld(const T* x, long p, int cs, int c) {
+  if constexpr (Elem<T>::R == 2) {
+    const uint16_t* u = reinterpret_cast<const uint16_t*>(x) + p * 2 * cs + c;
+    return bf2f(u[0]) + bf2f(u[cs]);
+  } else {
+    return Elem<T>::to_f(x[p * cs + c]);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void act_st(T* x, long p, int cs, int c, float v) {
+  if constexpr (Elem<T>::R == 2) {
+    uint16_t* u = reinterpret_cast<uint16_t*>(x) + p * 2 * cs + c;
+    const bf16_t h = f2bf(v);
+    u[0] = h;
+    u[cs] = f2bf(v - bf2f(h));
+  } else {
+    x[p * cs + c] = Elem<T>::from_f(v);
+  }
+}
+
+// 4 / 8 consecutive channels (c % 4 == 0 / c % 8 == 0) of one position, vectorised.
+__device__ __forceinline__ void unpack_bf16x4(uint2 u, float* v) {
+  v[0] = __uint_as_float(u.x << 16);
+  v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16);
+  v[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+template <typename T>
+__device__ __forceinline__ void act_ld4(const T* x, long p, int cs, int c, float* v) {
+  if constexpr (std::is_same<T, float>::value) {
+    const float4 f = *reinterpret_cast<const float4*>(x + p * cs + c);
+    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+  } else if constexpr (Elem<T>::R == 1) {
+    unpack_bf16x4(*reinterpret_cast<const uint2*>(x + p * cs + c), v);
+  } else {
+    const uint16_t* u = reinterpret_cast<const uint16_t*>(x) + p * 2 * cs + c;
+    float l[4];
+    unpack_bf16x4(*reinterpret_cast<const uint2*>(u), v);
+    unpack_bf16x4(*reinterpret_cast<const uint2*>(u + cs), l);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += l[j];
+  }
+}
+// split of 4 values: hi = bf16(v), lo = bf16(v - hi), each as 4 packed bf16
+__device__ __forceinline__ void split4(const float* v, uint2& hi, uint2& lo) {
+  hi.x = pack_bf16x2(v[0], v[1]);
+  hi.y = pack_bf16x2(v[2], v[3]);
+  float h[4];
+  unpack_bf16x4(hi, h);
+  lo.x = pack_bf16x2(v[0] - h[0], v[1] - h[1]);
+  lo.y = pack_bf16x2(v[2] - h[2], v[3] - h[3]);
+}
+template <typename T>
+__device__ __forceinline__ void act_st4(T* x, long p, int cs, int c, const float* v) {
+  if constexpr (std::is_same<T, float>::value) {
+    *reinterpret_cast<float4*>(x + p * cs + c) = make_float4(v[0], v[1], v[2], v[3]);
+  } else if constexpr (Elem<T>::R == 1) {
+    *reinterpret_cast<uint2*>(x + p * cs + c) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  } else {
+    uint16_t* u = reinterpret_cast<uint16_t*>(x) + p * 2 * cs + c;
+    uint2 hi, lo;
+    split4(v, hi, lo);
+    *reinterpret_cast<uint2*>(u) = hi;
+    *reinterpret_cast<uint2*>(u + cs) = lo;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void act_ld8(const T* x, long p, int cs, int c, float* v) {
+  act_ld4<T>(x, p, cs, c, v);
+  act_ld4<T>(x, p, cs, c + 4, v + 4);
+}
+template <typename T>
+__device__ __forceinline__ void act_st8(T* x, long p, int cs, int c, const float* v) {
+  act_st4<T>(x, p, cs, c, v);
+  act_st4<T>(x, p, cs, c + 4, v + 4);
+}
 
 // bf16-path activations: one v_exp_f32 + one v_rcp_f32 (1 ulp) instead of an IEEE divide and
 // __expf's denormal-range fix-up (a compare + select + multiply per value); e^-x underflowing to

@@ -69,15 +69,31 @@ static uint16_t f2bf_host(float f) {
   u += 0x7fffu + ((u >> 16) & 1u);
   return (uint16_t)(u >> 16);
 }
+static float bf2f_host(uint16_t h) {
+  const uint32_t u = (uint32_t)h << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+static void split_host(float f, uint16_t* hi, uint16_t* lo) {
+  *hi = f2bf_host(f);
+  *lo = f2bf_host(f - bf2f_host(*hi));
+}
 
 // Event-profiler record names = the kernels' demangled symbols as rocprofv3 prints them, so the
 // two profiles can be joined on the name.
 template <typename T>
 static std::string tname(const char* base, const char* extra = "") {
-  return std::string(base) + (std::is_same<T, bf16_t>::value ? "<unsigned short" : "<float") + extra + ">";
+  return std::string(base) + (std::is_same<T, bf16_t>::value ? "<unsigned short" : std::is_same<T, sp_t>::value ? "<m2s::sp_t" : "<float") +
+         extra + ">";
 }
 
-static int kc_of(int dtype) { return dtype == M2S_DT_BF16 ? Elem<bf16_t>::KC : Elem<float>::KC; }
+static int kc_of(int dtype) { return dtype == M2S_DT_F32 ? Elem<float>::KC : Elem<bf16_t>::KC; }
+// bytes per activation element of a dtype's storage (split fp32: hi + lo)
+static size_t act_bytes(int dtype) { return dtype == M2S_DT_BF16 ? 2 : 4; }
+
+// fp32 -> split pair (hi, lo) on the host, as the device's split4
+static void split_host(float f, uint16_t* hi, uint16_t* lo);
 
 static PConv make_pconv(int kind, int cin, int cout, int ntaps, int dtype) {
   PConv p;
@@ -106,6 +122,12 @@ static void pack_conv(Arena& ar, int dtype, PConv& p, Get get, Bias bias) {
   if (dtype == M2S_DT_BF16) {
     std::vector<uint16_t> h(w.size());
     for (size_t i = 0; i < w.size(); ++i) h[i] = f2bf_host(w[i]);
+    p.w_off = ar.add_vec(h);
+  } else if (dtype == M2S_DT_BF16X3) {  // rows [hi kp | lo kp]
+    std::vector<uint16_t> h(2 * w.size());
+    const size_t rows = w.size() / p.kp;
+    for (size_t r = 0; r < rows; ++r)
+      for (int k = 0; k < p.kp; ++k) split_host(w[r * p.kp + k], &h[2 * r * p.kp + k], &h[(2 * r + 1) * p.kp + k]);
     p.w_off = ar.add_vec(h);
   } else {
     p.w_off = ar.add_vec(w);
@@ -143,7 +165,7 @@ template <typename T>
 static void run_conv(const ConvArgs& a, const PConv& p, hipStream_t s) {
   const double rows = (double)a.M;
   const double flops = 2.0 * p.macs_per_row * rows;
-  const double es = sizeof(T);
+  const double es = sizeof(T) * Elem<T>::R;
   // compulsory traffic: input once, output once (+ residual/accum read), weights once
   double in_rows = p.kind == KIND_CONV2D ? (double)a.IH * a.IW * (a.M / ((double)a.OH * a.OW))
                                          : (p.kind == KIND_GEMM ? rows : 0.0);
@@ -199,7 +221,7 @@ static BN fold_bn(const StateDict& sd, const std::string& p, int c) {
 
 Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int device)
     : dtype_(dtype), device_(device), n_mels_(n_mels), hidden_(hidden) {
-  M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16, "bad dtype");
+  M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16 || dtype == M2S_DT_BF16X3, "bad dtype");
   M2S_CHECK(n_mels > 0 && hidden > 0 && hidden % 8 == 0, "bad n_mels / rnn_hidden");
   if (const char* e = std::getenv("M2S_IR_FUSED")) ir_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
@@ -488,7 +510,7 @@ void Acoustic::effnet_dims(int H, int W, size_t* io, size_t* mid, size_t* se) co
 size_t Acoustic::effnet_ws(int N, int H, int W) const {
   size_t io, mid, se;
   effnet_dims(H, W, &io, &mid, &se);
-  const size_t es = dtype_ == M2S_DT_BF16 ? 2 : 4;
+  const size_t es = act_bytes(dtype_);
   const size_t nc = std::min(N, chunk);
   Workspace ws(nullptr, 0);
   ws.take<char>(nc * io * es);
@@ -518,6 +540,8 @@ void Acoustic::effnet(const float* frames, int N, int H, int W, float* feats, in
                       int* probe_dims, Workspace& ws, hipStream_t s) {
   if (dtype_ == M2S_DT_BF16)
     effnet_t<bf16_t>(frames, N, H, W, feats, stop_after, probe, probe_dims, ws, s);
+  else if (dtype_ == M2S_DT_BF16X3)
+    effnet_t<sp_t>(frames, N, H, W, feats, stop_after, probe, probe_dims, ws, s);
   else
     effnet_t<float>(frames, N, H, W, feats, stop_after, probe, probe_dims, ws, s);
 }
@@ -529,14 +553,15 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
   size_t io, mid, se;
   effnet_dims(H, W, &io, &mid, &se);
   const int nc_max = std::min(N, chunk);
-  T* A = ws.take<T>((size_t)nc_max * io);
-  T* Bb = ws.take<T>((size_t)nc_max * io);
-  T* M = ws.take<T>((size_t)nc_max * mid);
-  T* M2 = ws.take<T>((size_t)nc_max * mid);
+  constexpr int R = Elem<T>::R;  // split fp32: hi + lo planes
+  T* A = ws.take<T>((size_t)nc_max * io * R);
+  T* Bb = ws.take<T>((size_t)nc_max * io * R);
+  T* M = ws.take<T>((size_t)nc_max * mid * R);
+  T* M2 = ws.take<T>((size_t)nc_max * mid * R);
   float* sums = ws.take<float>((size_t)nc_max * se);
-  T* se_mean = ws.take<T>((size_t)nc_max * max_mid_cs_);
-  T* se_hid = ws.take<T>((size_t)nc_max * SE_RD_MAX);
-  T* scale = ws.take<T>((size_t)nc_max * max_mid_cs_);
+  T* se_mean = ws.take<T>((size_t)nc_max * max_mid_cs_ * R);
+  T* se_hid = ws.take<T>((size_t)nc_max * SE_RD_MAX * R);
+  T* scale = ws.take<T>((size_t)nc_max * max_mid_cs_ * R);
 
   for (int n0 = 0; n0 < N; n0 += nc_max) {
     const int nc = std::min(nc_max, N - n0);
@@ -563,7 +588,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
       cc = 16;
       bi = 2;
     } else {
-      ProfScope ps(std::is_same<T, bf16_t>::value ? std::string("stem32_kernel") : tname<T>("stem_kernel"), 2.0 * nc * oh * ow * EFF_STEM * 27, 4.0 * nc * H * W + sizeof(T) * (double)nc * oh * ow * 32, s);
+      ProfScope ps(std::is_same<T, bf16_t>::value ? std::string("stem32_kernel") : tname<T>("stem_kernel"), 2.0 * nc * oh * ow * EFF_STEM * 27, 4.0 * nc * H * W + (sizeof(T) * Elem<T>::R) * (double)nc * oh * ow * 32, s);
       launch_stem<T>(frames + (size_t)n0 * H * W, nc, H, W, oh, ow, pt, pl, static_cast<const float*>(arena_.ptr(stem_w_)),
                      static_cast<const float*>(arena_.ptr(stem_b_)), EFF_STEM, chan_stride(EFF_STEM), A, s);
     }
@@ -675,13 +700,13 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         run_conv<T>(e, b.c1, s);
         {
           ProfScope ps(b.stride == 2 ? tname<T>("dwconv_kernel", ", 2") : tname<T>("dwconv_kernel", ", 1"), 2.0 * nc * nh * nw * b.mid * 9,
-                       sizeof(T) * (double)nc * (oh * ow + nh * nw) * b.mid, s);
+                       (sizeof(T) * Elem<T>::R) * (double)nc * (oh * ow + nh * nw) * b.mid, s);
           launch_dwconv<T>(M, nc, oh, ow, nh, nw, b.stride, qt, ql, b.mid, cs,
                            static_cast<const float*>(arena_.ptr(b.dw_w)), static_cast<const float*>(arena_.ptr(b.dw_b)),
                            M2, sums, s);
         }
         {
-          ProfScope ps(tname<T>("se_mean_kernel"), 0.0, 4.0 * nc * cs * dw_pixel_blocks(nh, nw) + sizeof(T) * (double)nc * cs, s);
+          ProfScope ps(tname<T>("se_mean_kernel"), 0.0, 4.0 * nc * cs * dw_pixel_blocks(nh, nw) + (sizeof(T) * Elem<T>::R) * (double)nc * cs, s);
           launch_se_mean<T>(sums, nc, dw_pixel_blocks(nh, nw), cs, 1.0f / (float)(nh * nw), se_mean, s);
         }
         }
@@ -724,7 +749,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
       }
     }
     if (stopped || !feats) continue;
-    ProfScope ps(tname<T>("gap_kernel"), (double)nc * oh * ow * cc, sizeof(T) * (double)nc * oh * ow * cc, s);
+    ProfScope ps(tname<T>("gap_kernel"), (double)nc * oh * ow * cc, (sizeof(T) * Elem<T>::R) * (double)nc * oh * ow * cc, s);
     launch_gap<T>(cur, nc, oh * ow, cc, chan_stride(cc), feats + (size_t)n0 * EFF_OUT, s);
   }
 }
@@ -797,7 +822,7 @@ static std::vector<float> fold_wn(const StateDict& sd, const std::string& p, std
 
 Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int device)
     : h_(h), dtype_(dtype), device_(device) {
-  M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16, "bad dtype");
+  M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16 || dtype == M2S_DT_BF16X3, "bad dtype");
   M2S_CHECK(h.resblock == 1 || h.resblock == 2, "resblock must be 1 or 2");
   if (const char* e = std::getenv("M2S_MRF_FUSED")) mrf_fused_ = std::strcmp(e, "0") != 0;
   M2S_CHECK(h.n_up >= 1 && h.n_up <= 8 && h.n_kernels >= 1 && h.n_kernels <= 8, "bad generator config");
@@ -918,7 +943,7 @@ size_t Vocoder::act_elems(int B, int T) const {
 }
 
 size_t Vocoder::workspace_bytes(int B, int T) const {
-  const size_t es = dtype_ == M2S_DT_BF16 ? 2 : 4;
+  const size_t es = act_bytes(dtype_);
   Workspace ws(nullptr, 0);
   ws.take<char>((size_t)B * T * chan_stride(h_.num_mels) * es);
   for (int i = 0; i < 5; ++i) ws.take<char>(act_elems(B, T) * es);
@@ -932,6 +957,10 @@ void Vocoder::forward(const float* mel, int layout, int B, int T, float* wav, Wo
     bf16_t* mn = ws.take<bf16_t>((size_t)B * T * cs);
     launch_mel_to_nlc<bf16_t>(mel, B, h_.num_mels, T, layout, mn, cs, s);
     run_t<bf16_t>(mn, B, T, wav, ws, s);
+  } else if (dtype_ == M2S_DT_BF16X3) {
+    sp_t* mn = ws.take<sp_t>((size_t)B * T * cs * 2);
+    launch_mel_to_nlc<sp_t>(mel, B, h_.num_mels, T, layout, mn, cs, s);
+    run_t<sp_t>(mn, B, T, wav, ws, s);
   } else {
     float* mn = ws.take<float>((size_t)B * T * cs);
     launch_mel_to_nlc<float>(mel, B, h_.num_mels, T, layout, mn, cs, s);
@@ -943,24 +972,28 @@ void Vocoder::forward_from_norm(const float* mel_norm, const float* mean, const 
                                 float* mel_db, float* mel_log, void* ln_buf, float* wav, Workspace& ws, hipStream_t s) {
   M2S_CHECK(B > 0 && T > 0, "vocoder: empty input");
   const int nm = h_.num_mels, cs = chan_stride(nm);
-  ws.take<char>((size_t)B * T * cs * (dtype_ == M2S_DT_BF16 ? 2 : 4));  // same carve as forward()
-  const bool bf = dtype_ == M2S_DT_BF16;
-  {
-    ProfScope ps(bf ? "mel_glue_kernel<unsigned short>" : "mel_glue_kernel<float>", 0.0, 4.0 * B * T * nm * 4, s);
-    if (bf)
-      launch_mel_glue<bf16_t>(mel_norm, B * T, nm, mean, std_, mel_db, mel_log, static_cast<bf16_t*>(ln_buf), cs, s);
-    else
-      launch_mel_glue<float>(mel_norm, B * T, nm, mean, std_, mel_db, mel_log, static_cast<float*>(ln_buf), cs, s);
+  ws.take<char>((size_t)B * T * cs * act_bytes(dtype_));  // same carve as forward()
+  if (dtype_ == M2S_DT_BF16) {
+    ProfScope ps("mel_glue_kernel<unsigned short>", 0.0, 4.0 * B * T * nm * 4, s);
+    launch_mel_glue<bf16_t>(mel_norm, B * T, nm, mean, std_, mel_db, mel_log, static_cast<bf16_t*>(ln_buf), cs, s);
+  } else if (dtype_ == M2S_DT_BF16X3) {
+    ProfScope ps("mel_glue_kernel<m2s::sp_t>", 0.0, 4.0 * B * T * nm * 4, s);
+    launch_mel_glue<sp_t>(mel_norm, B * T, nm, mean, std_, mel_db, mel_log, static_cast<sp_t*>(ln_buf), cs, s);
+  } else {
+    ProfScope ps("mel_glue_kernel<float>", 0.0, 4.0 * B * T * nm * 4, s);
+    launch_mel_glue<float>(mel_norm, B * T, nm, mean, std_, mel_db, mel_log, static_cast<float*>(ln_buf), cs, s);
   }
-  if (bf)
+  if (dtype_ == M2S_DT_BF16)
     run_t<bf16_t>(ln_buf, B, T, wav, ws, s);
+  else if (dtype_ == M2S_DT_BF16X3)
+    run_t<sp_t>(ln_buf, B, T, wav, ws, s);
   else
     run_t<float>(ln_buf, B, T, wav, ws, s);
 }
 
 template <typename T>
 void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& ws, hipStream_t s) {
-  const size_t n = act_elems(B, Tn);
+  const size_t n = act_elems(B, Tn) * Elem<T>::R;
   T* X = ws.take<T>(n);
   T* Hb[2] = {ws.take<T>(n), ws.take<T>(n)};
   T* T1 = ws.take<T>(n);
@@ -1046,7 +1079,7 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
       }
     }
   }
-  ProfScope ps(tname<T>("conv_post_kernel"), 2.0 * B * L * post_c_ * 7, sizeof(T) * (double)B * L * post_c_ + 4.0 * B * L, s);
+  ProfScope ps(tname<T>("conv_post_kernel"), 2.0 * B * L * post_c_ * 7, (sizeof(T) * Elem<T>::R) * (double)B * L * post_c_ + 4.0 * B * L, s);
   launch_conv_post<T>(S, B, L, post_c_, chan_stride(post_c_), static_cast<const float*>(arena_.ptr(post_w_)), post_b_,
                       wav, s);
 }

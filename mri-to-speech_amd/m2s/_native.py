@@ -14,8 +14,9 @@ import numpy as np
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libm2s.so")
 
-F32, BF16 = 0, 1
-DTYPES = {"fp32": F32, "float32": F32, "f32": F32, "bf16": BF16, "bfloat16": BF16}
+F32, BF16, BF16X3 = 0, 1, 2
+# "bf16x3": split fp32 (hi + lo bf16 pairs, three-term MFMA products), fp32 tolerance (include/m2s.h)
+DTYPES = {"fp32": F32, "float32": F32, "f32": F32, "bf16": BF16, "bfloat16": BF16, "bf16x3": BF16X3}
 ELEM_F32, ELEM_I64 = 0, 1
 
 

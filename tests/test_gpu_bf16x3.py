@@ -1,0 +1,97 @@
+"""Split-fp32 ("bf16x3") path vs the CPU oracle and the reference goldens at the fp32 tolerances.
+
+bf16x3 keeps every activation and weight as a bf16 pair hi + lo (17 significant bits) and forms
+each product as the three exact bf16 MFMA terms hi*hi + hi*lo + lo*hi with fp32 accumulation
+(include/m2s.h M2S_DT_BF16X3).  It must pass the SAME bars as the exact-f32 path
+(tests/test_gpu_parity.py): wav max |d| <= 1e-4 vs the reference goldens, CNN taps <= 1e-4 of the
+tensor's scale, mel_norm <= 1e-4 and wav <= 2e-4 end to end.  GPU box only.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from m2s import synth
+from m2s.config import HIFIGAN_H
+from oracle import acoustic, effnet, hifigan
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+DEV = torch.device("cuda", 0)
+
+
+def _gold(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+def _rel(a, b):
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-6))
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from m2s import runtime
+    return runtime
+
+
+@pytest.fixture(scope="module")
+def ac_state():
+    g = _gold("acoustic.npz")
+    return synth.synth_acoustic_state(int(g["seed"]))
+
+
+@pytest.mark.parametrize("case", ["r1", "r2"])
+def test_vocoder_bf16x3_matches_reference_golden(rt, case):
+    g = _gold("generator.npz")
+    h = json.loads(bytes(g[f"{case}_h"]).decode())
+    voc = rt.VocoderEngine(synth.synth_generator_state(int(g["seed"]), h), h, dtype="bf16x3", device=DEV)
+    wav = voc.forward(torch.from_numpy(g[f"{case}_mel"]).to(DEV)).cpu().numpy()
+    np.testing.assert_allclose(wav, g[f"{case}_wav"], atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("B,T", [(1, 1), (3, 17), (2, 64)])
+def test_vocoder_bf16x3_vs_oracle_shapes(rt, B, T):
+    sd = synth.synth_generator_state(5, HIFIGAN_H)
+    voc = rt.VocoderEngine(sd, HIFIGAN_H, dtype="bf16x3", device=DEV)
+    mel = synth.synth_mel_log(B, 64, T, seed=B * 100 + T)
+    ref = hifigan.generator({k: torch.from_numpy(v) for k, v in sd.items()}, HIFIGAN_H, torch.from_numpy(mel)).numpy()
+    wav = voc.forward(torch.from_numpy(mel).to(DEV)).cpu().numpy()
+    np.testing.assert_allclose(wav, ref, atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("hw", [(256, 256), (96, 80), (67, 101)])
+def test_effnet_bf16x3_every_block(rt, ac_state, hw):
+    sd = {k: torch.from_numpy(v) for k, v in ac_state.items()}
+    fr = torch.from_numpy(synth.synth_frames(1, 3, hw=hw, seed=4)[0])
+    taps = []
+    effnet.effnet_features(sd, fr, taps=taps)
+    eng = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    x = fr.to(DEV)
+    for i, ref in enumerate(taps):
+        got = eng.probe(x, i).cpu().numpy()
+        assert got.shape == ref.shape, (i, got.shape, ref.shape)
+        assert _rel(got, ref.numpy()) <= 1e-4, f"block {i}: rel err {_rel(got, ref.numpy())}"
+    gap = eng.effnet(x).cpu().numpy()
+    assert _rel(gap, effnet.effnet_gap(sd, fr).numpy()) <= 1e-4
+
+
+def test_pipeline_bf16x3_end_to_end(rt, ac_state):
+    sd = {k: torch.from_numpy(v) for k, v in ac_state.items()}
+    gsd = synth.synth_generator_state(3)
+    mean, std = synth.synth_scaler()
+    pipe = rt.Pipeline(rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV),
+                       rt.VocoderEngine(gsd, HIFIGAN_H, dtype="bf16x3", device=DEV), mean, std)
+    fr = synth.synth_frames(2, 6, seed=21)
+    out = {k: v.cpu().numpy() for k, v in pipe.forward(torch.from_numpy(fr).to(DEV)).items()}
+    B, T = fr.shape[:2]
+    f = effnet.effnet_gap(sd, torch.from_numpy(fr).reshape(B * T, 256, 256)).view(B, T, -1)
+    mn = acoustic.head(sd, acoustic.bilstm_summerge(sd, f))
+    db = acoustic.denormalize_mel(mn, mean, std)
+    ln = acoustic.mel_db_to_log(db)
+    wav = hifigan.generator({k: torch.from_numpy(v) for k, v in gsd.items()}, HIFIGAN_H, ln.transpose(1, 2))
+    np.testing.assert_allclose(out["mel_norm"], mn.numpy(), atol=1e-4, rtol=0)
+    np.testing.assert_allclose(out["mel_db"], db.numpy(), atol=2e-3, rtol=0)
+    np.testing.assert_allclose(out["mel_log"], ln.numpy(), atol=5e-4, rtol=0)
+    np.testing.assert_allclose(out["wav"], wav[:, 0].numpy(), atol=2e-4, rtol=0)
