@@ -4,10 +4,18 @@
 Metric (BASELINE.json): rtMRI frames/s (and real-time factor) end to end, 256x256 frames.
 Workload per GPU (weak scaling): ``--clips`` synthetic clips x ``--frames`` frames (default
 64 x 30 = the per-GPU share of configs[3], 512 clips over 8 GPUs), CNN-BiLSTM + head + mel glue
-+ HiFi-GAN generator, compute dtype ``--dtype`` (bf16 default, configs[1]).  One step = one pass
-of the whole path over the per-GPU batch with frames already resident in HBM, followed by the
-RCCL gather of wav + mel to rank 0 (N > 1).  Weights are random-init of the reference
-architecture (no checkpoints offline), broadcast from rank 0 over RCCL once, outside the timing.
++ HiFi-GAN generator.  One step = one pass of the whole path over the per-GPU batch with frames
+already resident in HBM, followed by the RCCL gather of wav + mel to rank 0 (N > 1).  Weights are
+random-init of the reference architecture (no checkpoints offline), broadcast from rank 0 over
+RCCL once, outside the timing.
+
+Precision.  The reference computes in fp32 (scripts/run_mri_video_inference.py:215-242, no
+autocast).  The headline dtype is ``bf16x3``: split fp32, every activation and weight a bf16 pair
+hi + lo and every product the three exact bf16 MFMA terms hi*hi + hi*lo + lo*hi accumulated in fp32
+(include/m2s.h).  The line carries its measured error against the fp32 CPU oracle on clip 0 of the
+same workload (``parity``), next to the fp32 tolerances of tests/test_gpu_configs.py.  At N = 1 a
+second, shorter run of the bf16 path (configs[1]'s dtype) is reported under ``bf16`` with its own
+error; it is not the headline.
 
 Launch: ``python bench.py`` (N=1) or
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N``.
@@ -17,7 +25,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -34,13 +41,28 @@ from m2s.config import HIFIGAN_H  # noqa: E402
 
 HOP = 420
 SR = 11413
-PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "bf16x3": 2500.0 / 3}  # dense MFMA peaks, MI355X_MICROARCH.md
+# dense MFMA peaks (MI355X_MICROARCH.md): per ALGORITHMIC flop, so bf16x3 (three bf16 MFMAs per
+# product) peaks at a third of the bf16 rate
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "bf16x3": 2500.0 / 3}
 PEAK_HBM_GBS = 8000.0
+FP32_TOL = {"mel_norm": 1e-4, "mel_log": 5e-4, "wav": 2e-4}  # tests/test_gpu_configs.py
+PRECISION = {
+    "bf16x3": "split fp32: bf16 hi+lo pairs (17-bit), 3 bf16 MFMA terms per product, fp32 accumulate; "
+              "BiLSTM/head/glue exact fp32",
+    "fp32": "exact f32 MFMA products (v_mfma_f32_16x16x4_f32), fp32 storage",
+    "bf16": "bf16 storage and operands, fp32 accumulate; BiLSTM/head/glue fp32",
+}
 
-
-MFMA_KERNELS = ("conv_gemm_kernel", "conv_halo_kernel", "conv_igemm_kernel", "ir_pwdw_kernel", "lstm_persistent_kernel",
+MFMA_KERNELS = ("conv_gemm_kernel", "conv_halo_kernel", "conv_igemm_kernel", "ir_pwdw", "lstm_persistent_kernel",
                 "rb1_fused_kernel", "stem_b0_kernel", "se_excite_kernel", "er_fused_kernel", "er2_fused_kernel",
-                "ir_block_kernel")
+                "ers2_fused_kernel")
+
+
+def kernel_arith(name: str, dtype: str) -> str:
+    """Arithmetic of a kernel in a run of `dtype`: the BiLSTM and its input projection are exact f32."""
+    if name.startswith("lstm_persistent") or name.startswith("lstm_step") or "<float" in name:
+        return "fp32"
+    return dtype
 
 
 def pmc_traffic(kernel):
@@ -57,23 +79,25 @@ def pmc_traffic(kernel):
     return round(k["hbm_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--clips", type=int, default=64, help="clips per GPU")
     p.add_argument("--frames", type=int, default=30, help="frames per clip")
     p.add_argument("--hw", type=int, default=256)
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "bf16x3"])
+    p.add_argument("--dtype", default="bf16x3", choices=["bf16x3", "fp32", "bf16"])
     p.add_argument("--chunk", type=int, default=1920, help="frames per CNN pass (1920 = one pass over the 64x30 step)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-profile", action="store_true")
-    return p.parse_args()
+    p.add_argument("--no-parity", action="store_true", help="skip the oracle check of clip 0")
+    p.add_argument("--no-compare", action="store_true", help="skip the secondary bf16 line (N = 1)")
+    return p.parse_args(argv)
 
 
-def init_dist(args):
+def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -81,6 +105,23 @@ def init_dist(args):
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
+
+
+def timed_loop(step, k: int, world: int, sync, device) -> float:
+    """Barrier + sync on both sides of exactly `k` steps; the max of the ranks' wall times."""
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        step()
+    if world > 1:
+        dist.barrier()
+    sync()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    return float(el.item())
 
 
 def make_frames(clips, frames, hw, rank, device):
@@ -92,13 +133,37 @@ def make_frames(clips, frames, hw, rank, device):
     return ((x - lo) / (hi - lo)).contiguous()
 
 
+def cpu_threads():
+    """Threads for the CPU leg: the host cores this process may run on (sched_getaffinity), capped by
+    OMP_NUM_THREADS when the box sets one (the GPU box's CPU share)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(aff, omp) if omp > 0 else aff), aff
+
+
+def oracle_clip(ac_sd, gen_sd, mean, std, frames_np):
+    sys.path.insert(0, REPO)
+    from oracle import pipeline
+    t = lambda sd: {k: torch.from_numpy(v) for k, v in sd.items()}  # noqa: E731
+    return pipeline.e2e(t(ac_sd), t(gen_sd), HIFIGAN_H, frames_np, mean, std)
+
+
+def parity_vs(ref, out, clip=0):
+    got = {k: out[k][clip:clip + 1].float().cpu().numpy() for k in ("mel_norm", "mel_log", "wav")}
+    w, rw = got["wav"].astype(np.float64), ref["wav"].astype(np.float64)
+    res = {f"{k}_max_abs": float(np.abs(got[k] - ref[k]).max()) for k in got}
+    res["wav_snr_db"] = round(float(10 * np.log10(np.sum(rw ** 2) / max(np.sum((w - rw) ** 2), 1e-30))), 2)
+    res["within_fp32_tol"] = all(res[f"{k}_max_abs"] <= t for k, t in FP32_TOL.items())
+    return res
+
+
 def cpu_baseline(args, ac_sd, gen_sd, mean, std):
     """Oracle (torch-CPU fp32 restatement of the reference graph) on this host's cores."""
     sys.path.insert(0, REPO)
     from oracle import acoustic, effnet, hifigan
 
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    torch.set_num_threads(cores)
+    threads, aff = cpu_threads()
+    torch.set_num_threads(threads)
     sd = {k: torch.from_numpy(v) for k, v in ac_sd.items()}
     gsd = {k: torch.from_numpy(v) for k, v in gen_sd.items()}
     T = args.frames
@@ -114,14 +179,50 @@ def cpu_baseline(args, ac_sd, gen_sd, mean, std):
             el = time.perf_counter() - t0
             if el >= args.cpu_seconds or done >= 50:
                 break
-    return {"value": round(done * T / el, 3), "unit": "rtMRI frames/s", "cores": cores, "kind": "port",
+    return {"value": round(done * T / el, 3), "unit": "rtMRI frames/s", "cores": threads, "affinity_cpus": aff,
+            "kind": "port",
             "sample": f"{done} clip(s) x {T} frames at {args.hw}x{args.hw}, end to end (CNN-BiLSTM + glue + "
-                      f"HiFi-GAN), fp32 oracle (torch-CPU restatement of the reference graph), {el:.1f} s"}
+                      f"HiFi-GAN), fp32 oracle (torch-CPU restatement of the reference graph), {el:.1f} s, "
+                      f"{threads} threads (sched_getaffinity {aff}, OMP_NUM_THREADS cap)"}
+
+
+def roofline(stats, dtype, steps, fps, frames_per_step):
+    tot_ms = sum(s["ms"] for s in stats)
+    dom = max(stats, key=lambda s: s["ms"])
+    ar = kernel_arith(dom["name"], dtype)
+    peak_tf = PEAK_TFLOPS[ar]
+    ridge = peak_tf * 1e12 / (PEAK_HBM_GBS * 1e9)  # bound = the roof its algorithmic intensity hits first
+    if dom["bytes"] <= 0 or dom["flops"] / dom["bytes"] > ridge:
+        achieved = dom["flops"] / (dom["ms"] * 1e-3) / 1e12
+        peak, unit, bound = peak_tf, "TFLOP/s", "mfma"
+    else:
+        achieved = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9
+        peak, unit, bound = PEAK_HBM_GBS, "GB/s", "hbm"
+    mm = [s for s in stats if s["name"].startswith(MFMA_KERNELS)]
+    mm_ms, mm_fl = sum(s["ms"] for s in mm), sum(s["flops"] for s in mm)
+    flop_per_frame = sum(s["flops"] for s in stats) / (steps * frames_per_step)
+    traffic, tsrc = pmc_traffic(dom["name"])
+    r = {
+        "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": unit,
+        "frac": round(achieved / peak, 4), "traffic": traffic,
+        "kernel": dom["name"], "arith": ar, "launches_per_step": dom["launches"] // steps,
+        "avg_launch_us": round(1000.0 * dom["ms"] / dom["launches"], 2),
+        "algorithmic_bytes_per_launch": round(dom["bytes"] / dom["launches"]),
+        "algorithmic_flop_per_launch": round(dom["flops"] / dom["launches"]),
+        "kernel_share_of_gpu_time": round(dom["ms"] / tot_ms, 3),
+        "all_mfma_kernels_tflops": round(mm_fl / (mm_ms * 1e-3) / 1e12, 2),
+        "plan_gflop_per_frame": round(flop_per_frame / 1e9, 4),
+        "e2e_tflops": round(flop_per_frame * fps / 1e12, 2),
+        "e2e_frac_of_peak": round(flop_per_frame * fps / 1e12 / PEAK_TFLOPS[dtype], 4),
+    }
+    if tsrc:
+        r["traffic_source"] = tsrc
+    return r
 
 
 def main():
     args = parse()
-    world, rank, local = init_dist(args)
+    world, rank, local = init_dist()
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     from m2s import _native, dp, runtime
@@ -130,45 +231,33 @@ def main():
     # (Other ranks start from a differently seeded state so the broadcast is what makes them equal.)
     ac_sd = synth.synth_acoustic_state(0 if rank == 0 else 1000 + rank)
     gen_sd = synth.synth_generator_state(0 if rank == 0 else 1000 + rank)
-    ac_sd_b = dp.broadcast_state(ac_sd, device)
-    gen_sd_b = dp.broadcast_state(gen_sd, device)
+    ac_sd = dp.broadcast_state(ac_sd, device)
+    gen_sd = dp.broadcast_state(gen_sd, device)
     mean, std = synth.synth_scaler()
-    ac = runtime.AcousticEngine(ac_sd_b, dtype=args.dtype, device=device, chunk=args.chunk)
-    voc = runtime.VocoderEngine(gen_sd_b, HIFIGAN_H, dtype=args.dtype, device=device)
-    pipe = runtime.Pipeline(ac, voc, mean, std)
 
+    def build(dtype):
+        ac = runtime.AcousticEngine(ac_sd, dtype=dtype, device=device, chunk=args.chunk)
+        voc = runtime.VocoderEngine(gen_sd, HIFIGAN_H, dtype=dtype, device=device)
+        return runtime.Pipeline(ac, voc, mean, std)
+
+    pipe = build(args.dtype)
     B, T, HW = args.clips, args.frames, args.hw
     frames = make_frames(B, T, HW, rank, device)
-    out = {"wav": torch.empty(B, T * HOP, device=device), "mel_db": torch.empty(B, T, 64, device=device),
-           "mel_log": torch.empty(B, T, 64, device=device)}
+    out = {"wav": torch.empty(B, T * HOP, device=device), "mel_norm": torch.empty(B, T, 64, device=device),
+           "mel_db": torch.empty(B, T, 64, device=device), "mel_log": torch.empty(B, T, 64, device=device)}
     if world > 1:  # C3: clip lengths of every rank (the gather is sized from them)
         all_lens = dp.all_gather_lengths([T] * B, device)
 
-    def step():
-        pipe.forward(frames, out=out)
+    def step(p=None):
+        (p or pipe).forward(frames, out=out)
         if world > 1:  # C2: wav + dB mel of every clip to rank 0 over RCCL
-            dp.gather_results(out["wav"], all_lens)
-            dp.gather_results(out["mel_db"], all_lens)
+            dp.gather_results(out["wav"], all_lens, per_step=HOP)
+            dp.gather_results(out["mel_db"], all_lens, per_step=1)
 
+    sync = lambda: torch.cuda.synchronize(device)  # noqa: E731
     for _ in range(args.warmup):
         step()
-
-    def timed(k):
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        for _ in range(k):
-            step()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(device)
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
-        if world > 1:
-            dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        return float(el.item())
-
-    elapsed = timed(args.steps)
+    elapsed = timed_loop(step, args.steps, world, sync, device)
     frames_total = world * B * T * args.steps
     fps = frames_total / elapsed
     audio_s = frames_total * HOP / SR
@@ -184,10 +273,11 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
+        "precision": PRECISION[args.dtype],
         "data": "synthetic (seeded U[0,1) frames, per-frame min-max; random-init weights of the reference architecture)",
         "rtf": round(elapsed / audio_s, 6),
         "config": {"workload": f"e2e rtMRI->wav, {B} clips x {T} frames per GPU at {HW}x{HW} " +
-                               ("(configs[4] clip length, bf16)" if T >= 1000 else "(configs[3] per-GPU share)"),
+                               ("(configs[4] clip length)" if T >= 1000 else "(configs[3] per-GPU share)"),
                    "clips_per_gpu": B, "frames_per_clip": T, "global_batch_clips": B * world, "hw": HW,
                    "parallelism": f"dp{world}", "chunk": args.chunk},
     }
@@ -195,42 +285,32 @@ def main():
     # roofline: a second pass identical to the timed region with HIP events around every launch
     if not args.no_profile:
         _native.prof_enable(True)
-        timed(args.steps)
+        timed_loop(step, args.steps, world, sync, device)
         _native.prof_enable(False)
         stats = _native.prof_collect()
-        tot_ms = sum(s["ms"] for s in stats)
-        dom = max(stats, key=lambda s: s["ms"])
-        # bound = the roof its algorithmic intensity hits first (ridge = peak FLOP/s / HBM B/s)
-        peak_tf = PEAK_TFLOPS["fp32" if args.dtype == "fp32" or "float" in dom["name"] else args.dtype]
-        ridge = peak_tf * 1e12 / (PEAK_HBM_GBS * 1e9)
-        if dom["bytes"] <= 0 or dom["flops"] / dom["bytes"] > ridge:
-            achieved = dom["flops"] / (dom["ms"] * 1e-3) / 1e12
-            peak, unit, bound = peak_tf, "TFLOP/s", "mfma"
-        else:
-            achieved = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9
-            peak, unit, bound = PEAK_HBM_GBS, "GB/s", "hbm"
-        mm = [s for s in stats if s["name"].startswith(MFMA_KERNELS)]
-        mm_ms, mm_fl = sum(s["ms"] for s in mm), sum(s["flops"] for s in mm)
-        traffic, tsrc = pmc_traffic(dom["name"])
-        result["roofline"] = {
-            "bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": traffic,
-            "kernel": dom["name"], "launches_per_step": dom["launches"] // args.steps,
-            "avg_launch_us": round(1000.0 * dom["ms"] / dom["launches"], 2),
-            "algorithmic_bytes_per_launch": round(dom["bytes"] / dom["launches"]),
-            "algorithmic_flop_per_launch": round(dom["flops"] / dom["launches"]),
-            "kernel_share_of_gpu_time": round(dom["ms"] / tot_ms, 3),
-            "all_mfma_kernels_tflops": round(mm_fl / (mm_ms * 1e-3) / 1e12, 2),
-            "e2e_tflops": round(3.831e9 * fps / 1e12, 2),
-        }
-        if tsrc:
-            result["roofline"]["traffic_source"] = tsrc
+        result["roofline"] = roofline(stats, args.dtype, args.steps, fps, B * T)
         if rank == 0 and os.environ.get("M2S_BENCH_KERNELS"):
             for s in sorted(stats, key=lambda s: -s["ms"]):
                 print(f"# {s['name']:40s} n={s['launches']:6d} ms={s['ms']:9.3f} "
                       f"TF/s={s['flops'] / max(s['ms'], 1e-9) / 1e9:8.2f} GB/s={s['bytes'] / max(s['ms'], 1e-9) / 1e6:8.1f}",
                       file=sys.stderr)
 
+    ref0 = None
+    if rank == 0 and not args.no_parity:  # clip 0 of this rank's workload through the fp32 oracle
+        ref0 = oracle_clip(ac_sd, gen_sd, mean, std, frames[:1].cpu().numpy())
+        result["parity"] = dict(parity_vs(ref0, out), clip=0, tolerance=FP32_TOL, reference="fp32 CPU oracle")
+    if world == 1 and not args.no_compare and args.dtype != "bf16":
+        del pipe
+        bpipe = build("bf16")
+        for _ in range(args.warmup):
+            step(bpipe)
+        k = max(5, args.steps // 2)
+        el = timed_loop(lambda: step(bpipe), k, world, sync, device)
+        result["bf16"] = {"value": round(B * T * k / el, 2), "ms_per_step": round(1000.0 * el / k, 3), "steps": k,
+                          "precision": PRECISION["bf16"]}
+        if ref0 is not None:
+            result["bf16"]["parity"] = parity_vs(ref0, out)
+        del bpipe
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, ac_sd, gen_sd, mean, std)
     if rank == 0:
@@ -239,7 +319,7 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     # release the engines' device memory while the HIP runtime is still up
-    del pipe, ac, voc, frames, out
+    del frames, out
     torch.cuda.synchronize(device)
 
 

@@ -69,27 +69,31 @@ def all_gather_lengths(local_lengths: Sequence[int], device: torch.device) -> Li
     return [[int(v) for v in b.tolist() if v >= 0] for b in bufs]
 
 
-def gather_results(local: torch.Tensor, lengths_by_rank: List[List[int]], dst: int = 0):
-    """C2.  ``local`` is this rank's (n_local, max_len_local, ...) result; returns, on ``dst``, the
-    per-rank list of tensors trimmed to (n_r, max_len_r, ...), else None.  Ranks pad to a common
-    (max clips, max length) so a single gather moves everything."""
+def gather_results(local: torch.Tensor, lengths_by_rank: List[List[int]], per_step: int, dst: int = 0):
+    """C2.  ``local`` is this rank's (n_local, max_len_local * per_step, ...) result (``per_step`` =
+    samples per mel frame: the hop for wav, 1 for mels); returns, on ``dst``, the per-rank list of
+    tensors trimmed to (n_r, max_len_r * per_step, ...), else None.  Every rank pads to the same
+    (max clips, max length) buffer, computed from ``lengths_by_rank`` alone, so ranks with no clips
+    (world > clips) take part with an all-padding buffer and a single gather moves everything."""
     world = dist.get_world_size()
     rank = dist.get_rank()
+    if per_step < 1:
+        raise ValueError("per_step must be >= 1")
     cap_n = max(max(len(l) for l in lengths_by_rank), 1)
     cap_t = max(max((max(l) if l else 0) for l in lengths_by_rank), 1)
     if local.dim() < 2:
         raise ValueError("expected (clips, time, ...) results")
-    scale = local.shape[1] // max(max(lengths_by_rank[rank]) if lengths_by_rank[rank] else 1, 1)
-    shape = (cap_n, cap_t * scale) + tuple(local.shape[2:])
+    shape = (cap_n, cap_t * per_step) + tuple(local.shape[2:])
     send = torch.zeros(shape, dtype=local.dtype, device=local.device)
-    send[: local.shape[0], : local.shape[1]] = local
+    if local.numel():
+        send[: local.shape[0], : local.shape[1]] = local
     if rank == dst:
         recv = [torch.empty_like(send) for _ in range(world)]
         dist.gather(send, recv, dst=dst)
         out = []
         for r in range(world):
             lens = lengths_by_rank[r]
-            n, t = len(lens), (max(lens) if lens else 0) * scale
+            n, t = len(lens), (max(lens) if lens else 0) * per_step
             out.append(recv[r][:n, :t])
         return out
     dist.gather(send, None, dst=dst)

@@ -1,0 +1,88 @@
+"""bench.py host logic on CPU: the timed loop of the N-GPU path (barriers, max over ranks, the wav /
+mel gather) under gloo with world 2, and the roofline arithmetic on synthetic profiler records."""
+import os
+import socket
+import sys
+import time
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+from m2s import dp  # noqa: E402
+
+
+def test_parse_defaults_are_the_headline_workload():
+    a = bench.parse([])
+    assert (a.gpus, a.clips, a.frames, a.hw, a.dtype) == (1, 64, 30, 256, "bf16x3")
+    assert a.steps * 0.06 >= 1.0  # a timed region of about a second or more at ~60 ms per step
+
+
+def test_roofline_picks_the_dominant_kernel_and_its_arithmetic():
+    stats = [
+        {"name": "dwconv_kernel<m2s::sp_t, 1>", "launches": 36, "ms": 20.0, "flops": 4e9 * 36, "bytes": 1.8e9 * 36},
+        {"name": "lstm_persistent_kernel", "launches": 2, "ms": 1.2, "flops": 2e10, "bytes": 1e8},
+        {"name": "conv_gemm_kernel<128, 128, 4, 4, 2, 3, 0, 1>", "launches": 40, "ms": 10.0, "flops": 1e12, "bytes": 1e10},
+    ]
+    r = bench.roofline(stats, "bf16x3", steps=2, fps=30000.0, frames_per_step=1920)
+    assert r["kernel"].startswith("dwconv") and r["bound"] == "hbm" and r["unit"] == "GB/s"
+    assert abs(r["achieved"] - 1.8e9 * 36 / 20e-3 / 1e9) < 1e-6 * r["achieved"]
+    assert r["launches_per_step"] == 18
+    assert bench.kernel_arith("lstm_persistent_kernel", "bf16x3") == "fp32"
+    assert bench.kernel_arith("conv_igemm_kernel<float, 2, 4, 3>", "bf16") == "fp32"
+    assert bench.PEAK_TFLOPS[bench.kernel_arith("conv_gemm_kernel<1>", "bf16x3")] == pytest.approx(2500.0 / 3)
+    fl = (4e9 * 36 + 2e10 + 1e12) / (2 * 1920)
+    assert r["plan_gflop_per_frame"] == pytest.approx(fl / 1e9, rel=1e-3)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cpu")
+        B, T, HOP = 3, 4, 5
+        all_lens = dp.all_gather_lengths([T] * B, dev)
+        wav = torch.full((B, T * HOP), float(rank + 1))
+        mel = torch.full((B, T, 2), float(10 * (rank + 1)))
+        got = {}
+
+        def step():
+            time.sleep(0.05 * (rank + 1))  # the slower rank sets the step time
+            got["wav"] = dp.gather_results(wav, all_lens, per_step=HOP)
+            got["mel"] = dp.gather_results(mel, all_lens, per_step=1)
+
+        el = bench.timed_loop(step, 3, world, lambda: None, dev)
+        ok = el >= 3 * 0.05 * world - 1e-3
+        if rank == 0:
+            ok &= all(bool((got["wav"][r] == r + 1).all()) and got["wav"][r].shape == (B, T * HOP) for r in range(world))
+            ok &= all(bool((got["mel"][r] == 10 * (r + 1)).all()) and got["mel"][r].shape == (B, T, 2) for r in range(world))
+        q.put((rank, ok, el))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_timed_loop_and_gather_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(2))
+    assert all(ok for _, ok, _ in res), res
+    assert res[0][2] == res[1][2]  # every rank reports the same (max) time

@@ -32,7 +32,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, n_clips):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -44,15 +44,15 @@ def _worker(rank, world, port, q):
         ok1 = np.array_equal(got["a.weight"], np.zeros((3, 4), np.float32)) and \
             np.array_equal(got["b"], np.arange(5, dtype=np.float32)) and int(got["n"]) == rank
         # shard a ragged clip list, C3 lengths, C2 gather of per-clip "wav" (T * 3 samples)
-        lens = [5, 9, 2, 7, 7, 1, 4]
+        lens = [5, 9, 2, 7, 7, 1, 4][:n_clips]
         mine = dp.shard_clips(lens, world)[rank]
         my_lens = [lens[i] for i in mine]
         all_lens = dp.all_gather_lengths(my_lens, dev)
-        tmax = max(my_lens) if my_lens else 1
+        tmax = max(my_lens) if my_lens else 0
         wav = torch.zeros(len(mine), tmax * 3)
         for j, i in enumerate(mine):
             wav[j, : lens[i] * 3] = float(i + 1)
-        res = dp.gather_results(wav, all_lens)
+        res = dp.gather_results(wav, all_lens, per_step=3)
         if rank == 0:
             shards = dp.shard_clips(lens, world)
             ok2 = True
@@ -66,12 +66,13 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_dp_collectives_gloo(world):
+@pytest.mark.parametrize("world,n_clips", [(2, 7), (4, 7), (4, 3)])
+def test_dp_collectives_gloo(world, n_clips):
+    """world 4 with 3 clips: one rank has an empty shard and still joins every collective."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, n_clips)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
