@@ -18,6 +18,11 @@
 //            dwords (no unpacking), SiLU, one v_cvt_pk_bf16_f32 per channel pair, 16-byte stores.
 //   squeeze: per-lane channel sums -> fixed xor-shuffle tree within each wave -> per-wave partials
 //            in LDS -> the image's waves added in order -> SE mean (deterministic).
+// Split fp32 (SP = 1, m2s_common.hpp sp_t): phase 1 loads hi and lo fragments of the weights and the
+// input and runs three MFMA terms per product; the LDS tile holds the fp32 expanded activation
+// (36-float rows) and phase 2 is an fp32 depthwise with fp32 taps, writing hi/lo pairs.  The fp32
+// tile is twice the bf16 one, so SP bounds the haloed rows per workgroup at 324 (one 16x16 image,
+// two 8x8 images): 47 KB, three workgroups per CU.
 #include <type_traits>
 
 #include "conv_igemm.hpp"
@@ -27,25 +32,15 @@
 namespace m2s {
 namespace {
 
-#ifndef IRF_SL
-#define IRF_SL 32
-#endif
-#ifndef IRF_OCC
-#define IRF_OCC 2  // workgroups per CU for IRF_SL != 32 (microbenchmark builds)
-#endif
-constexpr int SL = IRF_SL;         // expanded channels per slice
-#ifndef IRF_MROW
-#define IRF_MROW (SL + 8)
-#endif
-constexpr int MROW = IRF_MROW;  // LDS row stride in bf16 (80 B)
+constexpr int SL = 32;         // expanded channels per slice
+constexpr int MROW = SL + 8;   // bf16 LDS row stride in bf16 (80 B)
+constexpr int MROWF = SL + 4;  // fp32 (SP) LDS row stride in floats (144 B)
 constexpr int NT = SL / 16;    // 16-channel MFMA subtiles
 constexpr int CG = SL / 8;     // phase-2 channel groups (8 channels = one 16-byte vector)
 constexpr int PL = 256 / CG;   // phase-2 pixel lanes (64; 16 per wave)
 constexpr int ROWS_MAX = 400;  // haloed pixel rows per workgroup (4 x 10x10, 1 x 18x18)
+constexpr int ROWS_MAX_SP = 324;  // SP: fp32 rows (1 x 18x18, 2 x 10x10)
 constexpr int POS_MAX = 256;   // positions per workgroup
-#ifndef IRF_MODE
-#define IRF_MODE 0
-#endif
 // One slice per workgroup: a slice loop per workgroup (more reuse of the input) measured slower,
 // occupancy 4 -> 2.
 
@@ -56,7 +51,9 @@ __device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float acc) {
 
 // S = depthwise stride.  OH x OW is the conv_pw (input) map; with S = 2 the depthwise writes the
 // SOH x SOW map, TF-SAME with top / left pads pad_t / pad_l (the stride-2 blocks.5.0 at 16x16).
-template <int MT, int G, int S>
+// SP = 1: x, wpw (rows [hi kp | lo kp]), y and se_mean are split fp32; wdw2 is then the fp32
+// tap-major [9][cs_mid] depthwise weight.
+template <int MT, int G, int S, int SP>
 __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int cs_in, int kp,
                                                          const bf16_t* __restrict__ wpw, const float* __restrict__ bpw,
                                                          const uint32_t* __restrict__ wdw2,
@@ -64,11 +61,16 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
                                                          int cs_mid, bf16_t* __restrict__ y,
                                                          bf16_t* __restrict__ se_mean, int SOH, int SOW, int pad_t,
                                                          int pad_l) {
-  __shared__ __attribute__((aligned(16))) bf16_t tile[ROWS_MAX * MROW];
+  constexpr int TILE_BYTES = SP ? ROWS_MAX_SP * MROWF * 4 : ROWS_MAX * MROW * 2;
+  __shared__ __attribute__((aligned(16))) char tile_raw[TILE_BYTES];
+  bf16_t* tile = reinterpret_cast<bf16_t*>(tile_raw);
+  float* tilef = reinterpret_cast<float*>(tile_raw);
   __shared__ uint16_t lut[POS_MAX];
   __shared__ float red[4][SL];
-  __shared__ uint4 wdw_lds[9][SL / 4];  // this slice's depthwise taps (bf16 in their dword halves)
+  // this slice's depthwise taps: bf16 in their dword halves, or (SP) fp32
+  __shared__ uint4 wdw_lds[9][SL / 4];
   __shared__ float4 bdw_lds[SL / 4];
+  constexpr int R = SP ? 2 : 1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g16 = lane >> 4, r16 = lane & 15;
   const int P = OH * OW, WR = OW + 2, IR = (OH + 2) * WR;
@@ -86,7 +88,13 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
   // more than the whole depthwise
   if (tid < 9 * (SL / 4)) {
     const int t = tid / (SL / 4), k = tid - t * (SL / 4), c = sl * SL + 4 * k;
-    wdw_lds[t][k] = c < cs_mid ? *reinterpret_cast<const uint4*>(wdw2 + (size_t)t * cs_mid + c) : make_uint4(0, 0, 0, 0);
+    if constexpr (SP) {  // 8 fp32 taps per uint4 pair: k covers channels 4k..4k+3
+      const float* wf = reinterpret_cast<const float*>(wdw2);
+      reinterpret_cast<float4*>(&wdw_lds[t][0])[k] =
+          c < cs_mid ? *reinterpret_cast<const float4*>(wf + (size_t)t * cs_mid + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      wdw_lds[t][k] = c < cs_mid ? *reinterpret_cast<const uint4*>(wdw2 + (size_t)t * cs_mid + c) : make_uint4(0, 0, 0, 0);
+    }
     if (t == 0) bdw_lds[k] = c < cs_mid ? *reinterpret_cast<const float4*>(bdw + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
@@ -96,18 +104,18 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
     lut[tid] = (uint16_t)(g * IR + (oy + 1) * WR + ox + 1);
   }
   {
-    uint4* t4 = reinterpret_cast<uint4*>(tile);
-    if (!(IRF_MODE & 64))
-      for (int i = tid; i < G * IR * (MROW / 8); i += 256) t4[i] = make_uint4(0, 0, 0, 0);
+    uint4* t4 = reinterpret_cast<uint4*>(tile_raw);
+    const int n16 = SP ? G * IR * (MROWF / 4) : G * IR * (MROW / 8);
+    for (int i = tid; i < n16; i += 256) t4[i] = make_uint4(0, 0, 0, 0);
   }
 
-  const bf16_t* xi = x + (size_t)n0 * P * cs_in;
+  const bf16_t* xi = x + (size_t)n0 * P * cs_in * R;
   const int mw = wave * MT * 16;
   const int cg = tid % CG, pl = tid / CG;
   const int lpi = PL / G, g = pl / lpi, q = pl - g * lpi;  // phase-2 image and lane within it
   int off[9];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) off[t] = ((t / 3 - 1) * WR + (t % 3 - 1)) * MROW;
+  for (int t = 0; t < 9; ++t) off[t] = ((t / 3 - 1) * WR + (t % 3 - 1)) * (SP ? MROWF : MROW);
 
   {
     const int c0 = sl * SL;
@@ -118,25 +126,40 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi) acc[ni][mi] = f32x4{0.f, 0.f, 0.f, 0.f};
     uint4 fa[2][NT], fb[2][MT];
+    uint4 fal[2][SP ? NT : 1], fbl[2][SP ? MT : 1];  // SP: lo halves
     auto load = [&](int buf, int k0) {
 #pragma unroll
-      for (int ni = 0; ni < NT; ++ni)
-        fa[buf][ni] = *reinterpret_cast<const uint4*>(wpw + (size_t)(c0 + ni * 16 + r16) * kp + k0 + 8 * g16);
+      for (int ni = 0; ni < NT; ++ni) {
+        const bf16_t* w = wpw + (size_t)(c0 + ni * 16 + r16) * kp * R + k0 + 8 * g16;
+        fa[buf][ni] = *reinterpret_cast<const uint4*>(w);
+        if constexpr (SP) fal[buf][ni] = *reinterpret_cast<const uint4*>(w + kp);
+      }
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi) {
         const int m = mw + mi * 16 + r16, k = k0 + 8 * g16;
-        fb[buf][mi] = (m < MP && k < cs_in) ? *reinterpret_cast<const uint4*>(xi + (size_t)m * cs_in + k)
-                                            : make_uint4(0, 0, 0, 0);
+        const bool ok = m < MP && k < cs_in;
+        const bf16_t* xp = xi + (size_t)m * cs_in * R + k;
+        fb[buf][mi] = ok ? *reinterpret_cast<const uint4*>(xp) : make_uint4(0, 0, 0, 0);
+        if constexpr (SP) fbl[buf][mi] = ok ? *reinterpret_cast<const uint4*>(xp + cs_in) : make_uint4(0, 0, 0, 0);
       }
     };
     auto mma = [&](int buf) {
 #pragma unroll
       for (int ni = 0; ni < NT; ++ni)
 #pragma unroll
-        for (int mi = 0; mi < MT; ++mi)
+        for (int mi = 0; mi < MT; ++mi) {
+          if constexpr (SP) {
+            acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fal[buf][ni]),
+                                                                  __builtin_bit_cast(bf16x8, fb[buf][mi]), acc[ni][mi],
+                                                                  0, 0, 0);
+            acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[buf][ni]),
+                                                                  __builtin_bit_cast(bf16x8, fbl[buf][mi]), acc[ni][mi],
+                                                                  0, 0, 0);
+          }
           acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[buf][ni]),
                                                                 __builtin_bit_cast(bf16x8, fb[buf][mi]), acc[ni][mi],
                                                                 0, 0, 0);
+        }
     };
     // the K loop fully unrolled for the block widths of the backbone (kp = cs_in = 128 / 224): loads
     // from clamped addresses (no exec-masked branch; positions past MP feed only discarded output
@@ -144,11 +167,17 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
     // generic loop below made every k-step wait for its own loads (conditional loads end in vmcnt(0)).
     auto load_u = [&](int buf, int k0) {
 #pragma unroll
-      for (int ni = 0; ni < NT; ++ni)
-        fa[buf][ni] = *reinterpret_cast<const uint4*>(wpw + (size_t)(c0 + ni * 16 + r16) * kp + k0 + 8 * g16);
+      for (int ni = 0; ni < NT; ++ni) {
+        const bf16_t* w = wpw + (size_t)(c0 + ni * 16 + r16) * kp * R + k0 + 8 * g16;
+        fa[buf][ni] = *reinterpret_cast<const uint4*>(w);
+        if constexpr (SP) fal[buf][ni] = *reinterpret_cast<const uint4*>(w + kp);
+      }
 #pragma unroll
-      for (int mi = 0; mi < MT; ++mi)
-        fb[buf][mi] = *reinterpret_cast<const uint4*>(xi + (size_t)min(mw + mi * 16 + r16, MP - 1) * cs_in + k0 + 8 * g16);
+      for (int mi = 0; mi < MT; ++mi) {
+        const bf16_t* xp = xi + (size_t)min(mw + mi * 16 + r16, MP - 1) * cs_in * R + k0 + 8 * g16;
+        fb[buf][mi] = *reinterpret_cast<const uint4*>(xp);
+        if constexpr (SP) fbl[buf][mi] = *reinterpret_cast<const uint4*>(xp + cs_in);
+      }
     };
     auto unrolled = [&](auto ksn_c) {
       constexpr int KSN = decltype(ksn_c)::value;
@@ -161,8 +190,7 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
         __builtin_amdgcn_sched_barrier(0);
       }
     };
-    if (IRF_MODE & 1) {  // IRF_MODE: microbenchmark variants (tools/irf_bench.hip); 0 in the library
-    } else if (kp == 128 && cs_in == 128) {
+    if (kp == 128 && cs_in == 128) {
       unrolled(std::integral_constant<int, 4>());
     } else if (kp == 224 && cs_in == 224) {
       unrolled(std::integral_constant<int, 7>());
@@ -186,6 +214,12 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
       for (int mi = 0; mi < MT; ++mi) {
         const int m = mw + mi * 16 + r16;
         if (m >= MP) continue;
+        if constexpr (SP) {
+          *reinterpret_cast<float4*>(tilef + lut[m] * MROWF + cl) =
+              make_float4(silu(acc[ni][mi][0] + bb.x), silu(acc[ni][mi][1] + bb.y), silu(acc[ni][mi][2] + bb.z),
+                          silu(acc[ni][mi][3] + bb.w));
+          continue;
+        }
         uint2 u;
         u.x = pack_bf16x2(silu(acc[ni][mi][0] + bb.x), silu(acc[ni][mi][1] + bb.y));
         u.y = pack_bf16x2(silu(acc[ni][mi][2] + bb.z), silu(acc[ni][mi][3] + bb.w));
@@ -197,7 +231,48 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
     // ---- phase 2: depthwise 3x3 (stride 1, pad 1) from the haloed tile ------------------------
     const int c = c0 + cg * 8;
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (g < gi && c < cs_mid && !(IRF_MODE & 2)) {
+    if (SP && g < gi && c < cs_mid) {
+      float w[9][8], b[8];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const float4 lo = reinterpret_cast<const float4*>(&wdw_lds[t][0])[2 * cg];
+        const float4 hi = reinterpret_cast<const float4*>(&wdw_lds[t][0])[2 * cg + 1];
+        w[t][0] = lo.x; w[t][1] = lo.y; w[t][2] = lo.z; w[t][3] = lo.w;
+        w[t][4] = hi.x; w[t][5] = hi.y; w[t][6] = hi.z; w[t][7] = hi.w;
+      }
+      {
+        const float4 lo = bdw_lds[2 * cg], hi = bdw_lds[2 * cg + 1];
+        b[0] = lo.x; b[1] = lo.y; b[2] = lo.z; b[3] = lo.w;
+        b[4] = hi.x; b[5] = hi.y; b[6] = hi.z; b[7] = hi.w;
+      }
+      sp_t* ys = reinterpret_cast<sp_t*>(y);
+      for (int p = q; p < PO; p += lpi) {
+        int trow;
+        if constexpr (S == 1) {
+          trow = lut[g * P + p];
+        } else {
+          const int oy = p / SOW, ox = p - (p / SOW) * SOW;
+          trow = g * IR + (S * oy - pad_t + 2) * WR + S * ox - pad_l + 2;
+        }
+        const float* base = tilef + trow * MROWF + cg * 8;
+        float a[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = b[j];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const float4 u0 = *reinterpret_cast<const float4*>(base + off[t]);
+          const float4 u1 = *reinterpret_cast<const float4*>(base + off[t] + 4);
+          a[0] += w[t][0] * u0.x; a[1] += w[t][1] * u0.y; a[2] += w[t][2] * u0.z; a[3] += w[t][3] * u0.w;
+          a[4] += w[t][4] * u1.x; a[5] += w[t][5] * u1.y; a[6] += w[t][6] * u1.z; a[7] += w[t][7] * u1.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          a[j] = silu(a[j]);
+          s[j] += a[j];
+        }
+        act_st8<sp_t>(ys, (long)(n0 + g) * PO + p, cs_mid, c, a);
+      }
+    } else if (!SP && g < gi && c < cs_mid) {
       uint32_t w[9][8];
       float b[8];
 #pragma unroll
@@ -223,8 +298,7 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
         const bf16_t* base = tile + trow * MROW + cg * 8;
         uint4 in[9];
 #pragma unroll
-        for (int t = 0; t < 9; ++t)
-          in[t] = (IRF_MODE & 16) && t ? in[0] : *reinterpret_cast<const uint4*>(base + off[t]);
+        for (int t = 0; t < 9; ++t) in[t] = *reinterpret_cast<const uint4*>(base + off[t]);
         float a[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) a[j] = b[j];
@@ -233,25 +307,21 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
           const uint32_t u[4] = {in[t].x, in[t].y, in[t].z, in[t].w};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            if (IRF_MODE & 8) {  // microbenchmark: one plain add per channel pair instead of 2 dot2
-              a[2 * j] += __uint_as_float(u[j] ^ w[t][2 * j]);
-            } else {
-              a[2 * j] = dot2(u[j], w[t][2 * j], a[2 * j]);
-              a[2 * j + 1] = dot2(u[j], w[t][2 * j + 1], a[2 * j + 1]);
-            }
+            a[2 * j] = dot2(u[j], w[t][2 * j], a[2 * j]);
+            a[2 * j + 1] = dot2(u[j], w[t][2 * j + 1], a[2 * j + 1]);
           }
         }
         uint4 o;
         uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float v0 = (IRF_MODE & 32) ? a[2 * j] : silu(a[2 * j]);
-          const float v1 = (IRF_MODE & 32) ? a[2 * j + 1] : silu(a[2 * j + 1]);
+          const float v0 = silu(a[2 * j]);
+          const float v1 = silu(a[2 * j + 1]);
           s[2 * j] += v0;
           s[2 * j + 1] += v1;
           ow[j] = pack_bf16x2(v0, v1);
         }
-        if (!(IRF_MODE & 4) || o.x == 0x7fc17fc1u) *reinterpret_cast<uint4*>(yi + (size_t)p * cs_mid) = o;
+        *reinterpret_cast<uint4*>(yi + (size_t)p * cs_mid) = o;
       }
     }
     // ---- squeeze: the wave's 16 pixel lanes (lane / CG) share cg = lane % CG; one image per wave
@@ -269,81 +339,104 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
       if (gg < gi && c0 + cl < cs_mid) {
         float t = 0.f;
         for (int wv = gg * wpi; wv < (gg + 1) * wpi; ++wv) t += red[wv][cl];
-        se_mean[(size_t)(n0 + gg) * cs_mid + c0 + cl] = f2bf(t / (float)PO);
+        if constexpr (SP)
+          act_st<sp_t>(reinterpret_cast<sp_t*>(se_mean), n0 + gg, cs_mid, c0 + cl, t / (float)PO);
+        else
+          se_mean[(size_t)(n0 + gg) * cs_mid + c0 + cl] = f2bf(t / (float)PO);
       }
     }
   }
 }
 
-template <int MT, int G>
-__global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : IRF_OCC))
+template <int MT, int G, int SP>
+__global__ void __launch_bounds__(256, SP ? 3 : 4)
     ir_pwdw_kernel(const bf16_t* __restrict__ x, int cs_in, int kp, const bf16_t* __restrict__ wpw,
                    const float* __restrict__ bpw, const uint32_t* __restrict__ wdw2, const float* __restrict__ bdw, int N,
                    int OH, int OW, int cs_mid, bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean) {
-  ir_pwdw_body<MT, G, 1>(x, cs_in, kp, wpw, bpw, wdw2, bdw, N, OH, OW, cs_mid, y, se_mean, OH, OW, 1, 1);
+  ir_pwdw_body<MT, G, 1, SP>(x, cs_in, kp, wpw, bpw, wdw2, bdw, N, OH, OW, cs_mid, y, se_mean, OH, OW, 1, 1);
 }
 
-__global__ void __launch_bounds__(256, (IRF_SL == 32 ? 4 : IRF_OCC))
+template <int SP>
+__global__ void __launch_bounds__(256, SP ? 3 : 4)
     ir_pwdw_s2_kernel(const bf16_t* __restrict__ x, int cs_in, int kp, const bf16_t* __restrict__ wpw,
                       const float* __restrict__ bpw, const uint32_t* __restrict__ wdw2, const float* __restrict__ bdw,
                       int N, int IH, int IW, int cs_mid, bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, int OH,
                       int OW, int pad_t, int pad_l) {
-  ir_pwdw_body<4, 1, 2>(x, cs_in, kp, wpw, bpw, wdw2, bdw, N, IH, IW, cs_mid, y, se_mean, OH, OW, pad_t, pad_l);
+  ir_pwdw_body<4, 1, 2, SP>(x, cs_in, kp, wpw, bpw, wdw2, bdw, N, IH, IW, cs_mid, y, se_mean, OH, OW, pad_t, pad_l);
 }
 
-int ir_group(int OH, int OW) {
+int ir_group(int OH, int OW, bool sp) {
   const int P = OH * OW, rows = (OH + 2) * (OW + 2);
   for (int G = 4; G >= 1; G /= 2)
-    if (G * P <= POS_MAX && G * rows <= ROWS_MAX) return G;
+    if (G * P <= POS_MAX && G * rows <= (sp ? ROWS_MAX_SP : ROWS_MAX)) return G;
   return 0;
 }
 
 }  // namespace
 
-bool ir_fused_supported(int OH, int OW, int cs_in, int cs_mid) {
+bool ir_fused_supported(int OH, int OW, int cs_in, int cs_mid, bool split) {
   (void)cs_in;
-  return ir_group(OH, OW) > 0 && cs_mid % 8 == 0;
+  return ir_group(OH, OW, split) > 0 && cs_mid % 8 == 0;
 }
 
-void launch_ir_pwdw(const bf16_t* x, int N, int cs_in, int kp, const bf16_t* wpw, const float* bpw,
-                    const uint32_t* wdw2, const float* bdw, int OH, int OW, int cs_mid, bf16_t* y, bf16_t* se_mean,
-                    double flops, double bytes, hipStream_t s) {
-  M2S_CHECK(ir_fused_supported(OH, OW, cs_in, cs_mid), "ir_pwdw: unsupported shape");
+void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, const float* bpw, const void* wdw,
+                    const float* bdw, int OH, int OW, int cs_mid, void* y, void* se_mean, bool split, double flops,
+                    double bytes, hipStream_t s) {
+  M2S_CHECK(ir_fused_supported(OH, OW, cs_in, cs_mid, split), "ir_pwdw: unsupported shape");
   M2S_CHECK(kp % 32 == 0 && kp >= cs_in, "ir_pwdw: kp");
-  const int G = ir_group(OH, OW), pos = G * OH * OW;
+  const int G = ir_group(OH, OW, split), pos = G * OH * OW;
   const dim3 grid(ceil_div(cs_mid, SL) * ceil_div(N, G));
+  const bf16_t* xb = static_cast<const bf16_t*>(x);
+  const bf16_t* wb = static_cast<const bf16_t*>(wpw);
+  const uint32_t* wd = static_cast<const uint32_t*>(wdw);
+  bf16_t* yb = static_cast<bf16_t*>(y);
+  bf16_t* mb = static_cast<bf16_t*>(se_mean);
   // MT = 16-position subtiles per wave (pos <= 64 * MT); G = images per workgroup.  Each pair is
   // its own symbol, so rocprofv3 and the event profiler see the same kernel.
-#define M2S_IRF(MT_, G_)                                                                                 \
-  if (pos <= 64 * MT_ && G == G_) {                                                                      \
-    ProfScope ps("ir_pwdw_kernel<" #MT_ ", " #G_ ">", flops, bytes, s);                                 \
-    hipLaunchKernelGGL((ir_pwdw_kernel<MT_, G_>), grid, dim3(256), 0, s, x, cs_in, kp, wpw, bpw, wdw2, bdw, N, OH, OW, \
-                       cs_mid, y, se_mean);                                                              \
+#define M2S_IRF(MT_, G_, SP_)                                                                            \
+  if (pos <= 64 * MT_ && G == G_ && (int)split == SP_) {                                                 \
+    ProfScope ps("ir_pwdw_kernel<" #MT_ ", " #G_ ", " #SP_ ">", flops, bytes, s);                       \
+    hipLaunchKernelGGL((ir_pwdw_kernel<MT_, G_, SP_>), grid, dim3(256), 0, s, xb, cs_in, kp, wb, bpw, wd, bdw, N, OH, \
+                       OW, cs_mid, yb, mb);                                                              \
     M2S_HIP(hipGetLastError());                                                                          \
     return;                                                                                              \
   }
-  M2S_IRF(1, 1) M2S_IRF(1, 2) M2S_IRF(1, 4)
-  M2S_IRF(2, 1) M2S_IRF(2, 2) M2S_IRF(2, 4)
-  M2S_IRF(4, 1) M2S_IRF(4, 2) M2S_IRF(4, 4)
+  M2S_IRF(1, 1, 0) M2S_IRF(1, 2, 0) M2S_IRF(1, 4, 0)
+  M2S_IRF(2, 1, 0) M2S_IRF(2, 2, 0) M2S_IRF(2, 4, 0)
+  M2S_IRF(4, 1, 0) M2S_IRF(4, 2, 0) M2S_IRF(4, 4, 0)
+  M2S_IRF(1, 1, 1) M2S_IRF(1, 2, 1) M2S_IRF(1, 4, 1)
+  M2S_IRF(2, 1, 1) M2S_IRF(2, 2, 1) M2S_IRF(2, 4, 1)
+  M2S_IRF(4, 1, 1) M2S_IRF(4, 2, 1) M2S_IRF(4, 4, 1)
 #undef M2S_IRF
   M2S_CHECK(false, "ir_pwdw: no variant for this shape");
 }
 
-bool ir_fused_s2_supported(int IH, int IW, int cs_in, int cs_mid) {
-  return IH * IW <= 256 && IH * IW > 192 && (IH + 2) * (IW + 2) <= ROWS_MAX && cs_mid % 8 == 0 && cs_in > 0;
+bool ir_fused_s2_supported(int IH, int IW, int cs_in, int cs_mid, bool split) {
+  return IH * IW <= 256 && IH * IW > 192 && (IH + 2) * (IW + 2) <= (split ? ROWS_MAX_SP : ROWS_MAX) &&
+         cs_mid % 8 == 0 && cs_in > 0;
 }
 
-void launch_ir_pwdw_s2(const bf16_t* x, int N, int cs_in, int kp, const bf16_t* wpw, const float* bpw,
-                       const uint32_t* wdw2, const float* bdw, int IH, int IW, int OH, int OW, int pad_t, int pad_l,
-                       int cs_mid, bf16_t* y, bf16_t* se_mean, double flops, double bytes, hipStream_t s) {
-  M2S_CHECK(ir_fused_s2_supported(IH, IW, cs_in, cs_mid) && kp % 32 == 0 && kp >= cs_in, "ir_pwdw_s2: unsupported shape");
+void launch_ir_pwdw_s2(const void* x, int N, int cs_in, int kp, const void* wpw, const float* bpw, const void* wdw,
+                       const float* bdw, int IH, int IW, int OH, int OW, int pad_t, int pad_l, int cs_mid, void* y,
+                       void* se_mean, bool split, double flops, double bytes, hipStream_t s) {
+  M2S_CHECK(ir_fused_s2_supported(IH, IW, cs_in, cs_mid, split) && kp % 32 == 0 && kp >= cs_in,
+            "ir_pwdw_s2: unsupported shape");
   M2S_CHECK(OH == (IH + 1) / 2 && OW == (IW + 1) / 2 && OH * OW <= 64 && pad_t >= 0 && pad_t <= 1 && pad_l >= 0 &&
                 pad_l <= 1,
             "ir_pwdw_s2: geometry");
   const dim3 grid(ceil_div(cs_mid, SL) * N);
-  ProfScope ps("ir_pwdw_s2_kernel", flops, bytes, s);
-  hipLaunchKernelGGL(ir_pwdw_s2_kernel, grid, dim3(256), 0, s, x, cs_in, kp, wpw, bpw, wdw2, bdw, N, IH, IW, cs_mid, y,
-                     se_mean, OH, OW, pad_t, pad_l);
+  const bf16_t* xb = static_cast<const bf16_t*>(x);
+  const bf16_t* wb = static_cast<const bf16_t*>(wpw);
+  const uint32_t* wd = static_cast<const uint32_t*>(wdw);
+  if (split) {
+    ProfScope ps("ir_pwdw_s2_kernel<1>", flops, bytes, s);
+    hipLaunchKernelGGL(ir_pwdw_s2_kernel<1>, grid, dim3(256), 0, s, xb, cs_in, kp, wb, bpw, wd, bdw, N, IH, IW, cs_mid,
+                       static_cast<bf16_t*>(y), static_cast<bf16_t*>(se_mean), OH, OW, pad_t, pad_l);
+  } else {
+    ProfScope ps("ir_pwdw_s2_kernel<0>", flops, bytes, s);
+    hipLaunchKernelGGL(ir_pwdw_s2_kernel<0>, grid, dim3(256), 0, s, xb, cs_in, kp, wb, bpw, wd, bdw, N, IH, IW, cs_mid,
+                       static_cast<bf16_t*>(y), static_cast<bf16_t*>(se_mean), OH, OW, pad_t, pad_l);
+  }
   M2S_HIP(hipGetLastError());
 }
 

@@ -24,21 +24,23 @@ void launch_dwconv(const T* x, int N, int IH, int IW, int OH, int OW, int stride
 template <typename T>
 void launch_se_mean(const float* psum, int N, int npb, int cs, float inv_count, T* mean, hipStream_t s);
 
-// bf16 fused conv_pw + bn1 + SiLU + conv_dw (stride 1) + bn2 + SiLU + SE squeeze for maps whose
-// haloed tile fits a workgroup ((OH+2)(OW+2) <= 400, OH*OW <= 256): x (N,P,cs_in) -> y
-// (N,P,cs_mid), se_mean (N,cs_mid).  wpw packed [>=ceil64(cs_mid)][kp], bpw likewise padded;
-// wdw2 tap-major [9][cs_mid] bf16 weights in the dword half of their channel.  (ir_fused.hip)
-bool ir_fused_supported(int OH, int OW, int cs_in, int cs_mid);
-void launch_ir_pwdw(const bf16_t* x, int N, int cs_in, int kp, const bf16_t* wpw, const float* bpw,
-                    const uint32_t* wdw2, const float* bdw, int OH, int OW, int cs_mid, bf16_t* y, bf16_t* se_mean,
-                    double flops, double bytes, hipStream_t s);
+// Fused conv_pw + bn1 + SiLU + conv_dw (stride 1) + bn2 + SiLU + SE squeeze for maps whose
+// haloed tile fits a workgroup ((OH+2)(OW+2) <= 400 bf16 / 324 split, OH*OW <= 256): x (N,P,cs_in) ->
+// y (N,P,cs_mid), se_mean (N,cs_mid).  wpw packed [>=ceil64(cs_mid)][kp], bpw likewise padded.
+// bf16: x/y/se_mean bf16, wdw = tap-major [9][cs_mid] bf16 weights in the dword half of their channel
+// (uint32).  split (bf16x3): x/y/se_mean sp_t, wpw rows [hi kp | lo kp], wdw = fp32 [9][cs_mid].
+// (ir_fused.hip)
+bool ir_fused_supported(int OH, int OW, int cs_in, int cs_mid, bool split);
+void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, const float* bpw, const void* wdw,
+                    const float* bdw, int OH, int OW, int cs_mid, void* y, void* se_mean, bool split, double flops,
+                    double bytes, hipStream_t s);
 
 // The same for a stride-2 depthwise (TF-SAME, top / left pads pad_t / pad_l) on an IH x IW <= 256-pixel
 // conv_pw map: y (N, OH*OW, cs_mid), se_mean over the OH x OW output.  (ir_fused.hip)
-bool ir_fused_s2_supported(int IH, int IW, int cs_in, int cs_mid);
-void launch_ir_pwdw_s2(const bf16_t* x, int N, int cs_in, int kp, const bf16_t* wpw, const float* bpw,
-                       const uint32_t* wdw2, const float* bdw, int IH, int IW, int OH, int OW, int pad_t, int pad_l,
-                       int cs_mid, bf16_t* y, bf16_t* se_mean, double flops, double bytes, hipStream_t s);
+bool ir_fused_s2_supported(int IH, int IW, int cs_in, int cs_mid, bool split);
+void launch_ir_pwdw_s2(const void* x, int N, int cs_in, int kp, const void* wpw, const float* bpw, const void* wdw,
+                       const float* bdw, int IH, int IW, int OH, int OW, int pad_t, int pad_l, int cs_mid, void* y,
+                       void* se_mean, bool split, double flops, double bytes, hipStream_t s);
 
 // bf16 fused HiFi-GAN ResBlock1 (all (c1, c2) pairs of one resblock + the MRF running sum) for C in
 // {32, 64}: x (B, L, C) -> S (B, L, C) with S = x' (accum 0), S += x' (1), S = (S + x') / div (2).

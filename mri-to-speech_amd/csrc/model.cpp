@@ -674,22 +674,21 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                         s);
       } else {
         const int cs = chan_stride(b.mid);
-        if (std::is_same<T, bf16_t>::value && b.stride == 1 && ir_fused_ &&
-            ir_fused_supported(nh, nw, b.c1.cs_in, cs)) {
-          const double P = (double)nh * nw;
-          launch_ir_pwdw(reinterpret_cast<const bf16_t*>(cur), nc, b.c1.cs_in, b.c1.kp,
-                         static_cast<const bf16_t*>(b.c1.w), b.c1.b,
-                         static_cast<const uint32_t*>(arena_.ptr(b.dw_w2)), static_cast<const float*>(arena_.ptr(b.dw_b)),
-                         nh, nw, cs, reinterpret_cast<bf16_t*>(M2), reinterpret_cast<bf16_t*>(se_mean),
-                         2.0 * nc * P * b.mid * (b.c1.cin + 9), 2.0 * nc * P * (b.c1.cs_in + cs), s);
-        } else if (std::is_same<T, bf16_t>::value && b.stride == 2 && ir_fused_ &&
-                   ir_fused_s2_supported(oh, ow, b.c1.cs_in, cs) && nh * nw <= 64) {
-          const double Pi = (double)oh * ow, Po = (double)nh * nw;
-          launch_ir_pwdw_s2(reinterpret_cast<const bf16_t*>(cur), nc, b.c1.cs_in, b.c1.kp,
-                            static_cast<const bf16_t*>(b.c1.w), b.c1.b,
-                            static_cast<const uint32_t*>(arena_.ptr(b.dw_w2)), static_cast<const float*>(arena_.ptr(b.dw_b)),
-                            oh, ow, nh, nw, qt, ql, cs, reinterpret_cast<bf16_t*>(M2), reinterpret_cast<bf16_t*>(se_mean),
-                            2.0 * nc * b.mid * (Pi * b.c1.cin + Po * 9), 2.0 * nc * (Pi * b.c1.cs_in + Po * cs), s);
+        constexpr bool SPL = std::is_same<T, sp_t>::value;
+        constexpr bool FUSABLE = std::is_same<T, bf16_t>::value || SPL;
+        // bf16 feeds the fused kernel bf16 depthwise taps (dword halves), split fp32 the fp32 taps
+        const void* wdw = arena_.ptr(SPL ? b.dw_w : b.dw_w2);
+        if (FUSABLE && b.stride == 1 && ir_fused_ && ir_fused_supported(nh, nw, b.c1.cs_in, cs, SPL)) {
+          const double P = (double)nh * nw, es = SPL ? 4.0 : 2.0;
+          launch_ir_pwdw(cur, nc, b.c1.cs_in, b.c1.kp, b.c1.w, b.c1.b, wdw, static_cast<const float*>(arena_.ptr(b.dw_b)),
+                         nh, nw, cs, M2, se_mean, SPL, 2.0 * nc * P * b.mid * (b.c1.cin + 9),
+                         es * nc * P * (b.c1.cs_in + cs), s);
+        } else if (FUSABLE && b.stride == 2 && ir_fused_ && ir_fused_s2_supported(oh, ow, b.c1.cs_in, cs, SPL) &&
+                   nh * nw <= 64) {
+          const double Pi = (double)oh * ow, Po = (double)nh * nw, es = SPL ? 4.0 : 2.0;
+          launch_ir_pwdw_s2(cur, nc, b.c1.cs_in, b.c1.kp, b.c1.w, b.c1.b, wdw, static_cast<const float*>(arena_.ptr(b.dw_b)),
+                            oh, ow, nh, nw, qt, ql, cs, M2, se_mean, SPL, 2.0 * nc * b.mid * (Pi * b.c1.cin + Po * 9),
+                            es * nc * (Pi * b.c1.cs_in + Po * cs), s);
         } else {
         ConvArgs e = conv_args(b.c1);
         e.x = cur;
