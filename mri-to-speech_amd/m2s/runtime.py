@@ -1,4 +1,8 @@
-"""Device-side engines over libm2s (torch is used only for device memory and streams).
+"""Device-side engines over libm2s.
+
+The packed models are created and destroyed through the C ABI (ctypes, ``_native``); every compute
+call goes through the PyTorch-ROCm custom ops ``torch.ops.m2s.*`` (``ops``, csrc/torch_ops.cpp), which
+allocate outputs and workspace with the torch caching allocator on the current HIP stream.
 
 * ``AcousticEngine``  - packed CNN + BiLSTM + head (replaces OTNLikeCNNBiLSTM.forward,
                         mri2speech_code/mri_acoustic_model.py:116-136)
@@ -14,6 +18,7 @@ from typing import Dict, Optional
 import torch
 
 from . import _native as N
+from . import ops as _ops
 
 
 def _device(device) -> torch.device:
@@ -25,38 +30,21 @@ def _device(device) -> torch.device:
     return torch.device("cuda", d.index if d.index is not None else torch.cuda.current_device())
 
 
-def _ptr(t: Optional[torch.Tensor]):
-    return None if t is None else C.c_void_p(t.data_ptr())
-
-
-def _stream(device: torch.device):
-    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
-
-
 def _as_f32(t: torch.Tensor, device: torch.device) -> torch.Tensor:
     if t.device != device:
         raise N.M2SError(f"input on {t.device}, engine on {device}")
     return t.to(torch.float32).contiguous()
 
 
-class _WS:
-    """Grow-only device workspace owned by an engine (stream-ordered by torch's allocator)."""
-
-    def __init__(self, device):
-        self.device, self.buf = device, None
-
-    def get(self, nbytes: int) -> torch.Tensor:
-        if self.buf is None or self.buf.numel() < nbytes:
-            self.buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
-        return self.buf
-
-
 class AcousticEngine:
-    def __init__(self, state_dict: Dict, n_mels: int = 64, rnn_hidden: int = 640, dtype: str = "bf16",
+    def __init__(self, state_dict: Dict, n_mels: int = 64, rnn_hidden: int = 640, dtype: str = "bf16x3",
                  device=None, chunk: int = 256):
         self.device = _device(device)
         self.n_mels, self.rnn_hidden, self.dtype = n_mels, rnn_hidden, dtype
+        if dtype not in N.DTYPES:
+            raise N.M2SError(f"unknown dtype {dtype!r}; one of {sorted(N.DTYPES)}")
         L = N.lib()
+        self.ops = _ops.load()
         N.check(L.m2s_device_check(self.device.index))
         arr, keep = N.tensor_array(state_dict)
         h = C.c_void_p()
@@ -64,7 +52,6 @@ class AcousticEngine:
                                       C.byref(h)))
         del keep
         self._h = h
-        self._ws = _WS(self.device)
         N.check(L.m2s_acoustic_set_chunk(self._h, int(chunk)))
 
     def __del__(self):
@@ -74,11 +61,9 @@ class AcousticEngine:
             self._h = None
 
     @property
-    def handle(self):
-        return self._h
-
-    def workspace_bytes(self, B, T, H, W) -> int:
-        return int(N.lib().m2s_acoustic_workspace_bytes(self._h, B, T, H, W))
+    def handle(self) -> int:
+        """The m2s_acoustic* as the int the torch.ops.m2s ops take."""
+        return int(self._h.value)
 
     def forward(self, frames: torch.Tensor) -> torch.Tensor:
         """frames (B,T,1,H,W) or (B,T,H,W) fp32 -> normalised mel (B,T,n_mels) fp32."""
@@ -88,52 +73,29 @@ class AcousticEngine:
             frames = frames[:, :, 0]
         if frames.dim() != 4:
             raise N.M2SError(f"expected (B,T,H,W) frames, got {tuple(frames.shape)}")
-        x = _as_f32(frames, self.device)
-        B, T, H, W = x.shape
-        out = torch.empty(B, T, self.n_mels, dtype=torch.float32, device=self.device)
-        ws = self._ws.get(self.workspace_bytes(B, T, H, W))
-        N.check(N.lib().m2s_acoustic_forward(self._h, _ptr(x), B, T, H, W, _ptr(out), _ptr(ws), ws.numel(),
-                                             _stream(self.device)))
-        return out
+        return self.ops.acoustic_forward(self.handle, _as_f32(frames, self.device), self.n_mels)
 
     def effnet(self, frames: torch.Tensor) -> torch.Tensor:
         """frames (N,H,W) -> GAP features (N,208)."""
-        x = _as_f32(frames, self.device)
-        n, H, W = x.shape
-        out = torch.empty(n, 208, dtype=torch.float32, device=self.device)
-        ws = self._ws.get(self.workspace_bytes(n, 1, H, W))
-        N.check(N.lib().m2s_effnet_forward(self._h, _ptr(x), n, H, W, _ptr(out), _ptr(ws), ws.numel(),
-                                           _stream(self.device)))
-        return out
+        return self.ops.effnet_forward(self.handle, _as_f32(frames, self.device))
 
     def probe(self, frames: torch.Tensor, n_blocks: int) -> torch.Tensor:
         """Feature map after ``n_blocks`` timm blocks (0 = stem), (N,C,OH,OW) fp32."""
-        x = _as_f32(frames, self.device)
-        n, H, W = x.shape
-        out = torch.empty(n * ((H + 1) // 2) * ((W + 1) // 2) * 32, dtype=torch.float32, device=self.device)
-        ws = self._ws.get(self.workspace_bytes(n, 1, H, W))
-        oh, ow, oc = C.c_int(), C.c_int(), C.c_int()
-        N.check(N.lib().m2s_effnet_probe(self._h, _ptr(x), n, H, W, int(n_blocks), _ptr(out), C.byref(oh),
-                                         C.byref(ow), C.byref(oc), _ptr(ws), ws.numel(), _stream(self.device)))
-        return out[: n * oh.value * ow.value * oc.value].view(n, oh.value, ow.value, oc.value).permute(0, 3, 1, 2)
+        return self.ops.effnet_features(self.handle, _as_f32(frames, self.device), int(n_blocks))
 
     def bilstm(self, feats: torch.Tensor):
         """feats (B,T,208) -> (sum-merged BiLSTM output (B,T,H), head output (B,T,n_mels))."""
-        x = _as_f32(feats, self.device)
-        B, T, _ = x.shape
-        y = torch.empty(B, T, self.rnn_hidden, dtype=torch.float32, device=self.device)
-        m = torch.empty(B, T, self.n_mels, dtype=torch.float32, device=self.device)
-        ws = self._ws.get(self.workspace_bytes(B, T, 64, 64))
-        N.check(N.lib().m2s_bilstm_summerge(self._h, _ptr(x), B, T, _ptr(y), _ptr(m), _ptr(ws), ws.numel(),
-                                            _stream(self.device)))
-        return y, m
+        return self.ops.bilstm_summerge(self.handle, _as_f32(feats, self.device), self.rnn_hidden, self.n_mels)
 
 
 class VocoderEngine:
-    def __init__(self, state_dict: Dict, h, dtype: str = "bf16", device=None):
+    def __init__(self, state_dict: Dict, h, dtype: str = "bf16x3", device=None):
         self.device = _device(device)
         self.h, self.dtype = dict(h), dtype
+        if dtype not in N.DTYPES:
+            raise N.M2SError(f"unknown dtype {dtype!r}; one of {sorted(N.DTYPES)}")
         L = N.lib()
+        self.ops = _ops.load()
         N.check(L.m2s_device_check(self.device.index))
         arr, keep = N.tensor_array(state_dict)
         self._hh = N.hifigan_h(h)
@@ -142,7 +104,6 @@ class VocoderEngine:
                                      C.byref(v)))
         del keep
         self._h = v
-        self._ws = _WS(self.device)
         self.hop = 1
         for u in h["upsample_rates"]:
             self.hop *= int(u)
@@ -154,37 +115,25 @@ class VocoderEngine:
             self._h = None
 
     @property
-    def handle(self):
-        return self._h
+    def handle(self) -> int:
+        return int(self._h.value)
 
     def forward(self, mel: torch.Tensor, layout: int = 0) -> torch.Tensor:
         """mel (B,num_mels,T) [layout 0, as Generator.forward] or (B,T,num_mels) [layout 1] -> (B,1,T*hop)."""
         x = _as_f32(mel, self.device)
         if x.dim() != 3:
             raise N.M2SError(f"expected a 3-D mel, got {tuple(x.shape)}")
-        B = x.shape[0]
-        T = x.shape[2] if layout == 0 else x.shape[1]
         C_ = x.shape[1] if layout == 0 else x.shape[2]
         if C_ != self.h["num_mels"]:
             raise N.M2SError(f"mel has {C_} bins, generator expects {self.h['num_mels']}")
-        wav = torch.empty(B, 1, T * self.hop, dtype=torch.float32, device=self.device)
-        ws = self._ws.get(int(N.lib().m2s_vocoder_workspace_bytes(self._h, B, T)))
-        N.check(N.lib().m2s_vocoder_forward(self._h, _ptr(x), int(layout), B, T, _ptr(wav), _ptr(ws), ws.numel(),
-                                            _stream(self.device)))
-        return wav
+        return self.ops.hifigan_forward(self.handle, x, int(layout), self.hop)
 
 
 def mel_glue(mel_norm: torch.Tensor, mean: torch.Tensor, std: torch.Tensor):
     """(rows..., n_mels) -> (mel_db, mel_log), same shape."""
     d = mel_norm.device
-    x = mel_norm.to(torch.float32).contiguous()
-    n_mels = x.shape[-1]
-    rows = x.numel() // n_mels
-    mean = mean.to(device=d, dtype=torch.float32).contiguous()
-    std = std.to(device=d, dtype=torch.float32).contiguous()
-    db, ln = torch.empty_like(x), torch.empty_like(x)
-    N.check(N.lib().m2s_mel_glue(_ptr(x), rows, n_mels, _ptr(mean), _ptr(std), _ptr(db), _ptr(ln), _stream(d)))
-    return db, ln
+    return _ops.load().mel_glue(mel_norm.to(torch.float32).contiguous(), torch.as_tensor(mean).to(d),
+                                torch.as_tensor(std).to(d))
 
 
 def preprocess_frames(frames: torch.Tensor) -> torch.Tensor:
@@ -194,17 +143,9 @@ def preprocess_frames(frames: torch.Tensor) -> torch.Tensor:
         raise N.M2SError(f"expected uint8 frames, got {frames.dtype}")
     if frames.device.type != "cuda":
         raise N.M2SError("preprocess_frames runs on the HIP device; move the decoded frames there first")
-    x = frames.contiguous()
-    if x.dim() == 4 and x.shape[-1] == 3:
-        ch = 3
-    elif x.dim() == 3:
-        ch = 1
-    else:
-        raise N.M2SError(f"expected (T,H,W) or (T,H,W,3) frames, got {tuple(x.shape)}")
-    n, h, w = x.shape[:3]
-    out = torch.empty(n, h, w, dtype=torch.float32, device=x.device)
-    N.check(N.lib().m2s_preprocess_frames(_ptr(x), n, h, w, ch, _ptr(out), _stream(x.device)))
-    return out
+    if not (frames.dim() == 3 or (frames.dim() == 4 and frames.shape[-1] == 3)):
+        raise N.M2SError(f"expected (T,H,W) or (T,H,W,3) frames, got {tuple(frames.shape)}")
+    return _ops.load().preprocess_frames(frames.contiguous())
 
 
 class Pipeline:
@@ -216,25 +157,18 @@ class Pipeline:
         self.ac, self.voc, self.device = acoustic, vocoder, acoustic.device
         self.mean = torch.as_tensor(mean, dtype=torch.float32).to(self.device).contiguous()
         self.std = torch.as_tensor(std, dtype=torch.float32).to(self.device).contiguous()
-        self._ws = _WS(self.device)
 
-    def workspace_bytes(self, B, T, H, W) -> int:
-        return int(N.lib().m2s_pipeline_workspace_bytes(self.ac.handle, self.voc.handle, B, T, H, W))
-
-    def forward(self, frames: torch.Tensor, out: Optional[Dict[str, torch.Tensor]] = None, want_mels: bool = True):
+    def forward(self, frames: torch.Tensor, out: Optional[Dict[str, torch.Tensor]] = None):
+        """frames (B,T,[1,]H,W) -> dict mel_norm / mel_db / mel_log (B,T,n_mels), wav (B,T*hop)."""
         if frames.dim() == 5:
             frames = frames[:, :, 0]
         x = _as_f32(frames, self.device)
-        B, T, H, W = x.shape
-        nm = self.ac.n_mels
-        if out is None:
-            out = {"wav": torch.empty(B, T * self.voc.hop, dtype=torch.float32, device=self.device)}
-            if want_mels:
-                for k in ("mel_norm", "mel_db", "mel_log"):
-                    out[k] = torch.empty(B, T, nm, dtype=torch.float32, device=self.device)
-        ws = self._ws.get(self.workspace_bytes(B, T, H, W))
-        N.check(N.lib().m2s_pipeline_forward(
-            self.ac.handle, self.voc.handle, _ptr(x), B, T, H, W, _ptr(self.mean), _ptr(self.std),
-            _ptr(out.get("mel_norm")), _ptr(out.get("mel_db")), _ptr(out.get("mel_log")), _ptr(out["wav"]),
-            _ptr(ws), ws.numel(), _stream(self.device)))
-        return out
+        mn, db, ln, wav = self.ac.ops.pipeline_forward(self.ac.handle, self.voc.handle, x, self.mean, self.std,
+                                                       self.ac.n_mels, self.voc.hop)
+        res = {"mel_norm": mn, "mel_db": db, "mel_log": ln, "wav": wav}
+        if out is not None:  # caller-owned buffers (kept for API compatibility)
+            for k, v in res.items():
+                if k in out:
+                    out[k].copy_(v)
+            return out
+        return res

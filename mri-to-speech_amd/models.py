@@ -11,7 +11,11 @@ accept ``torch.nn.utils.remove_weight_norm``) as the reference models.py:11-140,
 ``forward`` (eval, HIP tensors) runs the whole generator in libm2s (conv_pre -> 4 x [LeakyReLU ->
 polyphase ConvTranspose1d -> 3 causal ResBlocks averaged] -> LeakyReLU(0.01) -> conv_post -> tanh).
 The torch sub-modules only hold parameters.  Discriminators and losses (training only) are not part
-of this path.  Compute dtype: ``M2S_DTYPE`` ("fp32" default, "bf16") or ``generator.m2s_dtype``.
+of this path.  ``forward`` dispatches to ``torch.ops.m2s.hifigan_forward``.  Compute dtype:
+``M2S_DTYPE`` / ``generator.m2s_dtype``: "bf16x3" (default; split fp32 within the fp32 tolerances),
+"fp32" (exact f32 MFMA), "bf16".  The packed engine is rebuilt after ``load_state_dict`` / ``.to()`` /
+a dtype change; ``generator.m2s_refresh()`` after in-place parameter edits.  Weight-norm removal
+does not change the folded weights, so it needs no repack.
 """
 from __future__ import annotations
 
@@ -111,9 +115,20 @@ class Generator(nn.Module):
         self.conv_post = _wn(Conv1d(ch, 1, 7, 1, padding=0))
         self.ups.apply(_init)
         self.conv_post.apply(_init)
-        self.m2s_dtype = os.environ.get("M2S_DTYPE", "fp32")
+        self.m2s_dtype = os.environ.get("M2S_DTYPE", "bf16x3")
         object.__setattr__(self, "_eng", None)
         object.__setattr__(self, "_eng_key", None)
+        object.__setattr__(self, "_gen", 0)
+        self.register_load_state_dict_post_hook(lambda mod, keys: mod.m2s_refresh())
+
+    def m2s_refresh(self):
+        """Repack the weights at the next forward (after in-place parameter edits)."""
+        object.__setattr__(self, "_gen", self._gen + 1)
+
+    def _apply(self, fn, *a, **k):  # .to() / .cuda() / .float() move or replace the parameters
+        r = super()._apply(fn, *a, **k)
+        self.m2s_refresh()
+        return r
 
     def _config(self):
         h = self.h
@@ -126,11 +141,10 @@ class Generator(nn.Module):
             raise NotImplementedError("m2s implements generator inference only; call .eval()")
         if device.type != "cuda":
             raise RuntimeError("m2s runs on MI355X (HIP) tensors only; move the generator and mel to 'cuda'")
-        sd = self.state_dict()
-        key = (str(device), self.m2s_dtype, tuple((k, v.data_ptr(), v._version) for k, v in sd.items()))
+        key = (str(device), self.m2s_dtype, self._gen)
         if self._eng is None or self._eng_key != key:
             from m2s.runtime import VocoderEngine
-            host = {k: v.detach().to("cpu") for k, v in sd.items()}
+            host = {k: v.detach().to("cpu") for k, v in self.state_dict().items()}
             object.__setattr__(self, "_eng", VocoderEngine(host, self._config(), dtype=self.m2s_dtype, device=device))
             object.__setattr__(self, "_eng_key", key)
         return self._eng

@@ -7,9 +7,14 @@ use_reentrant)``.  The returned module has the reference's tree (``cnn.backbone`
 ``rnn.lstm``, ``rnn.dropout``, ``head``) and state-dict keys (timm ``EfficientNetFeatures`` names for
 the backbone), so ``load_state_dict(checkpoint['model_state_dict'], strict=False)`` behaves the same.
 
-``forward`` (eval, HIP tensors) runs the whole CNN -> BiLSTM -> head graph in libm2s; the torch
-sub-modules are parameter containers only.  Compute dtype: ``M2S_DTYPE`` env var or
-``model.m2s_dtype`` ("fp32" default = reference numerics; "bf16" = MFMA fast path).
+``forward`` (eval, HIP tensors) runs the whole CNN -> BiLSTM -> head graph in libm2s through
+``torch.ops.m2s.acoustic_forward``; the torch sub-modules are parameter containers only.
+``model.cnn.backbone(x)`` returns timm's five feature maps (strides 2..32: 16/32/56/120/208 channels) in
+eval, as mri_gradcam_formant.py:155-158 reads them (``torch.ops.m2s.effnet_features``).
+Compute dtype: ``M2S_DTYPE`` env var or ``model.m2s_dtype``: "bf16x3" (default; split fp32, meets the
+fp32 tolerances of the parity tests), "fp32" (exact f32 MFMA products), "bf16" (fast, lower precision).
+The packed engine is rebuilt after ``load_state_dict`` / ``.to()`` or a dtype / chunk change; call
+``model.m2s_refresh()`` after editing parameters in place.
 No CPU fallback: CPU tensors, training mode and autograd raise.
 """
 from __future__ import annotations
@@ -72,6 +77,14 @@ class _FeatureInfo:
     def channels(self):
         return [16, 32, 56, 120, 208]
 
+    def reduction(self):
+        return [2, 4, 8, 16, 32]
+
+
+# n_blocks (effnet_features) after which each of timm's five features is taken: the end of
+# blocks.0 / .1 / .2 / .4 / .5 (features_only out_indices of tf_efficientnetv2_b2)
+_FEATURE_TAPS = (2, 5, 8, 18, 28)
+
 
 class _EffNetV2B2Features(nn.Module):
     """Parameter container with timm ``tf_efficientnetv2_b2`` features_only key names."""
@@ -88,8 +101,16 @@ class _EffNetV2B2Features(nn.Module):
         self.feature_info = _FeatureInfo()
 
     def forward(self, x):
-        raise NotImplementedError("m2s runs the backbone fused inside libm2s; per-stage feature maps "
-                                  "(Grad-CAM, mri_gradcam_formant.py:155-158) are not exposed yet")
+        """(N,3,H,W) repeated-grey or (N,1,H,W) frames -> [5 feature maps (N,C,H/s,W/s)] (eval only;
+        mri_gradcam_formant.py:153-158 passes x.repeat(1, 3, 1, 1) and keeps the last map)."""
+        if x.dim() != 4 or x.size(1) not in (1, 3):
+            raise ValueError(f"expected (N,1,H,W) or (N,3,H,W) frames, got {tuple(x.shape)}")
+        if x.size(1) == 3:
+            if not (torch.equal(x[:, 0], x[:, 1]) and torch.equal(x[:, 0], x[:, 2])):
+                raise ValueError("m2s folds the grey->RGB repeat into conv_stem; the 3 channels must be equal")
+        g = x[:, 0]
+        eng = self._root()._engine(x.device)
+        return [eng.probe(g, n) for n in _FEATURE_TAPS]
 
 
 class GlobalAvgPool(nn.Module):
@@ -139,17 +160,27 @@ class OTNLikeCNNBiLSTM(nn.Module):
         self.cnn = EffNetV2B2Backbone(pretrained=cnn_pretrained)
         self.rnn = BiLSTMSumMerge(in_dim=self.cnn.out_channels, hidden_size=rnn_hidden, dropout=dropout)
         self.head = nn.Linear(rnn_hidden, n_mels)
-        self.m2s_dtype = os.environ.get("M2S_DTYPE", "fp32")
+        self.m2s_dtype = os.environ.get("M2S_DTYPE", "bf16x3")
         self.m2s_chunk = int(os.environ.get("M2S_CHUNK", "256"))
         root = lambda: self  # noqa: E731  (children reach the engine without registering a cycle)
-        for m in (self.cnn, self.rnn):
+        for m in (self.cnn, self.rnn, self.cnn.backbone):
             object.__setattr__(m, "_root", root)
         object.__setattr__(self, "_eng", None)
         object.__setattr__(self, "_eng_key", None)
+        object.__setattr__(self, "_gen", 0)
+        self.register_load_state_dict_post_hook(lambda mod, keys: mod.m2s_refresh())
+
+    def m2s_refresh(self):
+        """Repack the weights at the next forward (after in-place parameter edits)."""
+        object.__setattr__(self, "_gen", self._gen + 1)
+
+    def _apply(self, fn, *a, **k):  # .to() / .cuda() / .float() move or replace the parameters
+        r = super()._apply(fn, *a, **k)
+        self.m2s_refresh()
+        return r
 
     def _signature(self, device):
-        return (str(device), self.m2s_dtype, self.m2s_chunk,
-                tuple((t.data_ptr(), t._version) for t in self.state_dict().values()))
+        return (str(device), self.m2s_dtype, self.m2s_chunk, self._gen)
 
     def _engine(self, device: torch.device):
         if self.training:
