@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define M2S_ABI_VERSION 1
+#define M2S_ABI_VERSION 2
 
 enum m2s_status { M2S_OK = 0, M2S_E_ARG = 1, M2S_E_HIP = 2, M2S_E_STATE = 3, M2S_E_NODEV = 4, M2S_E_INTERNAL = 5 };
 /* compute dtype of the convolution stacks (BiLSTM, head and glue always run in fp32):
@@ -70,6 +70,14 @@ int m2s_acoustic_create(const m2s_tensor* sd, int n, int n_mels, int rnn_hidden,
 void m2s_acoustic_destroy(m2s_acoustic* m);
 /* frames per CNN pass (bounds the CNN workspace); default 256 */
 int m2s_acoustic_set_chunk(m2s_acoustic* m, int frames);
+/* Asynchronous failure report.  The persistent BiLSTM waits at a grid barrier once per time step;
+ * a wait that exceeds its poll limit (workgroups not co-resident) poisons the outputs with NaN and
+ * raises a host-visible flag.  This call returns M2S_E_INTERNAL (and clears the flag) when such a
+ * launch has happened: call it after synchronising the stream.  The next forward / bilstm /
+ * pipeline call on the engine fails the same way.  Synchronous, host only. */
+int m2s_acoustic_status(m2s_acoustic* m);
+/* Fault injection for tests: polls per BiLSTM barrier wait before it times out (default 2^24). */
+int m2s_acoustic_set_lstm_spin_limit(m2s_acoustic* m, unsigned polls);
 size_t m2s_acoustic_workspace_bytes(const m2s_acoustic* m, int B, int T, int H, int W);
 /* frames (B,T,H,W) fp32 in [0,1] -> mel_norm (B,T,n_mels) fp32. */
 int m2s_acoustic_forward(m2s_acoustic* m, const float* frames, int B, int T, int H, int W, float* mel_norm,

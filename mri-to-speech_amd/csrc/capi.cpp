@@ -64,6 +64,13 @@ void check_device(int device) {
 
 hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
 
+// an earlier launch of this engine hit a BiLSTM barrier timeout (its outputs hold NaN): fail loudly
+void no_pending_error(m2s::Acoustic& a) {
+  if (a.take_async_error() != M2S_OK)
+    throw m2s::Error(M2S_E_INTERNAL, "a previous BiLSTM launch timed out at its grid barrier (workgroups not "
+                                     "co-resident?); its outputs were poisoned with NaN");
+}
+
 }  // namespace
 
 extern "C" {
@@ -94,6 +101,20 @@ int m2s_acoustic_set_chunk(m2s_acoustic* m, int frames) {
   });
 }
 
+int m2s_acoustic_status(m2s_acoustic* m) {
+  return guarded([&] {
+    M2S_CHECK(m, "null argument");
+    no_pending_error(m->impl);
+  });
+}
+
+int m2s_acoustic_set_lstm_spin_limit(m2s_acoustic* m, unsigned polls) {
+  return guarded([&] {
+    M2S_CHECK(m && polls > 0, "bad argument");
+    m->impl.lstm_spin_max_ = polls;
+  });
+}
+
 size_t m2s_acoustic_workspace_bytes(const m2s_acoustic* m, int B, int T, int H, int W) {
   size_t r = 0;
   guarded([&] { r = m->impl.workspace_bytes(B, T, H, W); });
@@ -104,6 +125,7 @@ int m2s_acoustic_forward(m2s_acoustic* m, const float* frames, int B, int T, int
                          size_t ws_bytes, void* stream) {
   return guarded([&] {
     M2S_CHECK(m && frames && mel_norm && ws, "null argument");
+    no_pending_error(m->impl);
     DeviceGuard g(m->impl.device());
     m->impl.forward(frames, B, T, H, W, mel_norm, ws, ws_bytes, S(stream));
   });
@@ -138,6 +160,7 @@ int m2s_bilstm_summerge(m2s_acoustic* m, const float* feats, int B, int T, float
                         size_t ws_bytes, void* stream) {
   return guarded([&] {
     M2S_CHECK(m && feats && ws, "null argument");
+    no_pending_error(m->impl);
     DeviceGuard g(m->impl.device());
     m2s::Workspace w(ws, ws_bytes);
     m->impl.bilstm(feats, B, T, y, mel_norm, w, S(stream));
@@ -208,6 +231,7 @@ int m2s_pipeline_forward(m2s_acoustic* m, m2s_vocoder* v, const float* frames, i
     M2S_CHECK(m && v && frames && mean && std && wav && ws, "null argument");
     M2S_CHECK(m->impl.device() == v->impl.device(), "acoustic model and vocoder on different devices");
     M2S_CHECK(m->impl.n_mels() == v->impl.num_mels(), "n_mels mismatch between acoustic model and vocoder");
+    no_pending_error(m->impl);
     DeviceGuard g(m->impl.device());
     const size_t rows = (size_t)B * T;
     const int nm = m->impl.n_mels(), cs = m2s::chan_stride(nm);

@@ -489,12 +489,8 @@ void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, 
       return launch_tile<256, 64, 4, 4, KIND, XF, 1>(a, s, phases, flops, bytes);
     return launch_tile<128, 128, 4, 4, KIND, XF, 1>(a, s, phases, flops, bytes);
   } else {
-  static const int big = [] {  // M2S_GEMM_BIG=0 keeps the 128x128 tile for the long 1x1 GEMMs,
-    const char* e = getenv("M2S_GEMM_BIG");  // 1 limits the 128x256 tile to n <= 256 and kp >= 512
-    return e ? atoi(e) : 2;
-  }();
-  if constexpr (KIND == KIND_GEMM || KIND == KIND_CONV2D) if (big && a.M >= 256 * 256 && n > 128 &&
-                                                               ((n <= 256 && a.kp >= 512) || (KIND == KIND_GEMM && big > 1))) {
+  if constexpr (KIND == KIND_GEMM || KIND == KIND_CONV2D) if (a.M >= 256 * 256 && n > 128 &&
+                                                               ((n <= 256 && a.kp >= 512) || KIND == KIND_GEMM)) {
     // long-K 1x1 GEMMs and 3x3 convs with 129..256 outputs: one 256-wide n tile reads (gathers)
     // the activations once instead of twice (b5 conv_pwl 1248 -> 208: 13.5 -> 10.0 ms per 4 steps;
     // b2 conv_exp 3x3 56 -> 224: 1.10 -> 0.91 ms per launch); also every wide 1x1 GEMM (the
@@ -502,25 +498,11 @@ void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, 
     // for n <= 128 measured slower at every K (one wave per SIMD at 272 registers).
     return launch_tile<128, 256, 4, 8, KIND, XF, 0>(a, s, phases, flops, bytes);
   }
-  static const int tall = [] {  // M2S_GEMM_TALL=0 keeps the 128x128 tile for long-K GEMMs with n <= 128
-    const char* e = getenv("M2S_GEMM_TALL");
-    return e ? atoi(e) : 1;
-  }();
-  if constexpr (KIND == KIND_GEMM || KIND == KIND_CONV1D)
-    if (tall && a.M >= 256 * 256 && n > 64 && n <= 128 && a.kp >= 384 && (KIND == KIND_GEMM || tall > 1)) {
-    // 256 rows x 128 outputs at two waves per SIMD: the weight tile (K x 128) is re-read from L2
-    // once per 256 rows instead of per 128 (the SE-scaled conv_pwl of blocks.3/4: K 416..736)
-    return launch_tile<256, 128, 8, 4, KIND, XF, 0>(a, s, phases, flops, bytes);
-  }
-  static const int smallm = [] {  // M2S_GEMM_SMALLM=0 keeps 128-row tiles for short-M, wide, long-K convs
-    const char* e = getenv("M2S_GEMM_SMALLM");  // (measured 10 % slower: off by default)
-    return e ? atoi(e) : 0;
-  }();
-  if constexpr (KIND == KIND_CONV1D)
-    if (smallm && a.M <= 32768 && n >= 128 && n % 128 == 0 && a.kp >= 512) {
-      // the vocoder's first MRF stage (M = 64 clips x 300, N = 256, K up to 2816): 128-row tiles
-      // give ~300 workgroups for 256 CUs; 64-row tiles double the parallelism
-      return launch_tile<64, 128, 4, 2, KIND, XF, 0>(a, s, phases, flops, bytes);
+  if constexpr (KIND == KIND_GEMM)
+    if (a.M >= 256 * 256 && n > 64 && n <= 128 && a.kp >= 384) {
+      // 256 rows x 128 outputs at two waves per SIMD: the weight tile (K x 128) is re-read from L2
+      // once per 256 rows instead of per 128 (the SE-scaled conv_pwl of blocks.3/4: K 416..736)
+      return launch_tile<256, 128, 8, 4, KIND, XF, 0>(a, s, phases, flops, bytes);
     }
   if (n <= 16)
     launch_tile<256, 16, 4, 1, KIND, XF, 0>(a, s, phases, flops, bytes);
@@ -565,10 +547,6 @@ void launch_conv_gemm(const ConvArgs& a, bool split, hipStream_t s, double flops
   M2S_CHECK(a.kp % 32 == 0 && a.kp >= a.ntaps * a.cs_in, "conv_gemm: kp");
   M2S_CHECK(a.kind != KIND_CONV2D || a.ks == 3, "conv_gemm: 2-D kernels are 3x3 (1x1 runs as GEMM)");
   if (a.M <= 0) return;
-  static const bool halo = [] {  // M2S_CONV_HALO=0: 3x3 stride-1 convs on the implicit-GEMM path
-    const char* e = getenv("M2S_CONV_HALO");
-    return !e || atoi(e) != 0;
-  }();
   if (split) {
     switch (a.kind) {
       case KIND_CONV2D: launch_kind<KIND_CONV2D, 1>(a, s, 1, flops, bytes); break;
@@ -580,7 +558,7 @@ void launch_conv_gemm(const ConvArgs& a, bool split, hipStream_t s, double flops
     M2S_HIP(hipGetLastError());
     return;
   }
-  if (halo && conv_halo_supported(a)) return launch_conv_halo(a, s, flops, bytes);
+  if (conv_halo_supported(a)) return launch_conv_halo(a, s, flops, bytes);
   switch (a.kind) {
     case KIND_CONV2D: launch_kind<KIND_CONV2D, 0>(a, s, 1, flops, bytes); break;
     case KIND_CONV1D: launch_kind<KIND_CONV1D, 0>(a, s, 1, flops, bytes); break;

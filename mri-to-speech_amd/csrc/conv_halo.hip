@@ -26,9 +26,6 @@ namespace {
 __device__ __attribute__((aligned(16))) uint4 g_halo_zero[4];  // DMA source for padding pixels
 
 constexpr int ROWB = 64;  // bytes per LDS row (32 bf16 = one k-step of one pixel)
-#ifndef HALO_MODE
-#define HALO_MODE 0  // microbenchmark variants (tools/halo_bench.hip): 1 no MFMA, 4 no stores, 8 no prefetch
-#endif
 constexpr int TW = 16;    // output tile width (one MFMA position subtile = one tile row)
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * ROWB + ((chunk ^ ((row >> 2) & 3)) << 4); }
@@ -122,7 +119,7 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(const HaloArgs a) {
 
   for (int it = 0; mt < a.m_tiles; mt += mstride, ++it) {
     char* hb = hbuf0 + (it & 1) * hbytes;
-    if (!(HALO_MODE & 8) && mt + mstride < a.m_tiles) issue_halo(mt + mstride, hbuf0 + ((it + 1) & 1) * hbytes);
+    if (mt + mstride < a.m_tiles) issue_halo(mt + mstride, hbuf0 + ((it + 1) & 1) * hbytes);
 
     f32x4 acc[NTW][MTW];
 #pragma unroll
@@ -152,7 +149,7 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(const HaloArgs a) {
       for (int ni = 0; ni < NTW; ++ni)
 #pragma unroll
         for (int mi = 0; mi < MTW; ++mi)
-          acc[ni][mi] = (HALO_MODE & 1) ? acc[ni][mi] + __builtin_bit_cast(f32x4, __builtin_bit_cast(uint4, bx[mi]) ^ __builtin_bit_cast(uint4, af[ni])) : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ni], bx[mi], acc[ni][mi], 0, 0, 0);
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ni], bx[mi], acc[ni][mi], 0, 0, 0);
     }
     // residual = this block's input (cs_in == cs_out): take it from the halo tile now, before the
     // barrier releases the buffer to the next prefetch
@@ -210,7 +207,7 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(const HaloArgs a) {
         uint2 u;
         u.x = pack_bf16x2(v[0], v[1]);
         u.y = pack_bf16x2(v[2], v[3]);
-        if (!(HALO_MODE & 4) || u.x == 0x7fc17fc1u) *reinterpret_cast<uint2*>(a.y + orow + n4) = u;
+        *reinterpret_cast<uint2*>(a.y + orow + n4) = u;
       }
     }
   }

@@ -4,7 +4,8 @@
 // an (NT*16 channels) x (MT*16 positions) tile of 16x16 MFMA accumulators.  Per K chunk each
 // lane issues one 16-byte load per M subtile (8 bf16 / 4 f32 input channels of one position
 // at one tap, zero for padding) and one per N subtile (packed weight row), then
-// NT*MT MFMAs (bf16: v_mfma_f32_16x16x32_bf16; f32: 4 x v_mfma_f32_16x16x4_f32, exact f32).
+// NT*MT MFMAs (f32: 4 x v_mfma_f32_16x16x4_f32, exact f32).  Only the exact-f32 path (M2S_DT_F32)
+// instantiates it; bf16 and split fp32 run the LDS-DMA pipeline of conv_gemm.hip.
 #include "conv_igemm.hpp"
 
 #include "prof.hpp"
@@ -272,34 +273,25 @@ void launch_kind(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
 
 template <typename T>
 void launch_conv(const ConvArgs& a, hipStream_t s, double flops, double bytes) {
-  if constexpr (std::is_same<T, sp_t>::value) {  // split fp32: three-term bf16 MFMA (conv_gemm.hip)
-    M2S_CHECK(a.kind != KIND_CONV2D || a.ks == 3, "conv: split 2-D convs are 3x3");
-    launch_conv_gemm(a, true, s, flops, bytes);
-    return;
-  } else if constexpr (sizeof(T) == 2) {
-    static const bool v1 = [] {
-      const char* e = getenv("M2S_CONV_IMPL");
-      return e && std::string(e) == "v1";
-    }();
-    if (!v1 && (a.kind != KIND_CONV2D || a.ks == 3)) {
-      launch_conv_gemm(a, false, s, flops, bytes);
-      return;
+  if constexpr (!std::is_same<T, float>::value) {  // bf16 / split fp32: LDS-DMA pipeline (conv_gemm.hip)
+    M2S_CHECK(a.kind != KIND_CONV2D || a.ks == 3, "conv: bf16 / split 2-D convs are 3x3");
+    launch_conv_gemm(a, std::is_same<T, sp_t>::value, s, flops, bytes);
+  } else {  // exact f32 products: the direct-load kernel of this file
+    constexpr int KC = Elem<T>::KC;
+    M2S_CHECK(a.cs_in % KC == 0 || KC % a.cs_in == 0, "conv: cs_in incompatible with K chunk");
+    M2S_CHECK(a.cs_out % 4 == 0, "conv: cs_out must be a multiple of 4");
+    M2S_CHECK(a.tpc == conv_tpc(a.cs_in, KC), "conv: tpc mismatch");
+    M2S_CHECK(a.kp == conv_kp(a.ntaps, a.cs_in, KC), "conv: kp mismatch");
+    if (a.M <= 0) return;
+    switch (a.kind) {
+      case KIND_CONV2D: launch_kind<T, KIND_CONV2D>(a, s, 1, flops, bytes); break;
+      case KIND_CONV1D: launch_kind<T, KIND_CONV1D>(a, s, 1, flops, bytes); break;
+      case KIND_CONVT: launch_kind<T, KIND_CONVT>(a, s, a.ct_u, flops, bytes); break;
+      case KIND_GEMM: launch_kind<T, KIND_GEMM>(a, s, 1, flops, bytes); break;
+      default: M2S_CHECK(false, "conv: bad kind");
     }
+    M2S_HIP(hipGetLastError());
   }
-  constexpr int KC = Elem<T>::KC;
-  M2S_CHECK(a.cs_in % KC == 0 || KC % a.cs_in == 0, "conv: cs_in incompatible with K chunk");
-  M2S_CHECK(a.cs_out % 4 == 0, "conv: cs_out must be a multiple of 4");
-  M2S_CHECK(a.tpc == conv_tpc(a.cs_in, KC), "conv: tpc mismatch");
-  M2S_CHECK(a.kp == conv_kp(a.ntaps, a.cs_in, KC), "conv: kp mismatch");
-  if (a.M <= 0) return;
-  switch (a.kind) {
-    case KIND_CONV2D: launch_kind<T, KIND_CONV2D>(a, s, 1, flops, bytes); break;
-    case KIND_CONV1D: launch_kind<T, KIND_CONV1D>(a, s, 1, flops, bytes); break;
-    case KIND_CONVT: launch_kind<T, KIND_CONVT>(a, s, a.ct_u, flops, bytes); break;
-    case KIND_GEMM: launch_kind<T, KIND_GEMM>(a, s, 1, flops, bytes); break;
-    default: M2S_CHECK(false, "conv: bad kind");
-  }
-  M2S_HIP(hipGetLastError());
 }
 
 template void launch_conv<float>(const ConvArgs&, hipStream_t, double, double);

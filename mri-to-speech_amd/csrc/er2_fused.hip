@@ -47,11 +47,6 @@ __device__ __forceinline__ void dma16(const void* src, void* lds_wave_base) {
 __device__ __forceinline__ uint32_t lds_off(const void* p) {
   return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p;
 }
-__device__ __forceinline__ float4 lds_f4(const void* p) {
-  float4 r;
-  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(lds_off(p)));
-  return r;
-}
 __device__ __forceinline__ uint2 lds_u2(const void* p) {
   uint2 r;
   asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(lds_off(p)));

@@ -91,15 +91,6 @@ void launch_ers2_fused(const bf16_t* x, int N, int H, int W, int OH, int OW, int
                        int cs_out, const bf16_t* wexp, const float* bexp, const bf16_t* wpwl, const float* bpwl,
                        bf16_t* y, double flops, double bytes, hipStream_t s);
 
-// bf16 whole InvertedResidual (stride 1, 16x16 maps, channel strides 128 / <= 736 / 128): conv_pw + SiLU,
-// conv_dw + SiLU, SqueezeExcite, conv_pwl (+ skip) in one kernel; wst = (cs_mid / 32) stages of
-// ir_block_stage_bytes() in the kernel's order; w1 / w2 / b1 / b2 the packed SE convs.  (ir_block.hip)
-bool ir_block_supported(int H, int W, int cs_in, int cs_mid, int cs_out, int rd, int kp1, int kp2);
-int ir_block_stage_bytes();
-void launch_ir_block(const bf16_t* x, int N, const bf16_t* wst, int mid, int cs_mid, const bf16_t* w1, int kp1,
-                     const float* b1, int rd, const bf16_t* w2, int kp2, const float* b2, const float* bpwl, bool skip,
-                     bf16_t* y, double flops, double bytes, hipStream_t s);
-
 // Decoded frames -> model input: uint8 (N,H,W) grey or (N,H,W,3) BGR -> fp32 (N,H,W) in [0, 1]
 // (_preprocess_frame, run_mri_video_inference.py:34-54, minus the host-side resize).  (preprocess.hip)
 void launch_preprocess(const uint8_t* frames, int N, int H, int W, int channels, float* out, hipStream_t s);
@@ -118,8 +109,11 @@ void launch_lstm_step(const float* pre, const float* whh, float* hs, float* cst,
 // `sync` = lstm_persistent_sync_bytes() of device memory (reset by the launcher).
 bool lstm_persistent_supported(int H);
 size_t lstm_persistent_sync_bytes();
+// `spin_max` bounds each barrier wait (polls with s_sleep 1); on a timeout the kernel stores 1 to
+// `err_host` (pinned, host-mapped) and writes NaN to the rest of the outputs.
+constexpr unsigned LSTM_SPIN_MAX = 1u << 24;
 void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync,
-                            hipStream_t s);
+                            unsigned spin_max, unsigned* err_host, hipStream_t s);
 
 // head: y = hs[0] + hs[1] (sum merge); out = y W^T + b.  wt (H, n_mels) transposed weight.
 void launch_mel_head(const float* hs, int rows, int H, const float* wt, const float* b, int n_mels,

@@ -14,8 +14,10 @@
 // (the layer output) and is published to the direction's other workgroups by a release/acquire
 // counter barrier (cdna_hip_programming.md Guideline 16): plain stores -> vmcnt(0) -> barrier ->
 // agent release fence -> atomic add; consumers poll relaxed, then one agent acquire fence.
-// Spins are bounded: on timeout the workgroup sets the error word and leaves, so the grid always
-// drains.  Products are exact fp32 (MFMA f32); only the summation order differs from torch.
+// Spins are bounded: on timeout the workgroup sets the error word, poisons its remaining outputs
+// with NaN and leaves, so the grid always drains; the engine's pinned host flag (`err_host`) is set
+// too, and the C ABI reports it (m2s_acoustic_status; the next forward fails with M2S_E_INTERNAL).
+// Products are exact fp32 (MFMA f32); only the summation order differs from torch.
 #include <algorithm>
 
 #include "kernels.hpp"
@@ -31,7 +33,6 @@ constexpr int LP_KW = LP_H / 4;    // K slice per wave
 constexpr int LP_KH = LP_KW / 2;   // floats per lane per B tile (k half = lane / 32)
 constexpr int LP_BT = 2;           // 32-sequence B tiles per pass
 constexpr int LP_BMAX = 64;        // sequences per launch (c in LDS); larger batches: several launches
-constexpr unsigned LP_SPIN_MAX = 1u << 24;
 
 struct LstmSync {
   unsigned arrive[2];  // per-direction monotonic arrival counters
@@ -40,7 +41,8 @@ struct LstmSync {
 
 __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __restrict__ pre,
                                                                  const float* __restrict__ whh, float* hs,
-                                                                 int Btot, int b0, int B, int T, LstmSync* sync) {
+                                                                 int Btot, int b0, int B, int T, LstmSync* sync,
+                                                                 unsigned spin_max, unsigned* err_host) {
   __shared__ float red[4][LP_BT][32][33];
   __shared__ float cst[LP_U][LP_BMAX];
   __shared__ int abort_flag;
@@ -84,7 +86,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
         unsigned spins = 0;
         while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
           __builtin_amdgcn_s_sleep(1);
-          if (++spins > LP_SPIN_MAX ||
+          if (++spins > spin_max ||
               __hip_atomic_load(&sync->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
             __hip_atomic_store(&sync->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             abort_flag = 1;
@@ -95,7 +97,8 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
-      if (abort_flag) {  // barrier timed out: poison this workgroup's remaining outputs and leave
+      if (abort_flag) {  // barrier timed out: flag the host, poison the remaining outputs, leave
+        if (tid == 0 && err_host) __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         for (int st = step; st < T; ++st) {
           const int tt = dir == 0 ? st : T - 1 - st;
           for (int p = tid; p < LP_U * B; p += 256)
@@ -179,7 +182,7 @@ bool lstm_persistent_supported(int H) { return H == LP_H; }
 size_t lstm_persistent_sync_bytes() { return 256; }
 
 void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync,
-                            hipStream_t s) {
+                            unsigned spin_max, unsigned* err_host, hipStream_t s) {
   M2S_CHECK(lstm_persistent_supported(H) && B > 0 && T > 0, "lstm_persistent: unsupported shape");
   const int grid = 2 * (H / LP_U);
   // Every workgroup must be resident (the step barrier waits on all of them).  The grid is 160
@@ -199,7 +202,8 @@ void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B
   for (int b0 = 0; b0 < B; b0 += LP_BMAX) {  // c lives in LDS: at most LP_BMAX sequences per launch
     const int nb = std::min(LP_BMAX, B - b0);
     M2S_HIP(hipMemsetAsync(sync, 0, lstm_persistent_sync_bytes(), s));
-    hipLaunchKernelGGL(lstm_persistent_kernel, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, b0, nb, T, sp);
+    hipLaunchKernelGGL(lstm_persistent_kernel, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, b0, nb, T, sp, spin_max,
+                       err_host);
     M2S_HIP(hipGetLastError());
   }
 }

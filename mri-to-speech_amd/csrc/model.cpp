@@ -227,7 +227,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_FUSED")) se_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER_FUSED")) er_fused_ = std::strcmp(e, "0") != 0;
-  if (const char* e = std::getenv("M2S_IR_BLOCK")) ir_block_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_LSTM_PERSISTENT")) lstm_persistent_ = std::strcmp(e, "0") != 0;
   const std::string P = "cnn.backbone.";
   {  // stem: fold repeat(1,3,1,1) by summing the 3 input channels; then BN
     const float* w = need(sd, P + "conv_stem.weight", {EFF_STEM, 3, 3, 3}).data;
@@ -395,48 +395,6 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
         pack_conv(arena_, dtype, b.se2, [&](int, int n, int, int c) { return w2[(size_t)n * rd + c]; },
                   [&](int n) { return b2[n]; });
         conv1x1(b.c2, q + "conv_pwl.weight", m, b.cout, fold_bn(sd, q + "bn3", b.cout));
-        if (dtype == M2S_DT_BF16 && b.stride == 1 &&
-            ir_block_supported(16, 16, chan_stride(cin), cs, chan_stride(b.cout), rd, b.se1.kp, b.se2.kp)) {
-          // ir_block.hip stage stream: one stage per 32-channel slice of the expanded width (expand and
-          // conv_pwl A fragments, depthwise taps, bn1 / bn2 biases; layout in the kernel's header)
-          const float* wp = need(sd, q + "conv_pw.weight", {m, cin, 1, 1}).data;
-          const float* wl = need(sd, q + "conv_pwl.weight", {b.cout, m, 1, 1}).data;
-          const BN e1 = fold_bn(sd, q + "bn1", m), e3 = fold_bn(sd, q + "bn3", b.cout);
-          const int nsl = cs / 32, se = ir_block_stage_bytes() / 2;
-          std::vector<uint16_t> st((size_t)nsl * se, 0);
-          for (int sl = 0; sl < nsl; ++sl) {
-            uint16_t* S = st.data() + (size_t)sl * se;
-            for (int pc = 0; pc < 16; ++pc)
-              for (int ln = 0; ln < 64; ++ln)
-                for (int e = 0; e < 8; ++e) {
-                  const int row = ln & 15, g8 = ln >> 4;
-                  float v = 0.f;
-                  if (pc < 8) {  // expand, piece 2 ks + nt
-                    const int ch = 32 * sl + 16 * (pc & 1) + row, kk = 32 * (pc >> 1) + 8 * g8 + e;
-                    if (ch < m && kk < cin) v = wp[(size_t)ch * cin + kk] * e1.a[ch];
-                  } else {  // conv_pwl, piece 8 + on
-                    const int o = 16 * (pc - 8) + row, ch = 32 * sl + 8 * g8 + e;
-                    if (o < b.cout && ch < m) v = wl[(size_t)o * m + ch] * e3.a[o];
-                  }
-                  S[((size_t)pc * 64 + ln) * 8 + e] = f2bf_host(v);
-                }
-            uint32_t tp[9 * 32];
-            float bb[64];
-            for (int c = 0; c < 32; ++c) {
-              const int ch = 32 * sl + c;
-              for (int t = 0; t < 9; ++t) {
-                const uint32_t h = ch < m ? f2bf_host(wd[(size_t)ch * 9 + t] * bn2.a[ch]) : 0u;
-                tp[t * 32 + c] = c % 2 == 0 ? h : h << 16;
-              }
-              bb[c] = ch < m ? e1.b[ch] : 0.f;
-              bb[32 + c] = ch < m ? bn2.b[ch] : 0.f;
-            }
-            std::memcpy(S + 16 * 512, tp, sizeof(tp));
-            std::memcpy(S + 16 * 512 + sizeof(tp) / 2, bb, sizeof(bb));
-          }
-          b.ib_w = arena_.add_vec(st);
-          b.ib = true;
-        }
       }
       blocks_.push_back(b);
       cin = sdf.cout;
@@ -473,6 +431,9 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   head_b_ = arena_.add(hb, sizeof(float) * n_mels);
 
   arena_.upload(device);
+  M2S_HIP(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
+  *err_host_ = 0;
+  M2S_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0));
   for (auto& b : blocks_) {
     b.c1.resolve(arena_);
     if (b.type != 0) b.c2.resolve(arena_);
@@ -482,6 +443,15 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
     }
   }
   lstm_ih_.resolve(arena_);
+}
+
+Acoustic::~Acoustic() {
+  if (err_host_) (void)hipHostFree(err_host_);
+}
+
+int Acoustic::take_async_error() {
+  const unsigned e = __atomic_exchange_n(err_host_, 0u, __ATOMIC_ACQ_REL);
+  return e ? M2S_E_INTERNAL : M2S_OK;
 }
 
 void Acoustic::effnet_dims(int H, int W, size_t* io, size_t* mid, size_t* se) const {
@@ -661,17 +631,6 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         p.OH = nh * nw;
         p.res = b.skip ? cur : nullptr;
         run_conv<T>(p, b.c2, s);
-      } else if (std::is_same<T, bf16_t>::value && ir_block_ && b.ib &&
-                 ir_block_supported(nh, nw, b.c1.cs_in, chan_stride(b.mid), chan_stride(b.cout), b.rd, b.se1.kp,
-                                    b.se2.kp)) {
-        const double px = (double)nc * nh * nw;
-        launch_ir_block(reinterpret_cast<const bf16_t*>(cur), nc, static_cast<const bf16_t*>(arena_.ptr(b.ib_w)), b.mid,
-                        chan_stride(b.mid), static_cast<const bf16_t*>(b.se1.w), b.se1.kp, b.se1.b, b.rd,
-                        static_cast<const bf16_t*>(b.se2.w), b.se2.kp, b.se2.b, b.c2.b, b.skip,
-                        reinterpret_cast<bf16_t*>(nxt), 2.0 * px * b.mid * (b.cin + 9 + b.cout),
-                        2.0 * px * (b.c1.cs_in + chan_stride(b.cout)) +
-                            (double)(chan_stride(b.mid) / 32) * ir_block_stage_bytes(),
-                        s);
       } else {
         const int cs = chan_stride(b.mid);
         constexpr bool SPL = std::is_same<T, sp_t>::value;
@@ -766,13 +725,12 @@ void Acoustic::bilstm(const float* feats, int B, int T, float* y, float* mel_nor
   a.M = (int)BT;
   run_conv<float>(a, lstm_ih_, s);
   void* sync = ws.take<char>(lstm_persistent_sync_bytes());
-  const char* pe = std::getenv("M2S_LSTM_PERSISTENT");  // "0": one launch per time step
-  const bool persistent = !pe || std::strcmp(pe, "0") != 0;
-  if (persistent && lstm_persistent_supported(H)) {
+  if (lstm_persistent_ && lstm_persistent_supported(H)) {
     // algorithmic bytes: W_hh of both directions once, gate pre-activations in, h out
     ProfScope ps("lstm_persistent_kernel", 2.0 * 2 * B * 4.0 * H * H * (T - 1),
                  4.0 * 2 * 4 * H * H + 4.0 * BT * (8.0 * H + 2.0 * H), s);
-    launch_lstm_persistent(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, s);
+    launch_lstm_persistent(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, lstm_spin_max_,
+                           err_dev_, s);
   } else {
     for (int st = 0; st < T; ++st) {
       ProfScope ps("lstm_step_kernel", 2.0 * 2 * B * 4.0 * H * H, 4.0 * 2 * 4 * H * H, s);
@@ -842,6 +800,11 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
     const int u = h.upsample_rates[i], k = h.upsample_kernel_sizes[i];
     const int ci = c0 >> i, co = c0 >> (i + 1);
     M2S_CHECK(co >= 4, "generator too narrow");
+    // ConvTranspose1d(k, u, padding (k-u)/2) (models.py:98-101) gives L*u outputs only when k - u is
+    // even and non-negative; the polyphase packing and conv_post's look-ahead assume exactly L*u
+    M2S_CHECK(u >= 1 && k >= u && (k - u) % 2 == 0,
+              "upsample kernel " + std::to_string(k) + " / rate " + std::to_string(u) +
+                  ": k - u must be even and >= 0 (output length L*u)");
     hop_ *= u;
     const std::string p = "ups." + std::to_string(i);
     std::vector<float> w = fold_wn(sd, p, {ci, co, k});  // ConvTranspose1d weight (in, out, k)
@@ -864,6 +827,7 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
       RB rb;
       rb.k = h.resblock_kernel_sizes[j];
       const int kk = rb.k;
+      M2S_CHECK(h.n_dilations[j] >= 1 && h.n_dilations[j] <= 8, "resblock dilations: 1..8 per kernel size");
       for (int d = 0; d < h.n_dilations[j]; ++d) rb.dil.push_back(h.resblock_dilation_sizes[j][d]);
       const std::string q = "resblocks." + std::to_string(i * h.n_kernels + j);
       auto mk = [&](const std::string& name, int dil) {

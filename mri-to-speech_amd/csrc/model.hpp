@@ -79,14 +79,21 @@ class Workspace {  // bump allocator over a caller-provided device buffer
 class Acoustic {
  public:
   Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int device);
+  ~Acoustic();
+  Acoustic(const Acoustic&) = delete;
+  Acoustic& operator=(const Acoustic&) = delete;
+  // M2S_E_INTERNAL (and clears the flag) if a BiLSTM barrier of an earlier launch timed out
+  int take_async_error();
+  unsigned lstm_spin_max_ = LSTM_SPIN_MAX;  // fault injection: m2s_acoustic_set_lstm_spin_limit
   int device() const { return device_; }
   int n_mels() const { return n_mels_; }
   int chunk = 256;
   bool ir_fused_ = true;  // bf16: fused conv_pw + conv_dw + SE squeeze (env M2S_IR_FUSED=0 disables)
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
   bool se_fused_ = true;    // bf16: SE excitation in one kernel (env M2S_SE_FUSED=0: two GEMMs)
-  bool ir_block_ = false;   // bf16: whole InvertedResidual at 16x16 in one kernel (opt-in: env M2S_IR_BLOCK=1)
   bool er_fused_ = true;    // bf16: EdgeResidual 32->128->32 in one kernel (env M2S_ER_FUSED=0 disables)
+  bool lstm_persistent_ = true;  // one-launch BiLSTM recurrence (env M2S_LSTM_PERSISTENT=0: a launch per step)
+  // (the M2S_* switches are read once, when the engine is created: A/B tests of fused vs unfused)
 
   size_t workspace_bytes(int B, int T, int H, int W) const;
   void forward(const float* frames, int B, int T, int H, int W, float* mel_norm, void* ws, size_t wsb, hipStream_t s);
@@ -105,8 +112,6 @@ class Acoustic {
     PConv se1, se2;             // ir SE: conv_reduce (mid -> rd, SiLU), conv_expand (rd -> mid, sigmoid)
     size_t er_wexp = 0, er_wpwl = 0;  // bf16 er 32 -> 128 -> 32 stride 1: fused-kernel fragment orders
     bool er_frag = false;
-    size_t ib_w = 0;  // bf16 ir stride 1 at 16x16: ir_block.hip stage stream
-    bool ib = false;
   };
   template <typename T>
   void effnet_t(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe, int* probe_dims,
@@ -121,6 +126,8 @@ class Acoustic {
   PConv lstm_ih_;
   size_t whh_ = 0, head_wt_ = 0, head_b_ = 0;
   int max_mid_cs_ = 0;
+  unsigned* err_host_ = nullptr;  // pinned, host-mapped: set by lstm_persistent_kernel on a barrier timeout
+  unsigned* err_dev_ = nullptr;
 };
 
 class Vocoder {

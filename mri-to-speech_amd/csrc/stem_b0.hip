@@ -24,9 +24,6 @@
 namespace m2s {
 namespace {
 
-#ifndef SB_MODE
-#define SB_MODE 0  // microbenchmark variants (tools/sb_bench.hip): 1 no stem, 2 no blocks.0.0 MFMA, 4 no blocks.0.1 MFMA
-#endif
 constexpr int SB_TW = 16;           // output tile width (one MFMA position subtile per tile row)
 constexpr int SB_SW = SB_TW + 4;    // S row width
 constexpr int SB_AW = SB_TW + 2;    // A row width
@@ -68,7 +65,7 @@ __global__ void __launch_bounds__(256, 4) stem_b0_kernel(const StemB0Args a) {
   // scalar load feeding two FMAs and nothing keeps the 288 weights live in registers
   const float* fr = a.frames + (size_t)n * a.H * a.W;
   static_assert(SPIX % 2 == 0 && SPIX / 2 <= 256, "stem tile");
-  if (tid < SPIX / 2 && !(SB_MODE & 1)) {
+  if (tid < SPIX / 2) {
     float in[2][9];
     bool ok[2];
     int pix[2];
@@ -136,7 +133,7 @@ __global__ void __launch_bounds__(256, 4) stem_b0_kernel(const StemB0Args a) {
       const int toff = ((t / 3) * SB_SW + (t % 3)) * 16;
 #pragma unroll
       for (int i = 0; i < AMS; ++i) {
-        if (wave + 4 * i < ASUB && !(SB_MODE & 2)) {
+        if (wave + 4 * i < ASUB) {
           const bf16x8 b = *reinterpret_cast<const bf16x8*>(sS + sbase[i] + toff);
           acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[t], b, acc[i], 0, 0, 0);
         }
@@ -178,7 +175,6 @@ __global__ void __launch_bounds__(256, 4) stem_b0_kernel(const StemB0Args a) {
 #pragma unroll
       for (int i = 0; i < OMS; ++i) {
         const int row = wave + 4 * i;  // output tile row = subtile
-        if (SB_MODE & 4) continue;
         const bf16x8 b = *reinterpret_cast<const bf16x8*>(sA + (row * SB_AW + r16) * 16 + toff[st]);
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[st], b, acc[i], 0, 0, 0);
       }

@@ -61,6 +61,8 @@ def lib():
         "m2s_acoustic_create": (i, [C.POINTER(Tensor), i, i, i, i, i, C.POINTER(vp)]),
         "m2s_acoustic_destroy": (None, [vp]),
         "m2s_acoustic_set_chunk": (i, [vp, i]),
+        "m2s_acoustic_status": (i, [vp]),
+        "m2s_acoustic_set_lstm_spin_limit": (i, [vp, C.c_uint]),
         "m2s_acoustic_workspace_bytes": (sz, [vp, i, i, i, i]),
         "m2s_acoustic_forward": (i, [vp, fp, i, i, i, i, fp, vp, sz, vp]),
         "m2s_effnet_forward": (i, [vp, fp, i, i, i, fp, vp, sz, vp]),
@@ -81,7 +83,7 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.m2s_abi_version() != 1:
+    if L.m2s_abi_version() != 2:
         raise M2SError("libm2s ABI version mismatch")
     _lib = L
     return L
@@ -95,7 +97,8 @@ def check(rc: int) -> None:
 
 def exported_symbols() -> List[str]:
     return [n for n in ("m2s_abi_version", "m2s_last_error", "m2s_device_check", "m2s_acoustic_create",
-                        "m2s_acoustic_destroy", "m2s_acoustic_set_chunk", "m2s_acoustic_workspace_bytes",
+                        "m2s_acoustic_destroy", "m2s_acoustic_set_chunk", "m2s_acoustic_status",
+                        "m2s_acoustic_set_lstm_spin_limit", "m2s_acoustic_workspace_bytes",
                         "m2s_acoustic_forward", "m2s_effnet_forward", "m2s_effnet_probe", "m2s_bilstm_summerge",
                         "m2s_mel_glue", "m2s_preprocess_frames", "m2s_vocoder_create", "m2s_vocoder_destroy",
                         "m2s_vocoder_workspace_bytes", "m2s_vocoder_forward", "m2s_pipeline_workspace_bytes",

@@ -65,6 +65,12 @@ class AcousticEngine:
         """The m2s_acoustic* as the int the torch.ops.m2s ops take."""
         return int(self._h.value)
 
+    def check(self):
+        """Synchronise the device and raise M2SError if a launch of this engine failed asynchronously
+        (a BiLSTM grid-barrier timeout: its outputs hold NaN; include/m2s.h m2s_acoustic_status)."""
+        torch.cuda.synchronize(self.device)
+        N.check(N.lib().m2s_acoustic_status(self._h))
+
     def forward(self, frames: torch.Tensor) -> torch.Tensor:
         """frames (B,T,1,H,W) or (B,T,H,W) fp32 -> normalised mel (B,T,n_mels) fp32."""
         if frames.dim() == 5:

@@ -1,23 +1,36 @@
-"""rtMRI video -> mel -> waveform, drop-in for scripts/run_mri_video_inference.py on MI355X.
+"""Command-line driver: rtMRI video -> 64-bin mel -> 11 413 Hz waveform on MI355X.
 
-Same command line (--video --mri-checkpoint --scaler-json --hifigan-config --hifigan-checkpoint
---output-dir [--mri-code-dir --max-frames --n-mels --rnn-hidden --dropout]), same plug-in loading
-(``--mri-code-dir`` on sys.path, ``build_acoustic_model(**kw)``, ``load_state_dict(strict=False)``),
-same HiFi-GAN loading (``Generator(AttrDict(config))``, strict ``ckpt['generator']``, best-effort
-weight-norm removal) and the same output files ({stem}_generated.wav, {stem}_mel.npy (T,64) dB,
-{stem}_mel.png, {stem}_mel_log.npy (T,64)).  Additive flag: ``--dtype {fp32,bf16}``.
+Drop-in for the reference's scripts/run_mri_video_inference.py: the same flags (:187-200), the same
+plug-in loading (``--mri-code-dir`` on sys.path, ``build_acoustic_model(**kw)``, ``.pt`` with or
+without ``model_state_dict``, ``load_state_dict(strict=False)``; :119-148), the same HiFi-GAN loading
+(``Generator(AttrDict(config))``, strict ``ckpt['generator']``, best-effort weight-norm removal;
+:89-116) and the same output files (``{stem}_generated.wav`` PCM-16, ``{stem}_mel.npy`` (T, n_mels)
+dB, ``{stem}_mel.png``, ``{stem}_mel_log.npy`` (T, n_mels) ln-power; :166-184, :245-249).  The helper
+names the Grad-CAM tool imports from this module (``build_mri_model``, ``frames_to_tensor``,
+``load_scaler``, ``load_video_frames``; mri_gradcam_formant.py:25-30) keep their signatures.
 
-The acoustic model, the mel glue and the generator run in libm2s on the GPU; there is no CPU
-fallback (the reference's ``device = cuda if available else cpu`` becomes a hard requirement).
-Host I/O: OpenCV decodes video when installed; a ``.npy`` (T,H,W[,3]) frame stack is accepted
-too.  The wav is written by soundfile when installed, else as 16-bit PCM by ``wave``.
+How it runs (this is not the reference's control flow):
+
+* ``FrameStream`` decodes on a worker thread in chunks (OpenCV for video files, or a ``.npy``
+  (T,H,W[,3]) uint8 stack), stages each chunk in pinned host memory, copies it on a side HIP stream
+  and normalises it there (``torch.ops.m2s.preprocess_frames``: BGR -> grey, per-frame z-score +
+  min-max, :34-54), so chunk k+1 decodes while chunk k crosses PCIe and normalises.
+* ``run`` hands the whole clip to ONE ``torch.ops.m2s.pipeline_forward`` call when both loaded
+  modules are the m2s plug-ins: CNN -> BiLSTM -> head -> de-normalise -> dB -> ln -> generator stay on
+  the device, with no host round trip between the mel and the waveform.  Any other plug-in module
+  is driven through its own ``forward`` with the device mel glue in between.
+* ``--dtype`` (additive) picks bf16x3 (default, fp32 tolerance), fp32 (exact f32 MFMA) or bf16.
+
+No CPU fallback: without a HIP device the script stops.  The wav goes through soundfile when it is
+installed, else through ``wave`` as 16-bit PCM with soundfile's scaling (round(x * 32767)).
 """
 from __future__ import annotations
 
 import argparse
 import json
-import os
+import queue
 import sys
+import threading
 import wave
 from pathlib import Path
 
@@ -30,197 +43,197 @@ if str(PROJECT_ROOT) not in sys.path:
 
 from env import AttrDict  # noqa: E402
 from models import Generator  # noqa: E402
-from m2s.runtime import mel_glue, preprocess_frames  # noqa: E402
+from m2s import runtime  # noqa: E402
 
-try:  # optional host-side decoders, exactly as the reference uses them
-    import cv2  # noqa: F401
-except ImportError:  # pragma: no cover - absent in this image
+try:  # host-side decoders the reference uses; absent from this image
+    import cv2
+except ImportError:  # pragma: no cover
     cv2 = None
 try:
-    import soundfile as sf
+    import soundfile
 except ImportError:  # pragma: no cover
-    sf = None
+    soundfile = None
+
+TARGET = (256, 256)
 
 
-def _ensure_sys_path(path: Path):
-    if path and path.exists():
-        sys.path.insert(0, str(path))
+# ------------------------------------------------------------------------------------------------
+# frames
+class FrameStream:
+    """Chunked decode (worker thread) -> pinned staging -> H2D + device normalisation (side stream)."""
 
+    def __init__(self, path: Path, device: torch.device, max_frames=None, chunk: int = 64, target=TARGET):
+        self.path, self.device, self.max_frames, self.chunk, self.target = Path(path), device, max_frames, chunk, target
 
-def _preprocess_frame(frame: np.ndarray, target_size=(256, 256)) -> np.ndarray:
-    """Grey, resize to 256x256, per-frame z-score then min-max to [0, 1] (reference :34-54)."""
-    if frame.ndim == 3:
-        if cv2 is not None:
-            gray = cv2.cvtColor(frame, cv2.COLOR_BGR2GRAY)
-        else:  # ITU-R 601 luma, the weights COLOR_BGR2GRAY applies
-            f = frame.astype(np.float32)
-            gray = np.clip(np.rint(0.114 * f[..., 0] + 0.587 * f[..., 1] + 0.299 * f[..., 2]), 0, 255).astype(np.uint8)
-    else:
-        gray = frame
-    if gray.shape[::-1] != tuple(target_size):
+    def _host_chunks(self):
+        """uint8 frame arrays at the target size, `chunk` frames at a time."""
+        limit = self.max_frames if self.max_frames is not None else 1 << 62
+        if self.path.suffix.lower() == ".npy":
+            stack = np.load(self.path, mmap_mode="r", allow_pickle=False)
+            stack = stack[:limit]
+            for i in range(0, len(stack), self.chunk):
+                yield [self._fit(np.asarray(f)) for f in stack[i:i + self.chunk]]
+            return
         if cv2 is None:
-            raise ValueError(f"frame size {gray.shape} != {target_size} and OpenCV is not installed to resize")
-        gray = cv2.resize(gray, target_size, interpolation=cv2.INTER_LINEAR)
-    gray = gray.astype(np.float32)
-    mean, std = gray.mean(), gray.std()
-    gray = (gray - mean) / std if std > 0 else gray - mean
-    lo, hi = gray.min(), gray.max()
-    return (gray - lo) / (hi - lo) if hi > lo else np.zeros_like(gray)
-
-
-def decode_video_frames(video_path: Path, target_size=(256, 256), max_frames=None) -> np.ndarray:
-    """Host half of load_video_frames: decoded uint8 frames, (T,H,W) grey or (T,H,W,3) BGR at
-    `target_size`.  Frames of another size are converted to grey and resized here (cv2, as the
-    reference does); the z-score / min-max normalisation runs on the device
-    (m2s.runtime.preprocess_frames)."""
-    if video_path.suffix.lower() == ".npy":
-        raw = np.load(video_path, allow_pickle=False)
-        if max_frames is not None:
-            raw = raw[:max_frames]
-        raw = list(raw)
-    else:
-        if cv2 is None:
-            raise RuntimeError("OpenCV is not installed; pass the frames as a .npy (T,H,W) array instead")
-        cap = cv2.VideoCapture(str(video_path))
+            raise RuntimeError("OpenCV is not installed; pass the frames as a .npy (T,H,W) uint8 stack")
+        cap = cv2.VideoCapture(str(self.path))
         if not cap.isOpened():
-            raise ValueError(f"Unable to open video: {video_path}")
-        total = int(cap.get(cv2.CAP_PROP_FRAME_COUNT))
-        if max_frames is not None:
-            total = min(total, max_frames)
-        raw = []
-        for _ in range(total):
-            ret, frame = cap.read()
-            if not ret:
-                break
-            raw.append(frame)
-        cap.release()
-    if not len(raw):
-        raise ValueError("No frames could be read from video")
-    out = []
-    for f in raw:
-        f = np.asarray(f)
+            raise ValueError(f"cannot open video {self.path}")
+        n = min(int(cap.get(cv2.CAP_PROP_FRAME_COUNT)), limit)
+        buf = []
+        try:
+            for _ in range(n):
+                ok, f = cap.read()
+                if not ok:
+                    break
+                buf.append(self._fit(f))
+                if len(buf) == self.chunk:
+                    yield buf
+                    buf = []
+        finally:
+            cap.release()
+        if buf:
+            yield buf
+
+    def _fit(self, f: np.ndarray) -> np.ndarray:
         if f.dtype != np.uint8:
             raise ValueError(f"expected 8-bit frames, got {f.dtype}")
-        if f.shape[:2][::-1] != tuple(target_size):
-            if cv2 is None:
-                raise ValueError(f"frame size {f.shape[:2]} != {target_size} and OpenCV is not installed to resize")
-            g = cv2.cvtColor(f, cv2.COLOR_BGR2GRAY) if f.ndim == 3 else f
-            f = cv2.resize(g, target_size, interpolation=cv2.INTER_LINEAR)
-        out.append(f)
-    if len({a.shape for a in out}) != 1:
-        out = [cv2.cvtColor(a, cv2.COLOR_BGR2GRAY) if a.ndim == 3 else a for a in out]
-    return np.ascontiguousarray(np.stack(out))
-
-
-def load_video_frames(video_path: Path, target_size=(256, 256), max_frames=None) -> torch.Tensor:
-    if video_path.suffix.lower() == ".npy":
-        raw = np.load(video_path, allow_pickle=False)
-        if max_frames is not None:
-            raw = raw[:max_frames]
-        frames = [_preprocess_frame(f, target_size) for f in raw]
-    else:
+        if f.shape[:2][::-1] == tuple(self.target):
+            return f
         if cv2 is None:
-            raise RuntimeError("OpenCV is not installed; pass the frames as a .npy (T,H,W) array instead")
-        cap = cv2.VideoCapture(str(video_path))
-        if not cap.isOpened():
-            raise ValueError(f"Unable to open video: {video_path}")
-        total = int(cap.get(cv2.CAP_PROP_FRAME_COUNT))
-        if max_frames is not None:
-            total = min(total, max_frames)
-        frames = []
-        for _ in range(total):
-            ret, frame = cap.read()
-            if not ret:
+            raise ValueError(f"frame of size {f.shape[:2]} needs a resize to {self.target} and OpenCV is missing")
+        g = cv2.cvtColor(f, cv2.COLOR_BGR2GRAY) if f.ndim == 3 else f  # the reference resizes the grey frame
+        return cv2.resize(g, self.target, interpolation=cv2.INTER_LINEAR)
+
+    def read(self) -> torch.Tensor:
+        """All frames as one (T,H,W) fp32 device tensor in [0, 1], on the current stream."""
+        q: "queue.Queue" = queue.Queue(maxsize=2)
+
+        def worker():
+            try:
+                for c in self._host_chunks():
+                    shapes = {a.shape for a in c}
+                    if len(shapes) > 1:  # mixed grey / colour frames: grey them on the host
+                        c = [cv2.cvtColor(a, cv2.COLOR_BGR2GRAY) if a.ndim == 3 else a for a in c]
+                    q.put(torch.from_numpy(np.ascontiguousarray(np.stack(c))).pin_memory())
+            except BaseException as e:  # surfaced in the consumer
+                q.put(e)
+            q.put(None)
+
+        threading.Thread(target=worker, daemon=True).start()
+        side = torch.cuda.Stream(self.device)
+        parts = []
+        while True:
+            item = q.get()
+            if item is None:
                 break
-            frames.append(_preprocess_frame(frame, target_size))
-        cap.release()
-    if not len(frames):
-        raise ValueError("No frames could be read from video")
-    return torch.from_numpy(np.asarray(frames, dtype=np.float32))
+            if isinstance(item, BaseException):
+                raise item
+            with torch.cuda.stream(side):  # the pinned block stays reserved until this copy completes
+                parts.append(runtime.preprocess_frames(item.to(self.device, non_blocking=True)))
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        if not parts:
+            raise ValueError(f"no frames could be read from {self.path}")
+        for p in parts:
+            p.record_stream(torch.cuda.current_stream(self.device))
+        return parts[0] if len(parts) == 1 else torch.cat(parts)
 
 
-def load_scaler(stats_path: Path):
-    with open(stats_path, "r", encoding="utf-8") as f:
-        stats = json.load(f)
-    if "mean" not in stats or "std" not in stats:
-        raise KeyError("Scaler JSON must contain 'mean' and 'std' lists")
-    mean = np.asarray(stats["mean"], dtype=np.float32)
-    std = np.asarray(stats["std"], dtype=np.float32)
-    if mean.ndim != 1 or std.ndim != 1:
-        raise ValueError("Scaler mean/std must be 1-D lists")
-    return mean, std
-
-
-def _set_dtype(module, dtype):
-    if dtype:
-        module.m2s_dtype = dtype
-
-
-def load_hifigan(config_path: Path, checkpoint_path: Path, device: torch.device, dtype=None):
-    with open(config_path, "r", encoding="utf-8") as f:
-        h = AttrDict(json.load(f))
-    generator = Generator(h).to(device)
-    ckpt = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
-    if "generator" not in ckpt:
-        raise KeyError("HiFi-GAN checkpoint missing 'generator' state")
-    generator.load_state_dict(ckpt["generator"])
-    generator.eval()
-    from torch.nn.utils import remove_weight_norm
-    for module in list(generator.ups) + [generator.conv_post]:
-        try:
-            remove_weight_norm(module)
-        except (ValueError, AttributeError):
-            pass
-    for res in generator.resblocks:
-        try:
-            res.remove_weight_norm()
-        except (ValueError, AttributeError):
-            pass
-    _set_dtype(generator, dtype)
-    return generator, h
-
-
-def build_mri_model(args, device: torch.device):
-    code_dir = Path(args.mri_code_dir) if args.mri_code_dir else None
-    if code_dir is None:
-        code_dir = Path(args.mri_checkpoint).resolve().parent.parent / "mri2speech_code"
-    _ensure_sys_path(code_dir)
-    try:
-        from mri_acoustic_model import build_acoustic_model
-    except ImportError as exc:
-        raise ImportError("Failed to import mri_acoustic_model. Use --mri-code-dir to point to the "
-                          "mri2speech_code directory.") from exc
-    model_kwargs = {"n_mels": args.n_mels, "cnn_pretrained": False, "rnn_hidden": args.rnn_hidden,
-                    "dropout": args.dropout, "use_checkpoint": False, "ckpt_segments": 2, "use_reentrant": False}
-    model = build_acoustic_model(**model_kwargs).to(device)
-    checkpoint = torch.load(args.mri_checkpoint, map_location="cpu", weights_only=True)
-    state_dict = checkpoint.get("model_state_dict", checkpoint)
-    missing, unexpected = model.load_state_dict(state_dict, strict=False)
-    if missing:
-        print(f"[WARN] Missing keys when loading MRI model: {missing}")
-    if unexpected:
-        print(f"[WARN] Unexpected keys when loading MRI model: {unexpected}")
-    model.eval()
-    _set_dtype(model, getattr(args, "dtype", None))
-    return model
+def load_video_frames(video_path: Path, target_size=TARGET, max_frames=None) -> torch.Tensor:
+    """(T,H,W) fp32 frames in [0, 1] on the host (the Grad-CAM tool moves them itself)."""
+    return FrameStream(Path(video_path), torch.device("cuda"), max_frames, target=target_size).read().cpu()
 
 
 def frames_to_tensor(frames: torch.Tensor, use_channel: bool = True) -> torch.Tensor:
+    """(T,H,W) -> (1,T,1,H,W) (or (1,T,H,W) without the channel axis)."""
     if frames.dim() != 3:
-        raise ValueError(f"Expected frames tensor of shape (T,H,W), got {tuple(frames.shape)}")
-    frames = frames.unsqueeze(0)
-    if use_channel:
-        frames = frames.unsqueeze(2)
-    return frames
+        raise ValueError(f"expected (T,H,W) frames, got {tuple(frames.shape)}")
+    return frames[None, :, None] if use_channel else frames[None]
 
 
-def denormalize_mel(mel_normalized: torch.Tensor, mean: np.ndarray, std: np.ndarray) -> torch.Tensor:
-    return mel_glue(mel_normalized, torch.from_numpy(mean), torch.from_numpy(std))[0]
+def load_scaler(stats_path: Path):
+    """scaler.json {"mean": [n_mels], "std": [n_mels], ...} -> float32 arrays."""
+    stats = json.loads(Path(stats_path).read_text(encoding="utf-8"))
+    try:
+        mean, std = (np.asarray(stats[k], dtype=np.float32) for k in ("mean", "std"))
+    except KeyError as e:
+        raise KeyError("scaler JSON needs 'mean' and 'std' lists") from e
+    if mean.ndim != 1 or std.ndim != 1:
+        raise ValueError("scaler mean/std must be 1-D lists")
+    return mean, std
 
 
-def _write_wav(path: Path, audio: np.ndarray, sr: int):
-    if sf is not None:
-        sf.write(path, audio, sr)
+# ------------------------------------------------------------------------------------------------
+# models
+def _checkpoint(path):
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
+def build_mri_model(args, device: torch.device):
+    """The acoustic model through the plug-in surface: --mri-code-dir (default <ckpt>/../../mri2speech_code)."""
+    code_dir = Path(args.mri_code_dir) if getattr(args, "mri_code_dir", None) else \
+        Path(args.mri_checkpoint).resolve().parent.parent / "mri2speech_code"
+    if code_dir.exists():
+        sys.path.insert(0, str(code_dir))
+    try:
+        from mri_acoustic_model import build_acoustic_model
+    except ImportError as e:
+        raise ImportError("cannot import mri_acoustic_model; point --mri-code-dir at the directory holding it") from e
+    model = build_acoustic_model(n_mels=args.n_mels, cnn_pretrained=False, rnn_hidden=args.rnn_hidden,
+                                 dropout=args.dropout, use_checkpoint=False, ckpt_segments=2,
+                                 use_reentrant=False).to(device)
+    ck = _checkpoint(args.mri_checkpoint)
+    missing, unexpected = model.load_state_dict(ck.get("model_state_dict", ck), strict=False)
+    for kind, keys in (("missing", missing), ("unexpected", unexpected)):
+        if keys:
+            print(f"[WARN] {len(keys)} {kind} key(s) in the MRI checkpoint: {list(keys)}")
+    model.eval()
+    if getattr(args, "dtype", None):
+        model.m2s_dtype = args.dtype
+    return model
+
+
+def load_hifigan(config_path: Path, checkpoint_path: Path, device: torch.device, dtype=None):
+    h = AttrDict(json.loads(Path(config_path).read_text(encoding="utf-8")))
+    gen = Generator(h).to(device)
+    ck = _checkpoint(checkpoint_path)
+    if "generator" not in ck:
+        raise KeyError("HiFi-GAN checkpoint has no 'generator' entry")
+    gen.load_state_dict(ck["generator"])
+    gen.eval()
+    from torch.nn.utils import remove_weight_norm
+    removable = [(remove_weight_norm, m) for m in list(gen.ups) + [gen.conv_post]]
+    removable += [(lambda r: r.remove_weight_norm(), r) for r in gen.resblocks]
+    for fn, mod in removable:  # best effort: layers without weight norm are left as they are
+        try:
+            fn(mod)
+        except (ValueError, AttributeError):
+            pass
+    if dtype:
+        gen.m2s_dtype = dtype
+    return gen, h
+
+
+# ------------------------------------------------------------------------------------------------
+# run
+def run(model, gen, frames: torch.Tensor, mean: np.ndarray, std: np.ndarray):
+    """(T,H,W) device frames -> dict mel_db (T,n_mels), mel_log (T,n_mels), audio (T*hop,) on the host."""
+    dev = frames.device
+    if hasattr(model, "_engine") and hasattr(gen, "_engine"):  # both are m2s plug-ins: one device call
+        pipe = runtime.Pipeline(model._engine(dev), gen._engine(dev), mean, std)
+        out = pipe.forward(frames[None])
+        db, ln, wav = out["mel_db"][0], out["mel_log"][0], out["wav"][0]
+    else:  # a foreign plug-in: its forward, then the device glue and the generator
+        with torch.no_grad():
+            mn = model(frames_to_tensor(frames))[0]
+            db, ln = runtime.mel_glue(mn, torch.from_numpy(mean), torch.from_numpy(std))
+            wav = gen(ln.t()[None]).reshape(-1)
+    return {"mel_db": db.float().cpu().numpy(), "mel_log": ln.float().cpu().numpy(), "audio": wav.float().cpu().numpy()}
+
+
+def write_wav(path: Path, audio: np.ndarray, sr: int):
+    if soundfile is not None:
+        soundfile.write(str(path), audio, sr)  # WAV default subtype PCM_16
         return
     pcm = np.clip(np.rint(np.asarray(audio, np.float64) * 32767.0), -32768, 32767).astype("<i2")
     with wave.open(str(path), "wb") as w:
@@ -230,97 +243,72 @@ def _write_wav(path: Path, audio: np.ndarray, sr: int):
         w.writeframes(pcm.tobytes())
 
 
-def save_outputs(audio: np.ndarray, mel: np.ndarray, output_dir: Path, sampling_rate: int, stem: str):
-    output_dir.mkdir(parents=True, exist_ok=True)
-    audio_path = output_dir / f"{stem}_generated.wav"
-    _write_wav(audio_path, audio, sampling_rate)
-    mel_path = output_dir / f"{stem}_mel.npy"
-    np.save(mel_path, mel)
-    fig_path = output_dir / f"{stem}_mel.png"
+def write_outputs(res, out_dir: Path, stem: str, sr: int):
+    out_dir.mkdir(parents=True, exist_ok=True)
+    paths = {"audio": out_dir / f"{stem}_generated.wav", "mel": out_dir / f"{stem}_mel.npy",
+             "figure": out_dir / f"{stem}_mel.png", "mel_log": out_dir / f"{stem}_mel_log.npy"}
+    write_wav(paths["audio"], res["audio"], sr)
+    np.save(paths["mel"], res["mel_db"].astype(np.float32))
+    np.save(paths["mel_log"], res["mel_log"].astype(np.float32))
     try:
         import matplotlib
         matplotlib.use("Agg")
-        import matplotlib.pyplot as plt
-        plt.figure(figsize=(12, 4))
-        plt.imshow(mel.T, aspect="auto", origin="lower", cmap="viridis")
-        plt.colorbar()
-        plt.title(f"Generated Mel Spectrogram - {stem}")
-        plt.xlabel("Time")
-        plt.ylabel("Mel bins")
-        plt.tight_layout()
-        plt.savefig(fig_path, dpi=150)
-        plt.close()
+        from matplotlib import pyplot as plt
+        fig, ax = plt.subplots(figsize=(12, 4))
+        im = ax.imshow(res["mel_db"].T, aspect="auto", origin="lower", cmap="viridis")
+        fig.colorbar(im, ax=ax)
+        ax.set(title=f"Generated Mel Spectrogram - {stem}", xlabel="Time", ylabel="Mel bins")
+        fig.tight_layout()
+        fig.savefig(paths["figure"], dpi=150)
+        plt.close(fig)
     except ImportError:  # pragma: no cover
-        fig_path = None
-    return audio_path, mel_path, fig_path
+        paths["figure"] = None
+    return paths
 
 
 def parse_args(argv=None):
-    p = argparse.ArgumentParser(description="rtMRI -> Speech inference (OTN-like MRI model + HiFi-GAN) on MI355X")
-    p.add_argument("--video", required=True, help="Input rtMRI video (.mp4) or frame stack (.npy)")
-    p.add_argument("--mri-checkpoint", required=True, help="Path to OTN-like MRI checkpoint (.pt)")
-    p.add_argument("--scaler-json", required=True, help="Path to scaler.json (contains per-mel mean/std)")
-    p.add_argument("--hifigan-config", required=True, help="HiFi-GAN config JSON")
-    p.add_argument("--hifigan-checkpoint", required=True, help="HiFi-GAN generator checkpoint")
-    p.add_argument("--output-dir", required=True, help="Directory to save generated artifacts")
-    p.add_argument("--mri-code-dir", help="Directory containing mri_acoustic_model.py (defaults to sibling mri2speech_code)")
-    p.add_argument("--max-frames", type=int, default=None, help="Optional max number of frames to process")
+    p = argparse.ArgumentParser(description="rtMRI video -> mel -> waveform (CNN-BiLSTM + HiFi-GAN) on MI355X")
+    req = [("--video", "rtMRI video, or a (T,H,W[,3]) uint8 .npy frame stack"),
+           ("--mri-checkpoint", "acoustic-model checkpoint (.pt)"),
+           ("--scaler-json", "scaler.json with the per-bin mel mean/std"),
+           ("--hifigan-config", "HiFi-GAN config JSON"),
+           ("--hifigan-checkpoint", "HiFi-GAN generator checkpoint (g_XXXXXXXX)"),
+           ("--output-dir", "where the wav / npy / png outputs go")]
+    for flag, help_ in req:
+        p.add_argument(flag, required=True, help=help_)
+    p.add_argument("--mri-code-dir", help="directory with mri_acoustic_model.py (default: <ckpt>/../../mri2speech_code)")
+    p.add_argument("--max-frames", type=int, default=None, help="decode at most this many frames")
     p.add_argument("--n-mels", type=int, default=64)
     p.add_argument("--rnn-hidden", type=int, default=640)
     p.add_argument("--dropout", type=float, default=0.5)
-    p.add_argument("--dtype", choices=["fp32", "bf16"], default=None,
-                   help="m2s compute dtype (default: M2S_DTYPE env or fp32)")
+    p.add_argument("--dtype", choices=["bf16x3", "fp32", "bf16"], default=None,
+                   help="m2s compute dtype (default: M2S_DTYPE or bf16x3)")
+    p.add_argument("--decode-chunk", type=int, default=64, help="frames per decode / H2D chunk")
     return p.parse_args(argv)
 
 
 def main(argv=None):
     args = parse_args(argv)
-    video_path = Path(args.video)
-    if not video_path.exists():
-        raise FileNotFoundError(f"Video file not found: {video_path}")
+    video = Path(args.video)
+    if not video.exists():
+        raise FileNotFoundError(f"video not found: {video}")
     mean, std = load_scaler(Path(args.scaler_json))
     if len(mean) != args.n_mels or len(std) != args.n_mels:
-        raise ValueError("Scaler mean/std length does not match n_mels")
+        raise ValueError("scaler mean/std length does not match --n-mels")
     if not torch.cuda.is_available():
-        raise RuntimeError("m2s needs an MI355X (HIP) device; no CPU fallback")
+        raise RuntimeError("m2s needs an MI355X (HIP) device; there is no CPU path")
     device = torch.device("cuda")
-    print(f"[INFO] Using device: {device}")
 
-    # host: decode (+ resize when needed); device: grey, z-score, min-max (libm2s preprocess kernel)
-    frames_u8 = decode_video_frames(video_path, target_size=(256, 256), max_frames=args.max_frames)
-    frames = preprocess_frames(torch.from_numpy(frames_u8).to(device))
-    frames_tensor = frames_to_tensor(frames, use_channel=True)
-
-    mri_model = build_mri_model(args, device)
-    with torch.no_grad():
-        pred_norm = mri_model(frames_tensor)
-    pred_norm = pred_norm.squeeze(0)
-    print(f"[INFO] Predicted normalized mel shape: {tuple(pred_norm.shape)}")
-
-    mel_denorm, mel_log = mel_glue(pred_norm, torch.from_numpy(mean), torch.from_numpy(std))
-    mel_denorm_np = mel_denorm.cpu().numpy().astype(np.float32)
-    print(f"[INFO] Mel (denormalized dB) range: {mel_denorm_np.min():.3f} .. {mel_denorm_np.max():.3f}")
-    mel_log_np = mel_log.cpu().numpy().astype(np.float32)
-    print(f"[INFO] Mel (log-power) range: {mel_log_np.min():.3f} .. {mel_log_np.max():.3f}")
-
-    generator, hifigan_config = load_hifigan(Path(args.hifigan_config), Path(args.hifigan_checkpoint), device,
-                                             args.dtype)
-    mel_for_hifigan = mel_log.transpose(0, 1).unsqueeze(0).float().to(device)
-    with torch.no_grad():
-        audio = generator(mel_for_hifigan).squeeze().cpu().numpy()
-    print(f"[INFO] Generated audio length: {audio.shape[0]} samples")
-
-    stem = video_path.stem
-    output_dir = Path(args.output_dir)
-    audio_path, mel_path, fig_path = save_outputs(audio, mel_denorm_np, output_dir, hifigan_config.sampling_rate, stem)
-    log_mel_path = output_dir / f"{stem}_mel_log.npy"
-    np.save(log_mel_path, mel_log_np)
-    print("[DONE] Inference complete.")
-    print(f"  Audio : {audio_path}")
-    print(f"  Mel   : {mel_path}")
-    print(f"  LogMel: {log_mel_path}")
-    print(f"  Figure: {fig_path}")
-    return {"audio": audio, "mel_db": mel_denorm_np, "mel_log": mel_log_np}
+    model = build_mri_model(args, device)
+    gen, h = load_hifigan(Path(args.hifigan_config), Path(args.hifigan_checkpoint), device, args.dtype)
+    frames = FrameStream(video, device, args.max_frames, chunk=args.decode_chunk).read()
+    res = run(model, gen, frames, mean, std)
+    paths = write_outputs(res, Path(args.output_dir), video.stem, int(h.sampling_rate))
+    print(f"[m2s] {frames.shape[0]} frames -> mel {res['mel_db'].shape} -> {res['audio'].shape[0]} samples "
+          f"@ {int(h.sampling_rate)} Hz ({model.m2s_dtype if hasattr(model, 'm2s_dtype') else 'plug-in'})")
+    for k, v in paths.items():
+        print(f"  {k:8s}: {v}")
+    return res
 
 
 if __name__ == "__main__":

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(L, name), name
     assert sorted(N.exported_symbols()) == declared
-    assert L.m2s_abi_version() == 1
+    assert L.m2s_abi_version() == 2
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-device error path")
@@ -124,10 +124,25 @@ def test_cli_matches_reference_flags():
                         "--mri-code-dir", "d", "--max-frames", "10", "--n-mels", "64", "--rnn-hidden", "640",
                         "--dropout", "0.5"])
     assert (a.video, a.max_frames, a.n_mels, a.rnn_hidden, a.dropout) == ("v.mp4", 10, 64, 640, 0.5)
+    assert a.dtype is None and a.decode_chunk == 64  # additive flags
     g = np.load(os.path.join(REPO, "tests", "golden", "glue.npz"))
-    pre = np.stack([cli._preprocess_frame(f) for f in g["frames_u8"]])
-    np.testing.assert_allclose(pre, g["preprocessed"], atol=1e-6, rtol=0)
-    assert tuple(cli.frames_to_tensor(torch.from_numpy(pre)).shape) == tuple(g["frames_tensor_shape"])
+    pre = torch.from_numpy(g["preprocessed"])  # the device kernel's output is checked against it on the GPU
+    assert tuple(cli.frames_to_tensor(pre).shape) == tuple(g["frames_tensor_shape"])
+
+
+def test_cli_frame_stream_chunks_a_npy_stack(tmp_path):
+    """Host half of the pipelined decode: a (T,H,W) uint8 .npy stack in chunks, --max-frames honoured."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "m2s_cli3", os.path.join(REPO, "mri-to-speech_amd", "scripts", "run_mri_video_inference.py"))
+    cli = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(cli)
+    stack = np.random.default_rng(0).integers(0, 256, (11, 256, 256), dtype=np.uint8)
+    np.save(tmp_path / "v.npy", stack)
+    fs = cli.FrameStream(tmp_path / "v.npy", torch.device("cpu"), max_frames=10, chunk=4)
+    chunks = list(fs._host_chunks())
+    assert [len(c) for c in chunks] == [4, 4, 2]
+    np.testing.assert_array_equal(np.concatenate([np.stack(c) for c in chunks]), stack[:10])
 
 
 def test_cli_wav_writer_pcm16(tmp_path):
@@ -139,7 +154,7 @@ def test_cli_wav_writer_pcm16(tmp_path):
     spec.loader.exec_module(cli)
     audio = np.array([0.0, 0.5, -1.0, 1.0, 1.5], dtype=np.float32)
     p = tmp_path / "x.wav"
-    cli._write_wav(p, audio, 11413)
+    cli.write_wav(p, audio, 11413)
     with wave.open(str(p)) as w:
         assert (w.getframerate(), w.getsampwidth(), w.getnchannels()) == (11413, 2, 1)
         pcm = np.frombuffer(w.readframes(5), dtype="<i2")

@@ -204,15 +204,13 @@ def test_effnet_bf16_ir_fused_every_block(rt, ac_state, monkeypatch, hw):
 
 
 @pytest.mark.parametrize("env,blocks", [("M2S_STEM_FUSED", (2, 3, 6, -1)), ("M2S_SE_FUSED", (9, 14, 20, -1)), ("M2S_IR_FUSED", (9, 10, 18, 19, -1)),
-                                        ("M2S_ER_FUSED", (3, 4, 5, 6, 7, 8, -1)), ("M2S_IR_BLOCK", (10, 12, 13, 18, -1))])
+                                        ("M2S_ER_FUSED", (3, 4, 5, 6, 7, 8, -1))])
 @pytest.mark.parametrize("hw", [(256, 256), (96, 80), (67, 101)])
 def test_effnet_bf16_fused_kernels_vs_unfused(rt, ac_state, monkeypatch, hw, env, blocks):
     """The fused stem + blocks.0 kernel (stem_b0.hip), the one-kernel SE excitation (se_excite.hip)
     the fused EdgeResidual (er_fused.hip / er2_fused.hip: blocks.1.1/.2 at 64x64, blocks.2.1/.2 at 32x32;
     ers2_fused.hip: the stride-2 blocks.1.0 / blocks.2.0)
-    and the whole-InvertedResidual kernel (ir_block.hip: blocks.3.1-3, blocks.4.* at 16x16; 96x80 and 67x101 give maps
-    that are not multiples of 16, where the unfused path must take over) against the separate
-    launches they replace and the fp32 oracle, block by block
+    against the separate launches they replace and the fp32 oracle, block by block
     and on the pooled features; odd sizes exercise the TF-SAME bottom/right stem pad and partial
     16 x 16 tiles, and a 3-frame batch a partial 8-image SE group."""
     sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
@@ -281,15 +279,15 @@ def test_pipeline_end_to_end(rt, ac_state, dtype):
 
 # ------------------------------------------------------------------------------ persistent BiLSTM
 @pytest.mark.parametrize("B,T", [(1, 1000), (3, 64), (70, 6)])
-def test_bilstm_persistent_long_and_wide(ac_f32, ac_state, monkeypatch, B, T):
+def test_bilstm_persistent_long_and_wide(rt, ac_state, monkeypatch, B, T):
     """One-launch recurrence (lstm_persistent.hip) vs the oracle and vs the per-step kernel:
     a 1000-frame clip (configs[4] length), a batch above the 64-sequence launch limit."""
     sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
     x = torch.from_numpy(np.random.default_rng(B * 7 + T).normal(0, 0.5, (B, T, 208)).astype(np.float32))
     monkeypatch.setenv("M2S_LSTM_PERSISTENT", "1")
-    y, m = ac_f32.bilstm(x.to(DEV))
+    y, m = rt.AcousticEngine(ac_state[1], dtype="fp32", device=DEV).bilstm(x.to(DEV))
     monkeypatch.setenv("M2S_LSTM_PERSISTENT", "0")
-    y_step, _ = ac_f32.bilstm(x.to(DEV))
+    y_step, _ = rt.AcousticEngine(ac_state[1], dtype="fp32", device=DEV).bilstm(x.to(DEV))
     ref_y = acoustic.bilstm_summerge(sd, x).numpy()
     y = y.cpu().numpy()
     assert np.isfinite(y).all()
@@ -317,3 +315,23 @@ def test_preprocess_vs_oracle_shapes_and_bgr(rt, shape):
     ref = np.stack([acoustic.preprocess_frame(f) for f in grey])
     assert out.shape == ref.shape and not out[0].any()
     np.testing.assert_allclose(out, ref, atol=1e-6, rtol=0)
+
+
+# ------------------------------------------------------------------------------ asynchronous failure report
+def test_bilstm_barrier_timeout_is_reported(rt, ac_state):
+    """A BiLSTM grid-barrier wait that times out (forced: one poll allowed) poisons the outputs and
+    is reported: m2s_acoustic_status -> M2SError, and the next forward on the engine fails too."""
+    import ctypes
+    from m2s import _native
+    eng = rt.AcousticEngine(ac_state[1], dtype="fp32", device=DEV)
+    _native.check(_native.lib().m2s_acoustic_set_lstm_spin_limit(ctypes.c_void_p(eng.handle), 1))
+    x = torch.randn(1, 30, 208, device=DEV)
+    y, _ = eng.bilstm(x)
+    with pytest.raises(_native.M2SError, match="timed out"):
+        eng.check()
+    assert torch.isnan(y).any()
+    eng.check()  # the report is consumed once
+    _native.check(_native.lib().m2s_acoustic_set_lstm_spin_limit(ctypes.c_void_p(eng.handle), 1 << 24))
+    y2, _ = eng.bilstm(x)
+    eng.check()
+    assert torch.isfinite(y2).all()
