@@ -54,12 +54,12 @@ void launch_rb1_fused(const bf16_t* x, bf16_t* s, int B, int L, int C, int k, in
                       const float* const* b2, int kp, int accum, float div, double flops, double bytes,
                       hipStream_t st);
 
-// bf16 conv_stem + bn1 + SiLU + blocks.0.0 (3x3 32->16 + SiLU) + blocks.0.1 (3x3 16->16 + SiLU + skip)
-// in one kernel: frames (N,H,W) fp32 -> y (N,OH,OW,16).  w0/w1: packed conv rows (kp 288 / 160).
-// (stem_b0.hip)
+// conv_stem + bn1 + SiLU + blocks.0.0 (3x3 32->16 + SiLU) + blocks.0.1 (3x3 16->16 + SiLU + skip) in
+// one kernel: frames (N,H,W) fp32 -> y (N,OH,OW,16).  w0/w1: packed conv rows (kp 288 / 160); bf16, or
+// split fp32 (`split`: [hi | lo] weight rows, y in sp_t layout).  (stem_b0.hip)
 void launch_stem_b0(const float* frames, int N, int H, int W, int OH, int OW, int pad_t, int pad_l, const float* w9,
-                    const float* b9, const bf16_t* w0, const float* b0, int kp0, const bf16_t* w1, const float* b1,
-                    int kp1, bf16_t* y, double flops, double bytes, hipStream_t s);
+                    const float* b9, const void* w0, const float* b0, int kp0, const void* w1, const float* b1,
+                    int kp1, void* y, bool split, double flops, double bytes, hipStream_t s);
 
 // bf16 SqueezeExcite excitation: gate (N, cs_mid) = sigmoid(W2 · SiLU(W1 · mean + b1) + b2), mean (N, cs_mid)
 // from the squeeze; w1 packed [>= rd][kp1], w2 packed [>= mid][kp2].  (se_excite.hip)

@@ -539,7 +539,8 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
     same_pad(H, 3, 2, &oh, &pt);
     same_pad(W, 3, 2, &ow, &pl);
     // stem + blocks.0 (two 3x3 ConvBnAct at stride 1: 32 -> 16, 16 -> 16 + skip) in one kernel
-    const bool front = std::is_same<T, bf16_t>::value && stem_fused_ && !(probe && stop_after >= 0 && stop_after < 2) &&
+    constexpr bool SPL = std::is_same<T, sp_t>::value;
+    const bool front = (std::is_same<T, bf16_t>::value || SPL) && stem_fused_ && !(probe && stop_after >= 0 && stop_after < 2) &&
                        blocks_.size() >= 2 && blocks_[0].type == 0 && blocks_[0].stride == 1 && !blocks_[0].skip &&
                        blocks_[0].cout == 16 && blocks_[0].c1.cs_in == 32 && blocks_[0].c1.kp == 288 &&
                        blocks_[1].type == 0 && blocks_[1].stride == 1 && blocks_[1].skip && blocks_[1].cout == 16 &&
@@ -551,10 +552,9 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
     if (front) {
       const double px = (double)nc * oh * ow;
       launch_stem_b0(frames + (size_t)n0 * H * W, nc, H, W, oh, ow, pt, pl, static_cast<const float*>(arena_.ptr(stem_w_)),
-                     static_cast<const float*>(arena_.ptr(stem_b_)), static_cast<const bf16_t*>(blocks_[0].c1.w),
-                     blocks_[0].c1.b, blocks_[0].c1.kp, static_cast<const bf16_t*>(blocks_[1].c1.w), blocks_[1].c1.b,
-                     blocks_[1].c1.kp, reinterpret_cast<bf16_t*>(A),
-                     2.0 * px * (EFF_STEM * 9 + 16 * 9 * 32 + 16 * 9 * 16), 4.0 * nc * H * W + 2.0 * px * 16, s);
+                     static_cast<const float*>(arena_.ptr(stem_b_)), blocks_[0].c1.w, blocks_[0].c1.b, blocks_[0].c1.kp,
+                     blocks_[1].c1.w, blocks_[1].c1.b, blocks_[1].c1.kp, A, SPL,
+                     2.0 * px * (EFF_STEM * 9 + 16 * 9 * 32 + 16 * 9 * 16), 4.0 * nc * H * W + (SPL ? 4.0 : 2.0) * px * 16, s);
       cc = 16;
       bi = 2;
     } else {

@@ -15,6 +15,9 @@
 //   phase 3  blocks.0.1 likewise (16 x 160: two taps of 16 channels per K step), + skip from A.
 // Both LDS images are planar ([16-byte chunk][pixel]) so a B-fragment read of 16 consecutive
 // pixels is bank-conflict free at any tap offset (see mrf_fused.hip).
+// Split fp32 (SP = 1, m2s_common.hpp sp_t): S and A keep a hi and a lo plane set (double the LDS,
+// two workgroups per CU), the conv weights come as [hi kp | lo kp] rows (A fragments hi and lo
+// resident), every product is the three MFMA terms and y is written as (N, OH, OW, [hi 16 | lo 16]).
 #include <algorithm>
 #include <cstdio>
 
@@ -32,16 +35,23 @@ struct StemB0Args {
   const float* frames;  // (N, H, W) fp32
   const float* w9;      // stem [32][9] (grey repeat folded), BN folded
   const float* b9;      // [32]
-  const bf16_t* w0;     // blocks.0.0 packed [>=16][kp0 = 288]
+  const bf16_t* w0;     // blocks.0.0 packed [>=16][kp0 = 288] (SP: [hi kp0 | lo kp0] rows)
   const float* b0;
-  const bf16_t* w1;     // blocks.0.1 packed [>=16][kp1 = 160]
+  const bf16_t* w1;     // blocks.0.1 packed [>=16][kp1 = 160] (SP: [hi kp1 | lo kp1] rows)
   const float* b1;
-  bf16_t* y;            // (N, OH, OW, 16)
+  bf16_t* y;            // (N, OH, OW, 16) (SP: (N, OH, OW, [hi 16 | lo 16]))
   int N, H, W, OH, OW, pad_t, pad_l, kp0, kp1, tiles_x, tiles_y;
 };
 
-template <int TH>
-__global__ void __launch_bounds__(256, 4) stem_b0_kernel(const StemB0Args a) {
+__device__ __forceinline__ bf16x8 frag(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ f32x4 mma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+}
+
+template <int TH, int SP>
+__global__ void __launch_bounds__(256, SP ? 2 : 4) stem_b0_kernel(const StemB0Args a) {
   constexpr int SH = TH + 4, AH = TH + 2;
   constexpr int SPIX = SH * SB_SW, APIX = AH * SB_AW;
   constexpr int APIX_PAD = (APIX + 15) / 16 * 16;
@@ -50,8 +60,10 @@ __global__ void __launch_bounds__(256, 4) stem_b0_kernel(const StemB0Args a) {
   constexpr int ASUB = APIX_PAD / 16;                         // A position subtiles
   constexpr int AMS = (ASUB + 3) / 4;                         // ... per wave, at most
   constexpr int OMS = TH / 4;                                 // output subtiles (rows) per wave
-  __shared__ __attribute__((aligned(16))) char sS[4 * SPLANE];
-  __shared__ __attribute__((aligned(16))) char sA[2 * APLANE];
+  constexpr int R = SP ? 2 : 1;  // plane sets: hi (+ lo)
+  __shared__ __attribute__((aligned(16))) char sS[R * 4 * SPLANE];
+  __shared__ __attribute__((aligned(16))) char sA[R * 2 * APLANE];
+  constexpr int SLO = 4 * SPLANE, ALO = 2 * APLANE;  // offset of the lo plane set
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -87,7 +99,7 @@ __global__ void __launch_bounds__(256, 4) stem_b0_kernel(const StemB0Args a) {
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      uint32_t v[2][4];
+      uint32_t v[2][4], vl[2][4];
 #pragma unroll
       for (int j = 0; j < 8; j += 2) {
         const float bj0 = a.b9[q * 8 + j], bj1 = a.b9[q * 8 + j + 1];
@@ -100,20 +112,39 @@ __global__ void __launch_bounds__(256, 4) stem_b0_kernel(const StemB0Args a) {
           c0 += w0 * in[1][t];
           c1 += w1 * in[1][t];
         }
-        v[0][j / 2] = ok[0] ? pack_bf16x2(silu(a0), silu(a1)) : 0u;
-        v[1][j / 2] = ok[1] ? pack_bf16x2(silu(c0), silu(c1)) : 0u;
+        const float s0 = silu(a0), s1 = silu(a1), t0 = silu(c0), t1 = silu(c1);
+        v[0][j / 2] = ok[0] ? pack_bf16x2(s0, s1) : 0u;
+        v[1][j / 2] = ok[1] ? pack_bf16x2(t0, t1) : 0u;
+        if constexpr (SP) {  // lo halves: v - hi
+          vl[0][j / 2] = ok[0] ? pack_bf16x2(s0 - __uint_as_float(v[0][j / 2] << 16),
+                                             s1 - __uint_as_float(v[0][j / 2] & 0xffff0000u)) : 0u;
+          vl[1][j / 2] = ok[1] ? pack_bf16x2(t0 - __uint_as_float(v[1][j / 2] << 16),
+                                             t1 - __uint_as_float(v[1][j / 2] & 0xffff0000u)) : 0u;
+        }
       }
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+      for (int h = 0; h < 2; ++h) {
         *reinterpret_cast<uint4*>(sS + q * SPLANE + pix[h] * 16) = make_uint4(v[h][0], v[h][1], v[h][2], v[h][3]);
+        if constexpr (SP)
+          *reinterpret_cast<uint4*>(sS + SLO + q * SPLANE + pix[h] * 16) =
+              make_uint4(vl[h][0], vl[h][1], vl[h][2], vl[h][3]);
+      }
     }
   }
   // resident weights of both convs (A fragments), in flight across the barrier
-  bf16x8 wf0[9], wf1[5];
+  bf16x8 wf0[9], wf1[5], wl0[SP ? 9 : 1], wl1[SP ? 5 : 1];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) wf0[t] = *reinterpret_cast<const bf16x8*>(a.w0 + (size_t)r16 * a.kp0 + t * 32 + 8 * g);
+  for (int t = 0; t < 9; ++t) {
+    const bf16_t* w = a.w0 + (size_t)r16 * a.kp0 * R + t * 32 + 8 * g;
+    wf0[t] = *reinterpret_cast<const bf16x8*>(w);
+    if constexpr (SP) wl0[t] = *reinterpret_cast<const bf16x8*>(w + a.kp0);
+  }
 #pragma unroll
-  for (int t = 0; t < 5; ++t) wf1[t] = *reinterpret_cast<const bf16x8*>(a.w1 + (size_t)r16 * a.kp1 + t * 32 + 8 * g);
+  for (int t = 0; t < 5; ++t) {
+    const bf16_t* w = a.w1 + (size_t)r16 * a.kp1 * R + t * 32 + 8 * g;
+    wf1[t] = *reinterpret_cast<const bf16x8*>(w);
+    if constexpr (SP) wl1[t] = *reinterpret_cast<const bf16x8*>(w + a.kp1);
+  }
   __syncthreads();
 
   // ---- phase 2: blocks.0.0 (32 -> 16) on MFMA -> A --------------------------------------------
@@ -134,8 +165,11 @@ __global__ void __launch_bounds__(256, 4) stem_b0_kernel(const StemB0Args a) {
 #pragma unroll
       for (int i = 0; i < AMS; ++i) {
         if (wave + 4 * i < ASUB) {
-          const bf16x8 b = *reinterpret_cast<const bf16x8*>(sS + sbase[i] + toff);
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[t], b, acc[i], 0, 0, 0);
+          const bf16x8 b = frag(sS + sbase[i] + toff);
+          if constexpr (SP)
+            acc[i] = mma3(wf0[t], wl0[t], b, frag(sS + SLO + sbase[i] + toff), acc[i]);
+          else
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[t], b, acc[i], 0, 0, 0);
         }
       }
     }
@@ -146,12 +180,19 @@ __global__ void __launch_bounds__(256, 4) stem_b0_kernel(const StemB0Args a) {
       if (wave + 4 * i >= ASUB || pa >= APIX) continue;
       const int ay = pa / SB_AW, ax = pa - (pa / SB_AW) * SB_AW;
       const int oy = ty0 - 1 + ay, ox = tx0 - 1 + ax;
-      uint2 u = make_uint2(0u, 0u);
+      uint2 u = make_uint2(0u, 0u), ul = make_uint2(0u, 0u);
       if (oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW) {
-        u.x = pack_bf16x2(silu(acc[i][0] + bb.x), silu(acc[i][1] + bb.y));
-        u.y = pack_bf16x2(silu(acc[i][2] + bb.z), silu(acc[i][3] + bb.w));
+        const float v[4] = {silu(acc[i][0] + bb.x), silu(acc[i][1] + bb.y), silu(acc[i][2] + bb.z),
+                            silu(acc[i][3] + bb.w)};
+        if constexpr (SP) {
+          split4(v, u, ul);
+        } else {
+          u.x = pack_bf16x2(v[0], v[1]);
+          u.y = pack_bf16x2(v[2], v[3]);
+        }
       }
       *reinterpret_cast<uint2*>(sA + (g >> 1) * APLANE + pa * 16 + (g & 1) * 8) = u;
+      if constexpr (SP) *reinterpret_cast<uint2*>(sA + ALO + (g >> 1) * APLANE + pa * 16 + (g & 1) * 8) = ul;
     }
   }
   __syncthreads();
@@ -175,8 +216,11 @@ __global__ void __launch_bounds__(256, 4) stem_b0_kernel(const StemB0Args a) {
 #pragma unroll
       for (int i = 0; i < OMS; ++i) {
         const int row = wave + 4 * i;  // output tile row = subtile
-        const bf16x8 b = *reinterpret_cast<const bf16x8*>(sA + (row * SB_AW + r16) * 16 + toff[st]);
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[st], b, acc[i], 0, 0, 0);
+        const char* p = sA + (row * SB_AW + r16) * 16 + toff[st];
+        if constexpr (SP)
+          acc[i] = mma3(wf1[st], wl1[st], frag(p), frag(p + ALO), acc[i]);
+        else
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[st], frag(p), acc[i], 0, 0, 0);
       }
     const float4 bb = *reinterpret_cast<const float4*>(a.b1 + 4 * g);
     const int ox = tx0 + r16;
@@ -184,14 +228,26 @@ __global__ void __launch_bounds__(256, 4) stem_b0_kernel(const StemB0Args a) {
     for (int i = 0; i < OMS; ++i) {
       const int row = wave + 4 * i, oy = ty0 + row;
       if (oy >= a.OH || ox >= a.OW) continue;
-      const uint2 r = *reinterpret_cast<const uint2*>(sA + (g >> 1) * APLANE + ((row + 1) * SB_AW + r16 + 1) * 16 +
-                                                      (g & 1) * 8);
-      const float v0 = silu(acc[i][0] + bb.x) + __uint_as_float(r.x << 16);
-      const float v1 = silu(acc[i][1] + bb.y) + __uint_as_float(r.x & 0xffff0000u);
-      const float v2 = silu(acc[i][2] + bb.z) + __uint_as_float(r.y << 16);
-      const float v3 = silu(acc[i][3] + bb.w) + __uint_as_float(r.y & 0xffff0000u);
-      *reinterpret_cast<uint2*>(a.y + (((size_t)n * a.OH + oy) * a.OW + ox) * 16 + 4 * g) =
-          make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+      const int soff = (g >> 1) * APLANE + ((row + 1) * SB_AW + r16 + 1) * 16 + (g & 1) * 8;
+      float r[4];
+      unpack_bf16x4(*reinterpret_cast<const uint2*>(sA + soff), r);
+      if constexpr (SP) {
+        float rl[4];
+        unpack_bf16x4(*reinterpret_cast<const uint2*>(sA + ALO + soff), rl);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] += rl[j];
+      }
+      const float v[4] = {silu(acc[i][0] + bb.x) + r[0], silu(acc[i][1] + bb.y) + r[1], silu(acc[i][2] + bb.z) + r[2],
+                          silu(acc[i][3] + bb.w) + r[3]};
+      bf16_t* yo = a.y + (((size_t)n * a.OH + oy) * a.OW + ox) * 16 * R + 4 * g;
+      if constexpr (SP) {
+        uint2 h, l;
+        split4(v, h, l);
+        *reinterpret_cast<uint2*>(yo) = h;
+        *reinterpret_cast<uint2*>(yo + 16) = l;
+      } else {
+        *reinterpret_cast<uint2*>(yo) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      }
     }
   }
 }
@@ -199,19 +255,19 @@ __global__ void __launch_bounds__(256, 4) stem_b0_kernel(const StemB0Args a) {
 }  // namespace
 
 void launch_stem_b0(const float* frames, int N, int H, int W, int OH, int OW, int pad_t, int pad_l, const float* w9,
-                    const float* b9, const bf16_t* w0, const float* b0, int kp0, const bf16_t* w1, const float* b1,
-                    int kp1, bf16_t* y, double flops, double bytes, hipStream_t s) {
+                    const float* b9, const void* w0, const float* b0, int kp0, const void* w1, const float* b1,
+                    int kp1, void* y, bool split, double flops, double bytes, hipStream_t s) {
   M2S_CHECK(kp0 == 288 && kp1 == 160 && N > 0 && OH > 0 && OW > 0, "stem_b0: unsupported shape");
   constexpr int TH = 16;
   StemB0Args a;
   a.frames = frames;
   a.w9 = w9;
   a.b9 = b9;
-  a.w0 = w0;
+  a.w0 = static_cast<const bf16_t*>(w0);
   a.b0 = b0;
-  a.w1 = w1;
+  a.w1 = static_cast<const bf16_t*>(w1);
   a.b1 = b1;
-  a.y = y;
+  a.y = static_cast<bf16_t*>(y);
   a.N = N;
   a.H = H;
   a.W = W;
@@ -224,8 +280,13 @@ void launch_stem_b0(const float* frames, int N, int H, int W, int OH, int OW, in
   a.tiles_x = ceil_div(OW, SB_TW);
   a.tiles_y = ceil_div(OH, TH);
   M2S_CHECK((double)N * a.tiles_x * a.tiles_y < 2147483647.0, "stem_b0: grid");
-  ProfScope ps("stem_b0_kernel<16>", flops, bytes, s);
-  hipLaunchKernelGGL(stem_b0_kernel<TH>, dim3(N * a.tiles_x * a.tiles_y), dim3(256), 0, s, a);
+  if (split) {
+    ProfScope ps("stem_b0_kernel<16, 1>", flops, bytes, s);
+    hipLaunchKernelGGL((stem_b0_kernel<TH, 1>), dim3(N * a.tiles_x * a.tiles_y), dim3(256), 0, s, a);
+  } else {
+    ProfScope ps("stem_b0_kernel<16, 0>", flops, bytes, s);
+    hipLaunchKernelGGL((stem_b0_kernel<TH, 0>), dim3(N * a.tiles_x * a.tiles_y), dim3(256), 0, s, a);
+  }
   M2S_HIP(hipGetLastError());
 }
 
