@@ -113,9 +113,19 @@ __device__ __forceinline__ void ld4f(const bf16_t* p, float* v) {
   v[3] = __uint_as_float(u.y & 0xffff0000u);
 }
 
+#ifndef SP_STAGES
+#define SP_STAGES 2
+#endif
 constexpr int ROW = 64;  // bytes per LDS row = 32 bf16 = one k-step
 
-__device__ __forceinline__ int swz(int row, int chunk) { return row * ROW + ((chunk ^ ((row >> 2) & 3)) << 4); }
+// Physical chunk of logical chunk c in row r: c ^ f((r >> 2) & 3) with f = [0, 2, 3, 1].  A fragment read
+// (lane = (g = lane >> 4, r16 = lane & 15): row r16, chunk g) is then conflict-free for ds_read_b128's
+// lane groups on gfx950 ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...; MI355X_MICROARCH.md LDS table):
+// within each group the four lanes that share (r16 & 3) land in four different 16-byte bank slots.
+// (The plain c ^ ((r >> 2) & 3) put lanes 0-3 and 20-23 on the same slots: 2-way conflicts, SQ
+// LDS_BANK_CONFLICT ~3x the LDS-active cycles.)
+__device__ __forceinline__ int swz_f(int x) { return (0x1320 >> (4 * x)) & 3; }
+__device__ __forceinline__ int swz(int row, int chunk) { return row * ROW + ((chunk ^ swz_f((row >> 2) & 3)) << 4); }
 
 // SP = 1: split-fp32 operands (m2s_common.hpp sp_t): every activation and weight row is [hi | lo],
 // each K step DMAs both halves into two planes of the slot and runs the three MFMA terms
@@ -159,7 +169,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
   // uniform offset, one bit test and one add per row (the address math used to be ~40 VALU per
   // row per step, which made VALU issue, not the MFMA, the limit of these kernels).
   const int lrow = lane >> 2;
-  const int q = (lane & 3) ^ ((lane >> 4) & 3);  // logical chunk this lane fetches ((row>>2)&3 = lane>>4 & 3)
+  const int q = (lane & 3) ^ swz_f((lane >> 4) & 3);  // logical chunk this lane fetches ((row>>2)&3 = lane>>4 & 3)
   int rbase[A_PER_WAVE];
   uint32_t rmask[A_PER_WAVE];
   const int delta = (KIND == KIND_CONVT) ? (phase + a.ct_pad) / a.ct_u : 0;
@@ -450,7 +460,7 @@ template <int BM, int BN, int MT, int NT, int KIND, int XF, int SP>
 void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
   // keep two workgroups' LDS per CU (128 x 256: the SE gate table too, and 256 registers a wave);
   // split operands double the slot, so they run two stages
-  constexpr int S = SP ? 2 : (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
+  constexpr int S = SP ? SP_STAGES : (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
   constexpr int R = SP ? 2 : 1;
   static bool attr = [] {
     M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF, SP>),

@@ -39,7 +39,10 @@ constexpr int NT = SL / 16;    // 16-channel MFMA subtiles
 constexpr int CG = SL / 8;     // phase-2 channel groups (8 channels = one 16-byte vector)
 constexpr int PL = 256 / CG;   // phase-2 pixel lanes (64; 16 per wave)
 constexpr int ROWS_MAX = 400;  // haloed pixel rows per workgroup (4 x 10x10, 1 x 18x18)
-constexpr int ROWS_MAX_SP = 324;  // SP: fp32 rows (1 x 18x18, 2 x 10x10)
+#ifndef IRF_ROWS_SP
+#define IRF_ROWS_SP 324
+#endif
+constexpr int ROWS_MAX_SP = IRF_ROWS_SP;  // SP: fp32 rows (1 x 18x18, 2 x 10x10)
 constexpr int POS_MAX = 256;   // positions per workgroup
 // One slice per workgroup: a slice loop per workgroup (more reuse of the input) measured slower,
 // occupancy 4 -> 2.

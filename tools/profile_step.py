@@ -14,8 +14,9 @@ import bench  # noqa: E402
 steps = int(os.environ.get("STEPS", "2"))
 clips, frames = int(os.environ.get("CLIPS", "64")), int(os.environ.get("FRAMES", "30"))
 dev = torch.device("cuda", 0)
-ac = runtime.AcousticEngine(synth.synth_acoustic_state(0), dtype="bf16", device=dev, chunk=int(os.environ.get("CHUNK", "1920")))
-voc = runtime.VocoderEngine(synth.synth_generator_state(0), HIFIGAN_H, dtype="bf16", device=dev)
+dt = os.environ.get("DTYPE", "bf16x3")
+ac = runtime.AcousticEngine(synth.synth_acoustic_state(0), dtype=dt, device=dev, chunk=int(os.environ.get("CHUNK", "1920")))
+voc = runtime.VocoderEngine(synth.synth_generator_state(0), HIFIGAN_H, dtype=dt, device=dev)
 mean, std = synth.synth_scaler()
 pipe = runtime.Pipeline(ac, voc, mean, std)
 x = bench.make_frames(clips, frames, 256, 0, dev)
