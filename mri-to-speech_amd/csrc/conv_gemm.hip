@@ -113,9 +113,6 @@ __device__ __forceinline__ void ld4f(const bf16_t* p, float* v) {
   v[3] = __uint_as_float(u.y & 0xffff0000u);
 }
 
-#ifndef SP_STAGES
-#define SP_STAGES 2
-#endif
 constexpr int ROW = 64;  // bytes per LDS row = 32 bf16 = one k-step
 
 // Physical chunk of logical chunk c in row r: c ^ f((r >> 2) & 3) with f = [0, 2, 3, 1].  A fragment read
@@ -460,7 +457,7 @@ template <int BM, int BN, int MT, int NT, int KIND, int XF, int SP>
 void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
   // keep two workgroups' LDS per CU (128 x 256: the SE gate table too, and 256 registers a wave);
   // split operands double the slot, so they run two stages
-  constexpr int S = SP ? SP_STAGES : (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
+  constexpr int S = SP ? 2 : (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
   constexpr int R = SP ? 2 : 1;
   static bool attr = [] {
     M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF, SP>),

@@ -39,10 +39,7 @@ constexpr int NT = SL / 16;    // 16-channel MFMA subtiles
 constexpr int CG = SL / 8;     // phase-2 channel groups (8 channels = one 16-byte vector)
 constexpr int PL = 256 / CG;   // phase-2 pixel lanes (64; 16 per wave)
 constexpr int ROWS_MAX = 400;  // haloed pixel rows per workgroup (4 x 10x10, 1 x 18x18)
-#ifndef IRF_ROWS_SP
-#define IRF_ROWS_SP 324
-#endif
-constexpr int ROWS_MAX_SP = IRF_ROWS_SP;  // SP: fp32 rows (1 x 18x18, 2 x 10x10)
+constexpr int ROWS_MAX_SP = 400;  // SP: fp32 rows (1 x 18x18, 4 x 10x10)
 constexpr int POS_MAX = 256;   // positions per workgroup
 // One slice per workgroup: a slice loop per workgroup (more reuse of the input) measured slower,
 // occupancy 4 -> 2.
@@ -64,8 +61,8 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
                                                          int cs_mid, bf16_t* __restrict__ y,
                                                          bf16_t* __restrict__ se_mean, int SOH, int SOW, int pad_t,
                                                          int pad_l) {
-  constexpr int TILE_BYTES = SP ? ROWS_MAX_SP * MROWF * 4 : ROWS_MAX * MROW * 2;
-  __shared__ __attribute__((aligned(16))) char tile_raw[TILE_BYTES];
+  // the haloed tile: dynamic LDS sized for this launch's G images (ir_tile_bytes)
+  extern __shared__ __attribute__((aligned(16))) char tile_raw[];
   bf16_t* tile = reinterpret_cast<bf16_t*>(tile_raw);
   float* tilef = reinterpret_cast<float*>(tile_raw);
   __shared__ uint16_t lut[POS_MAX];
@@ -262,11 +259,16 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
 #pragma unroll
         for (int j = 0; j < 8; ++j) a[j] = b[j];
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const float4 u0 = *reinterpret_cast<const float4*>(base + off[t]);
-          const float4 u1 = *reinterpret_cast<const float4*>(base + off[t] + 4);
-          a[0] += w[t][0] * u0.x; a[1] += w[t][1] * u0.y; a[2] += w[t][2] * u0.z; a[3] += w[t][3] * u0.w;
-          a[4] += w[t][4] * u1.x; a[5] += w[t][5] * u1.y; a[6] += w[t][6] * u1.z; a[7] += w[t][7] * u1.w;
+        for (int ty = 0; ty < 3; ++ty) {  // one tap row at a time: 24 registers of taps in flight
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) {
+            const int t = 3 * ty + tx;
+            const float4 u0 = *reinterpret_cast<const float4*>(base + off[t]);
+            const float4 u1 = *reinterpret_cast<const float4*>(base + off[t] + 4);
+            a[0] += w[t][0] * u0.x; a[1] += w[t][1] * u0.y; a[2] += w[t][2] * u0.z; a[3] += w[t][3] * u0.w;
+            a[4] += w[t][4] * u1.x; a[5] += w[t][5] * u1.y; a[6] += w[t][6] * u1.z; a[7] += w[t][7] * u1.w;
+          }
+          asm volatile("" ::: "memory");
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -352,7 +354,7 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
 }
 
 template <int MT, int G, int SP>
-__global__ void __launch_bounds__(256, SP ? 3 : 4)
+__global__ void __launch_bounds__(256, SP ? (MT >= 4 ? 3 : 4) : 4)
     ir_pwdw_kernel(const bf16_t* __restrict__ x, int cs_in, int kp, const bf16_t* __restrict__ wpw,
                    const float* __restrict__ bpw, const uint32_t* __restrict__ wdw2, const float* __restrict__ bdw, int N,
                    int OH, int OW, int cs_mid, bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean) {
@@ -368,11 +370,17 @@ __global__ void __launch_bounds__(256, SP ? 3 : 4)
   ir_pwdw_body<4, 1, 2, SP>(x, cs_in, kp, wpw, bpw, wdw2, bdw, N, IH, IW, cs_mid, y, se_mean, OH, OW, pad_t, pad_l);
 }
 
+// images per workgroup: up to 4 small images (measured on the 8x8 maps of blocks.5 in split fp32:
+// 1383 / 970 / 745 us per launch at G = 1 / 2 / 4; the per-workgroup latency chain loads -> MFMA ->
+// barrier -> depthwise -> barrier -> squeeze amortises over more positions)
 int ir_group(int OH, int OW, bool sp) {
   const int P = OH * OW, rows = (OH + 2) * (OW + 2);
   for (int G = 4; G >= 1; G /= 2)
     if (G * P <= POS_MAX && G * rows <= (sp ? ROWS_MAX_SP : ROWS_MAX)) return G;
   return 0;
+}
+size_t ir_tile_bytes(int OH, int OW, int G, bool sp) {
+  return (size_t)G * (OH + 2) * (OW + 2) * (sp ? MROWF * 4 : MROW * 2);
 }
 
 }  // namespace
@@ -399,8 +407,8 @@ void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, co
 #define M2S_IRF(MT_, G_, SP_)                                                                            \
   if (pos <= 64 * MT_ && G == G_ && (int)split == SP_) {                                                 \
     ProfScope ps("ir_pwdw_kernel<" #MT_ ", " #G_ ", " #SP_ ">", flops, bytes, s);                       \
-    hipLaunchKernelGGL((ir_pwdw_kernel<MT_, G_, SP_>), grid, dim3(256), 0, s, xb, cs_in, kp, wb, bpw, wd, bdw, N, OH, \
-                       OW, cs_mid, yb, mb);                                                              \
+    hipLaunchKernelGGL((ir_pwdw_kernel<MT_, G_, SP_>), grid, dim3(256), ir_tile_bytes(OH, OW, G, split), s, xb, cs_in, \
+                       kp, wb, bpw, wd, bdw, N, OH, OW, cs_mid, yb, mb);                                 \
     M2S_HIP(hipGetLastError());                                                                          \
     return;                                                                                              \
   }
@@ -433,11 +441,11 @@ void launch_ir_pwdw_s2(const void* x, int N, int cs_in, int kp, const void* wpw,
   const uint32_t* wd = static_cast<const uint32_t*>(wdw);
   if (split) {
     ProfScope ps("ir_pwdw_s2_kernel<1>", flops, bytes, s);
-    hipLaunchKernelGGL(ir_pwdw_s2_kernel<1>, grid, dim3(256), 0, s, xb, cs_in, kp, wb, bpw, wd, bdw, N, IH, IW, cs_mid,
+    hipLaunchKernelGGL(ir_pwdw_s2_kernel<1>, grid, dim3(256), ir_tile_bytes(IH, IW, 1, true), s, xb, cs_in, kp, wb, bpw, wd, bdw, N, IH, IW, cs_mid,
                        static_cast<bf16_t*>(y), static_cast<bf16_t*>(se_mean), OH, OW, pad_t, pad_l);
   } else {
     ProfScope ps("ir_pwdw_s2_kernel<0>", flops, bytes, s);
-    hipLaunchKernelGGL(ir_pwdw_s2_kernel<0>, grid, dim3(256), 0, s, xb, cs_in, kp, wb, bpw, wd, bdw, N, IH, IW, cs_mid,
+    hipLaunchKernelGGL(ir_pwdw_s2_kernel<0>, grid, dim3(256), ir_tile_bytes(IH, IW, 1, false), s, xb, cs_in, kp, wb, bpw, wd, bdw, N, IH, IW, cs_mid,
                        static_cast<bf16_t*>(y), static_cast<bf16_t*>(se_mean), OH, OW, pad_t, pad_l);
   }
   M2S_HIP(hipGetLastError());

@@ -153,8 +153,17 @@ __device__ __forceinline__ void act_ld8(const T* x, long p, int cs, int c, float
 }
 template <typename T>
 __device__ __forceinline__ void act_st8(T* x, long p, int cs, int c, const float* v) {
-  act_st4<T>(x, p, cs, c, v);
-  act_st4<T>(x, p, cs, c + 4, v + 4);
+  if constexpr (Elem<T>::R == 2) {  // split: one 16-byte store for the 8 hi halves, one for the lo
+    uint16_t* u = reinterpret_cast<uint16_t*>(x) + p * 2 * cs + c;
+    uint2 h0, l0, h1, l1;
+    split4(v, h0, l0);
+    split4(v + 4, h1, l1);
+    *reinterpret_cast<uint4*>(u) = make_uint4(h0.x, h0.y, h1.x, h1.y);
+    *reinterpret_cast<uint4*>(u + cs) = make_uint4(l0.x, l0.y, l1.x, l1.y);
+  } else {
+    act_st4<T>(x, p, cs, c, v);
+    act_st4<T>(x, p, cs, c + 4, v + 4);
+  }
 }
 
 // bf16-path activations: one v_exp_f32 + one v_rcp_f32 (1 ulp) instead of an IEEE divide and

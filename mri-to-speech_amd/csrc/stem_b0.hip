@@ -69,7 +69,12 @@ __global__ void __launch_bounds__(256, SP ? 2 : 4) stem_b0_kernel(const StemB0Ar
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const int tpi = a.tiles_x * a.tiles_y;
-  const int n = blockIdx.x / tpi, tr = blockIdx.x - n * tpi;
+  // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so consecutive blockIdx land
+  // on different L2s and neighbouring tiles re-fetched their shared frame halo from HBM (2.8x the
+  // frame bytes).  Remapped, each XCD walks a contiguous run of tiles (neighbours share its L2).
+  const int nwg = gridDim.x, xq = nwg / 8, xr = nwg % 8, xcd = blockIdx.x % 8;
+  const int wid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + blockIdx.x / 8;
+  const int n = wid / tpi, tr = wid - n * tpi;
   const int ty0 = (tr / a.tiles_x) * TH, tx0 = (tr - (tr / a.tiles_x) * a.tiles_x) * SB_TW;
 
   // ---- phase 1: stem (fp32 VALU) -> S -------------------------------------------------------
