@@ -81,6 +81,15 @@ int er2_stage_elems();
 void launch_er2_fused(const bf16_t* x, int N, int H, int W, const bf16_t* wst, const float* bexp, const float* bpwl,
                       bf16_t* y, double flops, double bytes, hipStream_t s);
 
+// Split-fp32 EdgeResidual (stride 1, skip), (cs_in, mid, cs_out) in {(32, 128, 32), (64, 224, 64)}: conv_exp
+// 3x3 + SiLU -> conv_pwl + x with the three-term products, weights streamed in W_hi / W_lo stages of
+// `nt` = mid / 16 fragments; x, y in sp_t layout; wst = er_sp_nt_stages() stages of nt x [64][8] bf16.
+// (er_sp_fused.hip)
+bool er_sp_supported(int H, int W, int cs_in, int mid, int cs_out);
+int er_sp_nt_stages(int cs_in, int mid, int cs_out, int* nt);
+void launch_er_sp(const void* x, int N, int H, int W, int cs_in, int mid, int cs_out, const void* wst, const float* bexp,
+                  const float* bpwl, void* y, double flops, double bytes, hipStream_t s);
+
 // bf16 stride-2 EdgeResidual (no skip), (cs_in, mid, cs_out) in {(16, 64, 32), (32, 128, 64)}: conv_exp
 // 3x3/s2 TF-SAME + SiLU -> conv_pwl; x (N,H,W,cs_in) -> y (N,OH,OW,cs_out); wexp ers2_exp_elems() bf16 in
 // the kernel's fragment order, wpwl [cs_out/16][mid/32][64][8] with er_fused.hip's K permutation.

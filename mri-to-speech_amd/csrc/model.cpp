@@ -273,7 +273,44 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
         b.mid = make_divisible(cin * (double)sdf.exp);
         conv2d_kxk(b.c1, q + "conv_exp.weight", cin, b.mid, fold_bn(sd, q + "bn1", b.mid));
         conv1x1(b.c2, q + "conv_pwl.weight", b.mid, b.cout, fold_bn(sd, q + "bn2", b.cout));
-        if (dtype == M2S_DT_BF16 && b.stride == 1 && b.skip && k == 3 &&
+        if (dtype == M2S_DT_BF16X3 && b.stride == 1 && b.skip && k == 3 &&
+            er_sp_supported(32, 32, b.c1.cs_in, b.mid, chan_stride(b.cout))) {
+          // er_sp_fused.hip stage stream: per conv_exp k-step (tap, 32 input channels) a W_hi and a W_lo
+          // stage of nt fragments [n16][lane][8]; then conv_pwl's W_hi stages and W_lo stages, piece
+          // j = (k-step j / ON, n16 j % ON), K permuted as in er_fused.hip
+          int nt = 0;
+          const int csi = b.c1.cs_in, cso = chan_stride(b.cout), nst = er_sp_nt_stages(csi, b.mid, cso, &nt);
+          const int kc = csi / 32, nce = 9 * kc * 2, on_n = cso / 16, pn = on_n * (b.mid / 32), nps = (pn + nt - 1) / nt;
+          const float* we = need(sd, q + "conv_exp.weight", {b.mid, cin, 3, 3}).data;
+          const float* wq = need(sd, q + "conv_pwl.weight", {b.cout, b.mid, 1, 1}).data;
+          const BN e1 = fold_bn(sd, q + "bn1", b.mid), e2 = fold_bn(sd, q + "bn2", b.cout);
+          std::vector<uint16_t> st((size_t)nst * nt * 64 * 8, 0);
+          for (int sg = 0; sg < nst; ++sg)
+            for (int pc = 0; pc < nt; ++pc)
+              for (int ln = 0; ln < 64; ++ln)
+                for (int e = 0; e < 8; ++e) {
+                  const int row = ln & 15, g8 = ln >> 4;
+                  float v = 0.f;
+                  int plane;
+                  if (sg < nce) {
+                    plane = sg & 1;
+                    const int ks = sg >> 1, t = ks / kc, c = (ks % kc) * 32 + 8 * g8 + e, n = 16 * pc + row;
+                    if (c < cin) v = we[((size_t)n * cin + c) * 9 + t] * e1.a[n];
+                  } else {
+                    plane = (sg - nce) / nps;
+                    const int j = ((sg - nce) % nps) * nt + pc;
+                    if (j >= pn) continue;
+                    const int kk = j / on_n, on = j % on_n, o = on * 16 + row;
+                    const int c = 32 * kk + (e < 4 ? 4 * g8 + e : 16 + 4 * g8 + e - 4);
+                    if (o < b.cout) v = wq[(size_t)o * b.mid + c] * e2.a[o];
+                  }
+                  uint16_t hi, lo;
+                  split_host(v, &hi, &lo);
+                  st[(((size_t)sg * nt + pc) * 64 + ln) * 8 + e] = plane == 0 ? hi : lo;
+                }
+          b.er_sp_w = arena_.add_vec(st);
+          b.er_sp = true;
+        } else if (dtype == M2S_DT_BF16 && b.stride == 1 && b.skip && k == 3 &&
             er_fused_supported(64, 64, cin, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
           // er_fused.hip operand orders: conv_exp [tap][n16][lane][8] (lane = (k8 group, row));
           // conv_pwl [n16][k-step][lane][8] with the k-slot permutation of the kernel's header
@@ -599,6 +636,11 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         a.act = ACT_SILU;
         a.res = b.skip ? cur : nullptr;
         run_conv<T>(a, b.c1, s);
+      } else if (b.type == 1 && std::is_same<T, sp_t>::value && er_fused_ && b.er_sp &&
+                 er_sp_supported(nh, nw, b.c1.cs_in, b.mid, chan_stride(b.cout))) {
+        const double px = (double)nc * nh * nw;
+        launch_er_sp(cur, nc, nh, nw, b.c1.cs_in, b.mid, chan_stride(b.cout), arena_.ptr(b.er_sp_w), b.c1.b, b.c2.b, nxt,
+                     2.0 * px * b.mid * (9.0 * b.cin + b.cout), 4.0 * px * (b.c1.cs_in + chan_stride(b.cout)), s);
       } else if (b.type == 1 && std::is_same<T, bf16_t>::value && er_fused_ && b.er_frag &&
                  er_fused_supported(nh, nw, b.cin, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
         const double px = (double)nc * nh * nw;

@@ -112,6 +112,8 @@ class Acoustic {
     PConv se1, se2;             // ir SE: conv_reduce (mid -> rd, SiLU), conv_expand (rd -> mid, sigmoid)
     size_t er_wexp = 0, er_wpwl = 0;  // bf16 er 32 -> 128 -> 32 stride 1: fused-kernel fragment orders
     bool er_frag = false;
+    size_t er_sp_w = 0;  // split fp32 er stride 1: er_sp_fused.hip stage stream
+    bool er_sp = false;
   };
   template <typename T>
   void effnet_t(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe, int* probe_dims,
