@@ -138,6 +138,8 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
   constexpr int B_PER_WAVE = (B_BLOCKS + 3) / 4;   // waves >= B_BLOCKS issue into a scratch block
   constexpr int SLOT = (R * (BM + BN) + 16) * ROW; // +16 rows: scratch for surplus B DMAs
   constexpr int PER_STAGE = R * (A_PER_WAVE + B_PER_WAVE);
+  constexpr bool PRE = SP && XF == IN_SE_SCALE;    // split SE scale applied in LDS (below)
+  constexpr bool SE = XF == IN_SE_SCALE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* se_tab = reinterpret_cast<float*>(smem + S * SLOT);
 
@@ -263,7 +265,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
 
   // ---- SE scale table for this workgroup's images (GEMM kind only) ---------------------------
   int img0 = 0;
-  if constexpr (XF == IN_SE_SCALE) {
+  if constexpr (SE) {
     img0 = m0 / a.OH;
     for (int i = tid; i < se_imgs * a.cs_in; i += 256) {
       const int im = i / a.cs_in, c = i - (i / a.cs_in) * a.cs_in;
@@ -274,12 +276,12 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
   // SE scale on the weight fragments when the tile is one image (its k-scales are shared by every
   // row): NT fragments and one table read per k-step instead of MT fragments and MT reads
   bool one_img = false;
-  if constexpr (XF == IN_SE_SCALE) one_img = img0 == (min(m0 + BM, a.M) - 1) / a.OH;
+  if constexpr (SE) one_img = img0 == (min(m0 + BM, a.M) - 1) / a.OH;
   int frow_img[MT];
 #pragma unroll
   for (int mi = 0; mi < MT; ++mi) {
     const int m = m0 + wm * MT * 16 + mi * 16 + r16;
-    frow_img[mi] = XF == IN_SE_SCALE ? (m < a.M ? m / a.OH : img0) - img0 : 0;
+    frow_img[mi] = SE ? (m < a.M ? m / a.OH : img0) - img0 : 0;
   }
 
   f32x4 acc[NT][MT];
@@ -288,23 +290,9 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) acc[ni][mi] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < nsteps) issue(s, s);
-
-  for (int st = 0; st < nsteps; ++st) {
-    // stage st has landed once at most min(S-2, nsteps-1-st) younger stages are outstanding
-    const int younger = min(S - 2, nsteps - 1 - st);
-    if (younger >= 2)
-      wait_vm<2 * PER_STAGE>();
-    else if (younger == 1)
-      wait_vm<PER_STAGE>();
-    else
-      wait_vm<0>();
-    __builtin_amdgcn_s_barrier();  // every wave's DMA for `st` landed; slot (st-1)%S is free
-    if (st + S - 1 < nsteps) issue(st + S - 1, (st + S - 1) % S);
-
-    const char* As = smem + (st % S) * SLOT;
+  // one K step of MFMAs on the operands in `slot` (input transforms applied to the fragments)
+  auto compute = [&](int st, int slot) {
+    const char* As = smem + slot * SLOT;
     const char* Bs = As + R * BM * ROW;
     bf16x8 af[NT], bx[MT];
 #pragma unroll
@@ -324,20 +312,6 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
       if constexpr (XF == IN_LRELU) {
 #pragma unroll
         for (int mi = 0; mi < MT; ++mi) lrelu_split(bx[mi], bxl[mi], a.in_slope);
-      } else if constexpr (XF == IN_SE_SCALE) {
-        if (one_img) {
-          float sc[8];
-          load_scales(se_tab + st * 32 + g * 8, sc);
-#pragma unroll
-          for (int ni = 0; ni < NT; ++ni) scale_split(af[ni], afl[ni], sc);
-        } else {
-#pragma unroll
-          for (int mi = 0; mi < MT; ++mi) {
-            float sc[8];
-            load_scales(se_tab + frow_img[mi] * a.cs_in + st * 32 + g * 8, sc);
-            scale_split(bx[mi], bxl[mi], sc);
-          }
-        }
       }
 #pragma unroll
       for (int ni = 0; ni < NT; ++ni)
@@ -347,7 +321,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
           acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ni], bxl[mi], acc[ni][mi], 0, 0, 0);
           acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ni], bx[mi], acc[ni][mi], 0, 0, 0);
         }
-      continue;
+      return;
     }
     if constexpr (XF == IN_LRELU) {
 #pragma unroll
@@ -368,6 +342,85 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi)
         acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ni], bx[mi], acc[ni][mi], 0, 0, 0);
+  };
+
+  if constexpr (PRE) {
+    // Split SE-scaled GEMM: the A tile is scaled IN LDS once per K step by the whole workgroup (each
+    // thread BM / 64 16-byte hi/lo chunk pairs) between two barriers, instead of per wave on its
+    // fragments (WN-fold redundant; the fp32 re-split is ~56 VALU per 8 values).  The second
+    // workgroup on the CU runs its MFMAs meanwhile.  Measured per launch (20 a step, split fp32):
+    // per-fragment 419 us, in-LDS on two slots 405 us, in-LDS one step ahead on three slots 568 us
+    // (one workgroup per CU).
+    static_assert(S == 2, "pre-scaled SE GEMM runs two slots");
+    constexpr int UPT = BM * 4 / 256;
+    uint32_t u_lds[UPT], u_tab[UPT];
+    const uint32_t tab0 = (uint32_t)(uintptr_t)se_tab;
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+      const int u = tid + 256 * j, row = u >> 2, p = u & 3;
+      const int c = p ^ swz_f((row >> 2) & 3);
+      const int m = m0 + row;
+      const int im = (m < a.M ? m / a.OH : img0) - img0;
+      u_lds[j] = (uint32_t)(row * ROW + p * 16);
+      u_tab[j] = tab0 + (uint32_t)((im * a.cs_in + c * 8) * 4);
+    }
+    const uint32_t smem0 = (uint32_t)(uintptr_t)smem;
+    auto scale_slot = [&](int st, int slot) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 h[UPT], l[UPT];
+      f32x4 s0[UPT], s1[UPT];
+#pragma unroll
+      for (int j = 0; j < UPT; ++j) {
+        const uint32_t ah = smem0 + slot * SLOT + u_lds[j], ta = u_tab[j] + st * 128;
+        // plain ds_reads here would let hipcc drain the in-flight DMA (vmcnt(0)): see load_scales
+        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:%6\n\tds_read_b128 %2, %5\n\tds_read_b128 %3, %5 offset:16"
+                     : "=&v"(h[j]), "=&v"(l[j]), "=&v"(s0[j]), "=&v"(s1[j])
+                     : "v"(ah), "v"(ta), "n"(BM * ROW)
+                     : "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < UPT; ++j) {
+        asm volatile("" : "+v"(h[j]), "+v"(l[j]), "+v"(s0[j]), "+v"(s1[j]));
+        const float sc[8] = {s0[j][0], s0[j][1], s0[j][2], s0[j][3], s1[j][0], s1[j][1], s1[j][2], s1[j][3]};
+        bf16x8 hv = __builtin_bit_cast(bf16x8, h[j]), lv = __builtin_bit_cast(bf16x8, l[j]);
+        scale_split(hv, lv, sc);
+        const uint32_t ah = smem0 + slot * SLOT + u_lds[j];
+        asm volatile("ds_write_b128 %0, %1\n\tds_write_b128 %0, %2 offset:%3"
+                     :
+                     : "v"(ah), "v"(__builtin_bit_cast(u32x4, hv)), "v"(__builtin_bit_cast(u32x4, lv)), "n"(BM * ROW)
+                     : "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // visible at the next barrier
+    };
+    issue(0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the SE table stores
+    for (int st = 0; st < nsteps; ++st) {
+      wait_vm<0>();
+      __builtin_amdgcn_s_barrier();  // st landed everywhere; slot (st + 1) % 2 free
+      if (st + 1 < nsteps) issue(st + 1, (st + 1) % 2);
+      scale_slot(st, st % 2);
+      __builtin_amdgcn_s_barrier();
+      compute(st, st % 2);
+    }
+  } else {
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nsteps) issue(s, s);
+
+  for (int st = 0; st < nsteps; ++st) {
+    // stage st has landed once at most min(S-2, nsteps-1-st) younger stages are outstanding
+    const int younger = min(S - 2, nsteps - 1 - st);
+    if (younger >= 2)
+      wait_vm<2 * PER_STAGE>();
+    else if (younger == 1)
+      wait_vm<PER_STAGE>();
+    else
+      wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for `st` landed; slot (st-1)%S is free
+    if (st + S - 1 < nsteps) issue(st + S - 1, (st + S - 1) % S);
+    compute(st, st % S);
+  }
   }
 
   // ---- epilogue: 4 consecutive channels of one position per lane ------------------------------
@@ -453,6 +506,9 @@ const char* kname(int k) {
   }
 }
 
+// rows of SE gates a tile needs: the images its BM rows touch
+inline int se_images(int BM, int OH) { return BM % OH == 0 ? BM / OH : OH % BM == 0 ? 1 : (BM + OH - 1) / OH + 1; }
+
 template <int BM, int BN, int MT, int NT, int KIND, int XF, int SP>
 void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
   // keep two workgroups' LDS per CU (128 x 256: the SE gate table too, and 256 registers a wave);
@@ -469,7 +525,7 @@ void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
   int se_imgs = 0;
   if (a.in_xform == IN_SE_SCALE) {
     M2S_CHECK(KIND == KIND_GEMM && a.OH > 0, "SE scale needs the GEMM kind with OH = rows per image");
-    se_imgs = (BM + a.OH - 1) / a.OH + 1;
+    se_imgs = se_images(BM, a.OH);
   }
   const size_t lds = (size_t)S * (R * (BM + BN) + 16) * ROW + (size_t)se_imgs * a.cs_in * sizeof(float);
   M2S_CHECK(lds <= 160 * 1024, "conv_gemm: LDS budget");

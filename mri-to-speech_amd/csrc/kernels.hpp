@@ -61,11 +61,12 @@ void launch_stem_b0(const float* frames, int N, int H, int W, int OH, int OW, in
                     const float* b9, const void* w0, const float* b0, int kp0, const void* w1, const float* b1,
                     int kp1, void* y, bool split, double flops, double bytes, hipStream_t s);
 
-// bf16 SqueezeExcite excitation: gate (N, cs_mid) = sigmoid(W2 · SiLU(W1 · mean + b1) + b2), mean (N, cs_mid)
-// from the squeeze; w1 packed [>= rd][kp1], w2 packed [>= mid][kp2].  (se_excite.hip)
+// SqueezeExcite excitation (bf16, or split fp32 with split = true): gate (N, cs_mid) =
+// sigmoid(W2 · SiLU(W1 · mean + b1) + b2), mean (N, cs_mid) from the squeeze; w1 packed [>= rd][kp1],
+// w2 packed [>= mid][kp2] (split: rows [hi kp | lo kp]).  (se_excite.hip)
 bool se_excite_supported(int rd, int kp2, int cs_mid);
-void launch_se_excite(const bf16_t* mean, int N, int mid, int cs_mid, const bf16_t* w1, int kp1, const float* b1,
-                      int rd, const bf16_t* w2, int kp2, const float* b2, bf16_t* gate, hipStream_t s);
+void launch_se_excite(const void* mean, int N, int mid, int cs_mid, const void* w1, int kp1, const float* b1,
+                      int rd, const void* w2, int kp2, const float* b2, void* gate, bool split, hipStream_t s);
 
 // bf16 EdgeResidual (stride 1, skip) 32 -> 128 -> 32: conv_exp 3x3 + SiLU, conv_pwl 1x1, + x in one
 // persistent kernel; x, y (N,H,W,32); wexp / wpwl in the kernel's fragment orders.  (er_fused.hip)

@@ -710,10 +710,9 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
           launch_se_mean<T>(sums, nc, dw_pixel_blocks(nh, nw), cs, 1.0f / (float)(nh * nw), se_mean, s);
         }
         }
-        if (std::is_same<T, bf16_t>::value && se_fused_ && se_excite_supported(b.rd, b.se2.kp, cs)) {
-          launch_se_excite(reinterpret_cast<const bf16_t*>(se_mean), nc, b.mid, cs, static_cast<const bf16_t*>(b.se1.w),
-                           b.se1.kp, b.se1.b, b.rd, static_cast<const bf16_t*>(b.se2.w), b.se2.kp, b.se2.b,
-                           reinterpret_cast<bf16_t*>(scale), s);
+        if (FUSABLE && se_fused_ && se_excite_supported(b.rd, b.se2.kp, cs)) {
+          launch_se_excite(se_mean, nc, b.mid, cs, b.se1.w, b.se1.kp, b.se1.b, b.rd, b.se2.w, b.se2.kp, b.se2.b, scale,
+                           SPL, s);
         } else {
         ConvArgs r1 = conv_args(b.se1);  // conv_reduce + SiLU, all images of the chunk at once
         r1.x = se_mean;

@@ -8,6 +8,10 @@
 // vectors read straight into B fragments; the hidden layer (bf16) goes through LDS; expand = the
 // cs_mid/16 channel tiles spread over the waves, 2 k-steps each.  Weights are the GEMM path's
 // packed rows ([>= rd][cs_mid] and [>= mid][cs(rd)]).
+// Split fp32 (SP = 1, m2s_common.hpp sp_t): the squeeze vectors, the weights (rows [hi kp | lo kp])
+// and the gates are hi/lo pairs, every product is the three MFMA terms hi*hi + hi*lo + lo*hi, and
+// the hidden layer goes through LDS as two bf16 planes.  (The split engine used to run the two
+// GEMMs through conv_gemm: 40 launches per step at 60-90 us, ~3 ms of a 56 ms step.)
 #include <algorithm>
 
 #include "kernels.hpp"
@@ -20,40 +24,71 @@ constexpr int SE_IMG = 16;   // images per workgroup (MFMA N)
 constexpr int SE_RDMAX = 64;
 constexpr int SE_HROW = SE_RDMAX + 8;  // LDS row of the hidden layer (bf16), padded
 
+__device__ __forceinline__ bf16x8 ld8(const bf16_t* p, bool ok) {
+  return __builtin_bit_cast(bf16x8, ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0u, 0u, 0u, 0u));
+}
+
+// acc += a * b over the split terms (SP) or the single bf16 term
+template <int SP>
+__device__ __forceinline__ f32x4 mma(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x4 acc) {
+  if constexpr (SP) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+  }
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+}
+
+// 4 values -> the dtype's storage at (row base u, channel c): bf16, or a hi/lo pair at +cs
+template <int SP>
+__device__ __forceinline__ void st4(bf16_t* u, int cs, const float* v) {
+  if constexpr (SP) {
+    uint2 hi, lo;
+    split4(v, hi, lo);
+    *reinterpret_cast<uint2*>(u) = hi;
+    *reinterpret_cast<uint2*>(u + cs) = lo;
+  } else {
+    *reinterpret_cast<uint2*>(u) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  }
+}
+
+template <int SP>
 __global__ void __launch_bounds__(256) se_excite_kernel(const bf16_t* __restrict__ mean, int N, int mid, int cs_mid,
                                                         const bf16_t* __restrict__ w1, int kp1,
                                                         const float* __restrict__ b1, int rd,
                                                         const bf16_t* __restrict__ w2, int kp2,
                                                         const float* __restrict__ b2, bf16_t* __restrict__ gate) {
-  __shared__ __attribute__((aligned(16))) bf16_t hid[SE_IMG][SE_HROW];
+  constexpr int R = SP ? 2 : 1;
+  constexpr int UB = SP ? 4 : 8;  // k-steps of loads in flight per batch
+  __shared__ __attribute__((aligned(16))) bf16_t hid[R][SE_IMG][SE_HROW];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const int n0 = blockIdx.x * SE_IMG;
   const bool img_ok = n0 + r16 < N;
-  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
 
   // ---- conv_reduce + SiLU: wave w owns hidden rows [16w, 16w + 16) ------------------------------
   {
     const int row = 16 * wave + r16;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
     if (16 * wave < rd) {
-      const bf16_t* wr = w1 + (size_t)row * kp1 + 8 * g;
-      const bf16_t* mr = mean + (size_t)(n0 + r16) * cs_mid + 8 * g;
-      // 8 k-steps of loads in flight per batch: the chain is load-latency bound, not MFMA bound
+      const bf16_t* wr = w1 + (size_t)row * kp1 * R + 8 * g;
+      const bf16_t* mr = mean + (size_t)(n0 + r16) * cs_mid * R + 8 * g;
+      // UB k-steps of loads in flight per batch: the chain is load-latency bound, not MFMA bound
       const bool rok = row < rd;
-      for (int k0 = 0; k0 < cs_mid; k0 += 8 * 32) {
-        uint4 a[8], b[8];
+      for (int k0 = 0; k0 < cs_mid; k0 += UB * 32) {
+        bf16x8 a[UB], b[UB], al[UB], bl[UB];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < UB; ++u) {
           const int k = k0 + 32 * u;
-          a[u] = rok && k < cs_mid ? *reinterpret_cast<const uint4*>(wr + k) : z4;
-          b[u] = img_ok && k < cs_mid ? *reinterpret_cast<const uint4*>(mr + k) : z4;
+          a[u] = ld8(wr + k, rok && k < cs_mid);
+          b[u] = ld8(mr + k, img_ok && k < cs_mid);
+          if constexpr (SP) {
+            al[u] = ld8(wr + kp1 + k, rok && k < cs_mid);
+            bl[u] = ld8(mr + cs_mid + k, img_ok && k < cs_mid);
+          }
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[u]), __builtin_bit_cast(bf16x8, b[u]),
-                                                        acc, 0, 0, 0);
+        for (int u = 0; u < UB; ++u) acc = mma<SP>(a[u], al[u], b[u], bl[u], acc);
       }
     }
     // lane holds hidden rows 16w + 4g .. + 3 of image r16
@@ -63,25 +98,31 @@ __global__ void __launch_bounds__(256) se_excite_kernel(const bf16_t* __restrict
       const int r = 16 * wave + 4 * g + j;
       h[j] = r < rd ? silu(acc[j] + b1[r]) : 0.f;
     }
-    *reinterpret_cast<uint2*>(&hid[r16][16 * wave + 4 * g]) = make_uint2(pack_bf16x2(h[0], h[1]), pack_bf16x2(h[2], h[3]));
+    st4<SP>(&hid[0][r16][16 * wave + 4 * g], SE_IMG * SE_HROW, h);
   }
   __syncthreads();
 
   // ---- conv_expand + sigmoid: channel tiles of 16 over the waves ---------------------------------
-  bf16x8 hb[SE_RDMAX / 32];
+  bf16x8 hb[SE_RDMAX / 32], hl[SE_RDMAX / 32];
 #pragma unroll
-  for (int ks = 0; ks < SE_RDMAX / 32; ++ks) hb[ks] = *reinterpret_cast<const bf16x8*>(&hid[r16][32 * ks + 8 * g]);
+  for (int ks = 0; ks < SE_RDMAX / 32; ++ks) {
+    hb[ks] = *reinterpret_cast<const bf16x8*>(&hid[0][r16][32 * ks + 8 * g]);
+    if constexpr (SP) hl[ks] = *reinterpret_cast<const bf16x8*>(&hid[R - 1][r16][32 * ks + 8 * g]);
+  }
   const int nks = kp2 / 32;
   const int ntile = cs_mid / 16;
   // 4 channel tiles per batch, all their weight fragments loaded before the MFMAs
   for (int t0 = wave; t0 < ntile; t0 += 4 * 4) {
-    uint4 a[4][SE_RDMAX / 32];
+    bf16x8 a[4][SE_RDMAX / 32], al[4][SE_RDMAX / 32];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int c = 16 * (t0 + 4 * u) + r16;  // weight row of this lane's A fragment
 #pragma unroll
-      for (int ks = 0; ks < SE_RDMAX / 32; ++ks)
-        a[u][ks] = c < mid && ks < nks ? *reinterpret_cast<const uint4*>(w2 + (size_t)c * kp2 + 32 * ks + 8 * g) : z4;
+      for (int ks = 0; ks < SE_RDMAX / 32; ++ks) {
+        const bf16_t* wp = w2 + (size_t)c * kp2 * R + 32 * ks + 8 * g;
+        a[u][ks] = ld8(wp, c < mid && ks < nks);
+        if constexpr (SP) al[u][ks] = ld8(wp + kp2, c < mid && ks < nks);
+      }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -89,16 +130,13 @@ __global__ void __launch_bounds__(256) se_excite_kernel(const bf16_t* __restrict
       if (t >= ntile) break;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < SE_RDMAX / 32; ++ks)
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[u][ks]), hb[ks], acc, 0, 0, 0);
+      for (int ks = 0; ks < SE_RDMAX / 32; ++ks) acc = mma<SP>(a[u][ks], al[u][ks], hb[ks], hl[ks], acc);
       // lane holds gates of channels 16t + 4g .. + 3 for image r16
       const int c4 = 16 * t + 4 * g;
       float v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = c4 + j < mid ? sigmoidf_(acc[j] + b2[c4 + j]) : 0.f;
-      if (img_ok)
-        *reinterpret_cast<uint2*>(gate + (size_t)(n0 + r16) * cs_mid + c4) =
-            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      if (img_ok) st4<SP>(gate + (size_t)(n0 + r16) * cs_mid * R + c4, cs_mid, v);
     }
   }
 }
@@ -109,12 +147,16 @@ bool se_excite_supported(int rd, int kp2, int cs_mid) {
   return rd >= 1 && rd <= SE_RDMAX && kp2 >= rd && kp2 % 32 == 0 && kp2 <= SE_RDMAX && cs_mid % 32 == 0;
 }
 
-void launch_se_excite(const bf16_t* mean, int N, int mid, int cs_mid, const bf16_t* w1, int kp1, const float* b1,
-                      int rd, const bf16_t* w2, int kp2, const float* b2, bf16_t* gate, hipStream_t s) {
+void launch_se_excite(const void* mean, int N, int mid, int cs_mid, const void* w1, int kp1, const float* b1,
+                      int rd, const void* w2, int kp2, const float* b2, void* gate, bool split, hipStream_t s) {
   M2S_CHECK(se_excite_supported(rd, kp2, cs_mid) && kp1 >= cs_mid && N > 0, "se_excite: unsupported shape");
-  ProfScope ps("se_excite_kernel", 2.0 * 2.0 * N * mid * rd, 2.0 * (2.0 * N * cs_mid) + 2.0 * 2.0 * mid * rd, s);
-  hipLaunchKernelGGL(se_excite_kernel, dim3(ceil_div(N, SE_IMG)), dim3(256), 0, s, mean, N,
-                     mid, cs_mid, w1, kp1, b1, rd, w2, kp2, b2, gate);
+  const double es = split ? 4.0 : 2.0;
+  ProfScope ps(split ? "se_excite_kernel<1>" : "se_excite_kernel<0>", 2.0 * 2.0 * N * mid * rd,
+               es * (2.0 * N * cs_mid) + es * 2.0 * mid * rd, s);
+  auto k = split ? se_excite_kernel<1> : se_excite_kernel<0>;
+  hipLaunchKernelGGL(k, dim3(ceil_div(N, SE_IMG)), dim3(256), 0, s, static_cast<const bf16_t*>(mean), N, mid, cs_mid,
+                     static_cast<const bf16_t*>(w1), kp1, b1, rd, static_cast<const bf16_t*>(w2), kp2, b2,
+                     static_cast<bf16_t*>(gate));
   M2S_HIP(hipGetLastError());
 }
 
