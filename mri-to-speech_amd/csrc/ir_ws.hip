@@ -1,0 +1,430 @@
+// Split-fp32 InvertedResidual front half for the stride-1 blocks on 16x16 and 8x8 maps, as one
+// persistent warp-specialised workgroup per CU:
+//   conv_pw (1x1 expand, 3-term MFMA) + bn1 + SiLU -> fp32 LDS tile -> conv_dw 3x3 + bn2 + SiLU -> HBM
+//   + the SE squeeze (per-image channel means).
+// (timm InvertedResidual conv_pw/bn1/conv_dw/bn2/se.mean; mri_acoustic_model.py:28-34.)  Same outputs
+// as ir_pwdw_kernel<.., SP = 1> (ir_fused.hip), which launches one short workgroup per (images, 32-
+// channel slice) and spends most of its ~16 us life waiting on a chain of loads and barriers.
+//
+// A workgroup (16 waves) owns whole images and walks their 32-channel slices:
+//   waves 0-7 (producers): the image's input rows sit in LDS (loaded once per band of 8 output rows
+//     plus the halo rows, by LDS-DMA); the slice's expand weights, biases and depthwise taps stream
+//     through double-buffered LDS stages (DMA one slice ahead).  MFMA A = weights (16 channels x 32
+//     k), B = 16 positions x 32 k, three terms hi*hi + hi*lo + lo*hi; SiLU(acc + b) -> tile[f % 2].
+//   waves 8-15 (consumers): the depthwise of the PREVIOUS slice from tile[(f - 1) % 2] (a lane = 4
+//     channels x 1-2 pixels, fp32 taps in registers, no bounds checks: the tile carries a zero halo),
+//     SiLU, split-fp32 stores, and the squeeze partial sums.
+// Every weight, tap and bias reaches LDS by DMA from the producers, so the consumers issue no loads
+// (a load's wait would also drain their in-flight stores).  One barrier per slice orders both; each
+// SIMD holds two producer and two consumer waves, whose MFMA and VALU work interleave.  Bands of one
+// image run back to back in the same workgroup, so the squeeze sums of a 16x16 image accumulate in LDS.
+//
+// LDS layouts (reads conflict-free for ds_read_b128's lane groups, MI355X_MICROARCH.md LDS table):
+//   x     [pos][hi plane | lo plane], planes padded to 256-byte multiples; 16-byte chunk L of row r
+//         stored at (L & ~15) | ((L & 15) ^ h(r)), h(r) = ((r & 3) << 2) | f((r >> 2) & 3), f = [0,2,3,1]
+//         (the XOR is applied on the DMA source side: a DMA lane's LDS slot is fixed).
+//   W     [k-step][plane][32 rows][4 chunks] with the conv_gemm row swizzle.
+//   tile  8 planes of 4 channels x TROWS rows of 16 B; row = (band row + 1) * (W + 2) + col + 1 with a
+//         zero halo (columns zeroed once, out-of-image rows written as zeros by the producers);
+//         TROWS = 4 (mod 16): a consumer wave's lane groups (8 planes x 2 pixels) then land in 16
+//         distinct bank slots (searched exhaustively over plane strides).
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+#include "kernels.hpp"
+#include "prof.hpp"
+
+namespace m2s {
+namespace {
+
+__device__ __attribute__((aligned(16))) uint4 g_ws_zero[4];  // DMA source of padding chunks
+
+constexpr int WS_SL = 32;  // expanded channels per slice
+constexpr int WS_BR = 8;   // output rows per band
+constexpr int WS_NP = 8;   // producer waves
+constexpr int WS_NC = 8;   // consumer waves
+constexpr int WS_UMAX = 3; // producer units per wave (ws_layout bounds the band's subtiles to 12)
+
+__device__ __forceinline__ int swz_f(int x) { return (0x1320 >> (4 * x)) & 3; }
+__device__ __forceinline__ int hx_of(int r) { return ((r & 3) << 2) | swz_f((r >> 2) & 3); }
+// LDS-DMA in inline asm (cdna_hip_programming.md 'Operands and clobbers', the glds16 recipe): hipcc
+// neither sees nor counts it, so it does not drain it with vmcnt(0) before the producer's own LDS
+// reads (it did with the builtin: W(i+1)'s DMA waited for at every slice).  Completion: wait_vm0.
+__device__ __forceinline__ void dma16(const void* src, uint32_t lds_wave_base) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds_wave_base)
+               : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
+}
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+struct WsLayout {
+  int XR, TROWS, x_bytes, tile_bytes, w_bytes, total;
+};
+
+__host__ __device__ inline int ws_cpp(int cs_in) { return (cs_in * 2 + 255) / 256 * 16; }  // chunks per plane
+__host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mid) {
+  WsLayout L;
+  const int cpp = ws_cpp(cs_in), xp = 2 * cpp * 16;
+  L.XR = 0;  // input rows a band needs (its rows and the in-image halo rows)
+  for (int r0 = 0; r0 < H; r0 += WS_BR) {
+    const int a = r0 > 0 ? r0 - 1 : 0, b = r0 + WS_BR + 1 < H ? r0 + WS_BR + 1 : H;
+    L.XR = b - a > L.XR ? b - a : L.XR;
+  }
+  const int tr = ((H < WS_BR ? H : WS_BR) + 2) * (W + 2);
+  L.TROWS = tr + (20 - tr % 16) % 16;
+  L.x_bytes = L.XR * W * xp;
+  L.tile_bytes = 2 * 8 * L.TROWS * 16;
+  L.w_bytes = 2 * (cs_in / 32) * 4096;
+  const int nb = (H + WS_BR - 1) / WS_BR;
+  L.total = L.x_bytes + L.tile_bytes + L.w_bytes + (2 * 320 + 2 * 32 + 2 * WS_NC * 32) * 4 + (nb > 1 ? cs_mid * 4 : 0);
+  return L;
+}
+
+template <int W, int KS>
+__global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
+    ir_ws_kernel(const bf16_t* __restrict__ x, int N, int H, int cs_mid, const bf16_t* __restrict__ wpw,
+                 const float* __restrict__ bpw, const float* __restrict__ wdw, const float* __restrict__ bdw,
+                 bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, unsigned long long* __restrict__ trace) {
+  constexpr int CS = KS * 32;  // input channel stride = expand K
+  constexpr int CPP = (CS * 2 + 255) / 256 * 16;
+  constexpr int CPR = 2 * CPP;  // 16-byte chunks per LDS x row
+  constexpr int XP = CPR * 16;
+  constexpr int WT = W + 2;     // tile row (with the zero halo columns)
+  constexpr int WS_PXL = WS_BR * W / 64;  // output pixels per consumer lane per slice
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const WsLayout Lg = ws_layout(H, W, CS, cs_mid);
+  const int NB = (H + WS_BR - 1) / WS_BR, NS = cs_mid / WS_SL, P = H * W;
+  const int PLT = Lg.TROWS * 16;
+  char* xs = smem;
+  char* tiles = xs + Lg.x_bytes;
+  char* wbuf = tiles + Lg.tile_bytes;
+  float* wdl = reinterpret_cast<float*>(wbuf + Lg.w_bytes);  // [2][9 x 32 taps | 32 depthwise bias]
+  float* bpl = wdl + 2 * 320;                                 // [2][32] expand bias
+  float* red = bpl + 2 * 32;                                  // [2][WS_NC][32]
+  float* se_acc = red + 2 * WS_NC * 32;                       // [cs_mid] (NB > 1)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const bool prod = wave < WS_NP;
+  const int n_units = blockIdx.x < N ? (N - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int T = n_units * NB * NS;
+
+  auto TR = [&](int i, int k) {
+#ifdef IRWS_TRACE
+    if (trace && blockIdx.x == 0 && (wave == 0 || wave == WS_NP) && i < 64) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      trace[((i * 2 + (wave == WS_NP)) * 8 + k) * 64 + lane] = t;
+    }
+#else
+    (void)i; (void)k; (void)trace;
+#endif
+  };
+  // (image, band, slice) of a flat step, advanced incrementally (no integer divisions per step)
+  struct Step {
+    int img, band, sl;
+  };
+  auto next_step = [&](Step d) {
+    if (++d.sl == NS) {
+      d.sl = 0;
+      if (++d.band == NB) {
+        d.band = 0;
+        d.img += gridDim.x;
+      }
+    }
+    return d;
+  };
+
+  // the tiles' halo columns are zero for good (the producers write only interior columns)
+  for (int i = tid; i < 2 * 8 * Lg.TROWS; i += 64 * (WS_NP + WS_NC)) {
+    const int pl = i / Lg.TROWS, r = i - pl * Lg.TROWS, c = r % WT;
+    if (c == 0 || c == WT - 1) *reinterpret_cast<float4*>(tiles + pl * PLT + r * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
+  // ---- producer pieces -----------------------------------------------------------------------
+  auto issue_w = [&](int f, Step d) {  // the slice's expand weights (4 * KS DMA pieces) + expand bias
+    const int sl = d.sl;
+    char* base = wbuf + (f & 1) * KS * 4096;
+    if (wave == 0 && lane < 8) dma16(bpw + sl * WS_SL + 4 * lane, lds_addr(bpl + (f & 1) * 32));
+    const int q = (lane & 3) ^ swz_f((lane >> 4) & 3);
+    for (int j = wave; j < 4 * KS; j += WS_NP) {
+      const int ks = j >> 2, plane = (j >> 1) & 1, half = j & 1;
+      const int row = sl * WS_SL + half * 16 + (lane >> 2);
+      dma16(wpw + (size_t)row * CS * 2 + plane * CS + ks * 32 + q * 8, lds_addr(base + ks * 4096 + plane * 2048 + half * 1024));
+    }
+  };
+  auto issue_wd = [&](int f, Step d) {  // the slice's depthwise taps [9][32] + bias: 80 lanes of 16 B
+    const int c0 = d.sl * WS_SL;
+    float* dst = wdl + (f & 1) * 320;
+    if (wave == WS_NP - 2) {
+      dma16(wdw + (size_t)(lane >> 3) * cs_mid + c0 + 4 * (lane & 7), lds_addr(dst));
+    } else if (wave == WS_NP - 1 && lane < 16) {
+      const float* src = lane < 8 ? wdw + (size_t)8 * cs_mid + c0 + 4 * lane : bdw + c0 + 4 * (lane - 8);
+      dma16(src, lds_addr(dst + 256));
+    }
+  };
+  auto issue_x = [&](int img, int band) {  // input rows of the band (+ halo rows), swizzled
+    const int r0 = band * WS_BR, xr0 = max(r0 - 1, 0), xr1 = min(r0 + WS_BR + 1, H);
+    const int ninstr = (xr1 - xr0) * W * CPR / 64;
+    const bf16_t* xi = x + ((size_t)img * P + (size_t)xr0 * W) * CS * 2;
+    for (int j = wave; j < ninstr; j += WS_NP) {
+      const int id = j * 64 + lane, r = id / CPR, p = id - r * CPR;
+      const int L = (p & ~15) | ((p & 15) ^ hx_of(r));
+      const int plane = L / CPP, k8 = L - plane * CPP;
+      const void* src = k8 * 8 < CS ? static_cast<const void*>(xi + (size_t)r * CS * 2 + plane * CS + k8 * 8)
+                                    : static_cast<const void*>(g_ws_zero);
+      dma16(src, lds_addr(xs + j * 1024));
+    }
+  };
+  auto produce = [&](int f, Step d) {
+    const int r0 = d.band * WS_BR, br = min(WS_BR, H - r0), xr0 = max(r0 - 1, 0), xr1 = min(r0 + WS_BR + 1, H);
+    const int PB = (xr1 - xr0) * W, nunit = 2 * ((PB + 15) / 16);
+    const char* wb = wbuf + (f & 1) * KS * 4096;
+    const int hxl = hx_of(r16);
+    // units = (16-position subtile t, 16-channel tile nt), dealt round-robin over the producer waves
+    // (9 subtiles x 2 on a 16x16 band: at most 3 units = 36 MFMAs a wave)
+    f32x4 acc[WS_UMAX];
+#pragma unroll
+    for (int k = 0; k < WS_UMAX; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int Lh = ks * 4 + g, Ll = CPP + ks * 4 + g;
+      const int ph = ((Lh & ~15) | ((Lh & 15) ^ hxl)) << 4, pl = ((Ll & ~15) | ((Ll & 15) ^ hxl)) << 4;
+#pragma unroll
+      for (int k = 0; k < WS_UMAX; ++k) {
+        const int u = wave + WS_NP * k;
+        if (u < nunit) {
+          const int t = u >> 1, row = (u & 1) * 16 + r16;
+          const int o = row * 64 + ((g ^ swz_f((row >> 2) & 3)) << 4);
+          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(wb + ks * 4096 + o);
+          const bf16x8 al = *reinterpret_cast<const bf16x8*>(wb + ks * 4096 + 2048 + o);
+          const char* xr = xs + (t * 16 + r16) * XP;
+          const bf16x8 bh = *reinterpret_cast<const bf16x8*>(xr + ph);
+          const bf16x8 bl = *reinterpret_cast<const bf16x8*>(xr + pl);
+          acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[k], 0, 0, 0);
+          acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[k], 0, 0, 0);
+          acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[k], 0, 0, 0);
+        }
+      }
+      asm volatile("" ::: "memory");  // one k-step of fragments in flight (registers)
+    }
+    TR(f, 6);
+    // bias + SiLU -> tile[f % 2]; lane holds channels 4g..4g+3 (of 16-channel tile nt) of position r16
+    char* tb = tiles + (f & 1) * 8 * PLT;
+    const int trow0 = xr0 - r0 + 1;  // tile row of x row 0
+#pragma unroll
+    for (int k = 0; k < WS_UMAX; ++k) {
+      const int u = wave + WS_NP * k, nt = u & 1, m = (u >> 1) * 16 + r16;
+      if (u < nunit && m < PB) {
+        // from LDS (staged with the weights): a global load here would make hipcc drain the DMA
+        const float4 bb = *reinterpret_cast<const float4*>(bpl + (f & 1) * 32 + nt * 16 + 4 * g);
+        const int ti = (m / W + trow0) * WT + (m % W) + 1;
+        *reinterpret_cast<float4*>(tb + (nt * 4 + g) * PLT + ti * 16) =
+            make_float4(silu(acc[k][0] + bb.x), silu(acc[k][1] + bb.y), silu(acc[k][2] + bb.z), silu(acc[k][3] + bb.w));
+      }
+    }
+    // halo rows outside the image (above the first band, below the last) hold zeros
+    if (tid < 8 * W) {
+      const int pl = tid / W, c = tid - pl * W;
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r0 == 0) *reinterpret_cast<float4*>(tb + pl * PLT + (c + 1) * 16) = z;
+      if (r0 + br == H) *reinterpret_cast<float4*>(tb + pl * PLT + ((br + 1) * WT + c + 1) * 16) = z;
+    }
+  };
+
+  // ---- consumer pieces -----------------------------------------------------------------------
+  const int ct = tid - 64 * WS_NP, cw = ct >> 6, cg = ct & 7, cpl = ct >> 3;
+  auto consume = [&](int f, Step d) {
+    const int img = d.img, c0 = d.sl * WS_SL, r0 = d.band * WS_BR, br = min(WS_BR, H - r0);
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    TR(f + 1, 4);
+    // lane = (4-channel plane cg, pixels cpl + 64 k): the plane's 9 taps stay in registers
+    const float* wd = wdl + (f & 1) * 320 + 4 * cg;
+    float w[9][4], b[4];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float4 v = *reinterpret_cast<const float4*>(wd + t * 32);
+      w[t][0] = v.x; w[t][1] = v.y; w[t][2] = v.z; w[t][3] = v.w;
+    }
+    {
+      const float4 v = *reinterpret_cast<const float4*>(wd + 288);
+      b[0] = v.x; b[1] = v.y; b[2] = v.z; b[3] = v.w;
+    }
+    const char* tpl = tiles + (f & 1) * 8 * PLT + cg * PLT;
+    sp_t* ys = reinterpret_cast<sp_t*>(y);
+#pragma unroll
+    for (int k = 0; k < WS_PXL; ++k) {
+      const int p = cpl + 64 * k;
+      if (p < br * W) {
+        const int oy = p / W, ox = p - (p / W) * W;  // band-relative output pixel
+        const char* tp = tpl + (oy * WT + ox) * 16;
+        float a[4] = {b[0], b[1], b[2], b[3]};
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const float4 u = *reinterpret_cast<const float4*>(tp + ((t / 3) * WT + (t % 3)) * 16);
+          a[0] += w[t][0] * u.x;
+          a[1] += w[t][1] * u.y;
+          a[2] += w[t][2] * u.z;
+          a[3] += w[t][3] * u.w;
+          if (t % 3 == 2) asm volatile("" ::: "memory");  // one tap row of loads in flight (registers)
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = silu(a[j]);
+          s[j] += a[j];
+        }
+        act_st4<sp_t>(ys, (long)img * P + (long)(r0 + oy) * W + ox, cs_mid, c0 + 4 * cg, a);
+      }
+    }
+    TR(f + 1, 5);
+    // squeeze partials: the wave's 8 pixel lanes of each plane (lane bits 3..5): a DPP row rotation
+    // inside each 16-lane row, then two cross-row shuffles; one row of 32 channels per wave
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s[j] += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s[j]), 0x128, 0xF, 0xF, false));
+      s[j] += __shfl_xor(s[j], 16);
+      s[j] += __shfl_xor(s[j], 32);
+    }
+    if (lane < 8)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[((f & 1) * WS_NC + cw) * 32 + lane * 4 + j] = s[j];
+  };
+  auto finalize = [&](int f, Step d) {  // slice f's channel sums -> bands -> SE mean (4 channels a wave)
+    if (lane >= 4) return;
+    const int cl = 4 * cw + lane, c = d.sl * WS_SL + cl;
+    const float* rf = red + (f & 1) * WS_NC * 32 + cl;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < WS_NC; ++w) t += rf[32 * w];
+    if (NB > 1) {
+      if (d.band > 0) t += se_acc[c];
+      se_acc[c] = t;
+    }
+    if (d.band == NB - 1) act_st<sp_t>(reinterpret_cast<sp_t*>(se_mean), d.img, cs_mid, c, t / (float)P);
+  };
+
+  // ---- the slice pipeline: producers on f = i, consumers on f = i - 1 (and the squeeze of i - 2) --
+  Step cur{(int)blockIdx.x, 0, 0}, prev{}, prev2{};  // steps i, i - 1, i - 2
+  if (prod && T > 0) issue_w(0, cur);
+  for (int i = 0; i <= T + 1; ++i) {
+    const Step nxt = next_step(cur);
+    TR(i, 0);
+    if (prod) wait_vm0();  // this wave's pieces of W(i) (and taps of i - 1) landed
+    TR(i, 1);
+    lds_fence();
+    __builtin_amdgcn_s_barrier();  // W(i) everywhere; tile[i % 2], W[(i + 1) % 2], taps[i % 2] free
+    TR(i, 2);
+    if (i < T && cur.sl == 0) {  // a new band: its input rows (the producers finished the last band's MFMAs)
+      if (prod) {
+        issue_x(cur.img, cur.band);
+        wait_vm0();
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+    if (prod) {
+      if (i + 1 < T) issue_w(i + 1, nxt);
+      TR(i, 4);
+      if (i < T) {
+        issue_wd(i, cur);  // read by the consumers next iteration
+        TR(i, 5);
+        produce(i, cur);
+      }
+    } else {  // no global loads here: the consumers' VM counter holds only their stores
+      if (i >= 2) finalize(i - 2, prev2);
+      if (i >= 1 && i <= T) consume(i - 1, prev);
+    }
+    TR(i, 3);
+    prev2 = prev;
+    prev = cur;
+    cur = nxt;
+  }
+}
+
+#ifdef IRWS_TRACE
+// Diagnostic build only (-DIRWS_TRACE, M2S_IR_WS_TRACE=1): per-phase s_memtime stamps of workgroup 0's
+// first producer and consumer waves for the first slices of each launch, printed to stderr.
+static void dump_trace(unsigned long long* tr, hipStream_t s, const char* tag) {
+  static int calls = 0;
+  if (++calls > 40) return;
+  std::vector<unsigned long long> h(64 * 2 * 8 * 64);
+  M2S_HIP(hipStreamSynchronize(s));
+  M2S_HIP(hipMemcpy(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost));
+  auto at = [&](int i, int c, int k) { return (long long)h[((i * 2 + c) * 8 + k) * 64]; };
+  fprintf(stderr, "TRACE %s:", tag);
+  for (int i = 2; i < 12; ++i)
+    fprintf(stderr, " [P wait %lld bar %lld dmaw %lld dmawd %lld mfma %lld epi %lld | C bar %lld pre %lld px %lld red %lld]", at(i, 0, 1) - at(i, 0, 0),
+            at(i, 0, 2) - at(i, 0, 1), at(i, 0, 4) - at(i, 0, 2), at(i, 0, 5) - at(i, 0, 4), at(i, 0, 6) - at(i, 0, 5), at(i, 0, 3) - at(i, 0, 6),
+            at(i, 1, 2) - at(i, 1, 0), at(i, 1, 4) - at(i, 1, 2), at(i, 1, 5) - at(i, 1, 4), at(i, 1, 3) - at(i, 1, 5));
+  fprintf(stderr, "\n");
+  M2S_HIP(hipMemset(tr, 0, h.size() * 8));
+}
+#endif
+
+}  // namespace
+
+bool ir_ws_supported(int H, int W, int cs_in, int kp, int cs_mid) {
+  if (!((W == 8 && (kp == 128 || kp == 224)) || (W == 16 && kp == 128)) || H < 1 || H > 64 || cs_in != kp) return false;
+  if (cs_mid % WS_SL != 0 || cs_mid < WS_SL) return false;
+  const WsLayout L = ws_layout(H, W, cs_in, cs_mid);
+  const int cpr = 2 * ws_cpp(cs_in);
+  return L.total <= 160 * 1024 && (L.XR * W * cpr) % 64 == 0 && L.XR * W * cpr / 64 / WS_NP + 1 <= 60 &&
+         2 * ((L.XR * W + 15) / 16) <= WS_NP * WS_UMAX;
+}
+
+void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_mid, const void* wpw, const float* bpw,
+                  const float* wdw, const float* bdw, void* y, void* se_mean, double flops, double bytes,
+                  hipStream_t s) {
+  M2S_CHECK(ir_ws_supported(H, W, cs_in, kp, cs_mid) && N > 0, "ir_ws: unsupported shape");
+  const WsLayout L = ws_layout(H, W, cs_in, cs_mid);
+  static int n_cu = [] {
+    int dev = 0, n = 0;
+    M2S_HIP(hipGetDevice(&dev));
+    M2S_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    return n > 0 ? n : 256;
+  }();
+  const dim3 grid(std::min(N, n_cu));
+#ifdef IRWS_TRACE
+  static unsigned long long* tr = [] {
+    unsigned long long* p = nullptr;
+    if (getenv("M2S_IR_WS_TRACE")) M2S_HIP(hipMalloc(&p, 64 * 2 * 8 * 64 * 8));
+    return p;
+  }();
+#define M2S_IRWS_DUMP(tag) \
+  if (tr) dump_trace(tr, s, tag);
+#else
+  unsigned long long* tr = nullptr;
+#define M2S_IRWS_DUMP(tag)
+#endif
+  const bf16_t* xb = static_cast<const bf16_t*>(x);
+  const bf16_t* wb = static_cast<const bf16_t*>(wpw);
+  bf16_t* yb = static_cast<bf16_t*>(y);
+  bf16_t* mb = static_cast<bf16_t*>(se_mean);
+#define M2S_IRWS(W_, KS_)                                                                               \
+  if (W == W_ && kp == KS_ * 32) {                                                                      \
+    static bool attr = [] {                                                                             \
+      M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ir_ws_kernel<W_, KS_>),                \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));             \
+      return true;                                                                                      \
+    }();                                                                                                \
+    (void)attr;                                                                                         \
+    ProfScope ps("ir_ws_kernel<" #W_ ", " #KS_ ">", flops, bytes, s);                                   \
+    hipLaunchKernelGGL((ir_ws_kernel<W_, KS_>), grid, dim3(64 * (WS_NP + WS_NC)), L.total, s, xb, N, H, cs_mid, wb, \
+                       bpw, wdw, bdw, yb, mb, tr);                                                      \
+    M2S_IRWS_DUMP(#W_ "," #KS_)                                                                         \
+    M2S_HIP(hipGetLastError());                                                                         \
+    return;                                                                                             \
+  }
+  M2S_IRWS(8, 4) M2S_IRWS(8, 7) M2S_IRWS(16, 4)
+#undef M2S_IRWS
+#undef M2S_IRWS_DUMP
+  M2S_CHECK(false, "ir_ws: no variant for this shape");
+}
+
+}  // namespace m2s

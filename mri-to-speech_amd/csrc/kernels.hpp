@@ -37,6 +37,13 @@ void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, co
 
 // The same for a stride-2 depthwise (TF-SAME, top / left pads pad_t / pad_l) on an IH x IW <= 256-pixel
 // conv_pw map: y (N, OH*OW, cs_mid), se_mean over the OH x OW output.  (ir_fused.hip)
+// Split-fp32 stride-1 IR front half (conv_pw + bn1 + SiLU + conv_dw + bn2 + SiLU + SE squeeze) on
+// W = 8 / 16 maps as one persistent warp-specialised workgroup per CU; same outputs as
+// launch_ir_pwdw(split = true).  wdw: fp32 tap-major [9][cs_mid].  (ir_ws.hip)
+bool ir_ws_supported(int H, int W, int cs_in, int kp, int cs_mid);
+void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_mid, const void* wpw, const float* bpw,
+                  const float* wdw, const float* bdw, void* y, void* se_mean, double flops, double bytes,
+                  hipStream_t s);
 bool ir_fused_s2_supported(int IH, int IW, int cs_in, int cs_mid, bool split);
 void launch_ir_pwdw_s2(const void* x, int N, int cs_in, int kp, const void* wpw, const float* bpw, const void* wdw,
                        const float* bdw, int IH, int IW, int OH, int OW, int pad_t, int pad_l, int cs_mid, void* y,

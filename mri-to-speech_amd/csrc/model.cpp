@@ -224,6 +224,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16 || dtype == M2S_DT_BF16X3, "bad dtype");
   M2S_CHECK(n_mels > 0 && hidden > 0 && hidden % 8 == 0, "bad n_mels / rnn_hidden");
   if (const char* e = std::getenv("M2S_IR_FUSED")) ir_fused_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_IR_WS")) ir_ws_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_FUSED")) se_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER_FUSED")) er_fused_ = std::strcmp(e, "0") != 0;
@@ -679,7 +680,12 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         constexpr bool FUSABLE = std::is_same<T, bf16_t>::value || SPL;
         // bf16 feeds the fused kernel bf16 depthwise taps (dword halves), split fp32 the fp32 taps
         const void* wdw = arena_.ptr(SPL ? b.dw_w : b.dw_w2);
-        if (FUSABLE && b.stride == 1 && ir_fused_ && ir_fused_supported(nh, nw, b.c1.cs_in, cs, SPL)) {
+        if (SPL && b.stride == 1 && ir_fused_ && ir_ws_ && ir_ws_supported(nh, nw, b.c1.cs_in, b.c1.kp, cs)) {
+          const double P = (double)nh * nw;
+          launch_ir_ws(cur, nc, nh, nw, b.c1.cs_in, b.c1.kp, cs, b.c1.w, b.c1.b, static_cast<const float*>(arena_.ptr(b.dw_w)),
+                       static_cast<const float*>(arena_.ptr(b.dw_b)), M2, se_mean, 2.0 * nc * P * b.mid * (b.c1.cin + 9),
+                       4.0 * nc * P * (b.c1.cs_in + cs), s);
+        } else if (FUSABLE && b.stride == 1 && ir_fused_ && ir_fused_supported(nh, nw, b.c1.cs_in, cs, SPL)) {
           const double P = (double)nh * nw, es = SPL ? 4.0 : 2.0;
           launch_ir_pwdw(cur, nc, b.c1.cs_in, b.c1.kp, b.c1.w, b.c1.b, wdw, static_cast<const float*>(arena_.ptr(b.dw_b)),
                          nh, nw, cs, M2, se_mean, SPL, 2.0 * nc * P * b.mid * (b.c1.cin + 9),

@@ -52,12 +52,13 @@ class AcousticEngine:
                                       C.byref(h)))
         del keep
         self._h = h
+        self._destroy = L.m2s_acoustic_destroy  # bound now: module globals may be gone at exit
         N.check(L.m2s_acoustic_set_chunk(self._h, int(chunk)))
 
     def __del__(self):
-        h = getattr(self, "_h", None)
-        if h is not None and h.value:
-            N.lib().m2s_acoustic_destroy(h)
+        h, destroy = getattr(self, "_h", None), getattr(self, "_destroy", None)
+        if h is not None and h.value and destroy is not None:
+            destroy(h)
             self._h = None
 
     @property
@@ -110,14 +111,15 @@ class VocoderEngine:
                                      C.byref(v)))
         del keep
         self._h = v
+        self._destroy = L.m2s_vocoder_destroy
         self.hop = 1
         for u in h["upsample_rates"]:
             self.hop *= int(u)
 
     def __del__(self):
-        h = getattr(self, "_h", None)
-        if h is not None and h.value:
-            N.lib().m2s_vocoder_destroy(h)
+        h, destroy = getattr(self, "_h", None), getattr(self, "_destroy", None)
+        if h is not None and h.value and destroy is not None:
+            destroy(h)
             self._h = None
 
     @property

@@ -95,3 +95,20 @@ def test_pipeline_bf16x3_end_to_end(rt, ac_state):
     np.testing.assert_allclose(out["mel_db"], db.numpy(), atol=2e-3, rtol=0)
     np.testing.assert_allclose(out["mel_log"], ln.numpy(), atol=5e-4, rtol=0)
     np.testing.assert_allclose(out["wav"], wav[:, 0].numpy(), atol=2e-4, rtol=0)
+
+
+@pytest.mark.parametrize("hw,n", [((256, 256), 300), ((128, 128), 263)])
+def test_ir_ws_matches_grid_kernel(rt, ac_state, monkeypatch, hw, n):
+    """The persistent warp-specialised IR front half (ir_ws.hip: 16x16 and 8x8 maps, more images than
+    workgroups) against the one-slice-per-workgroup kernel it replaces (M2S_IR_WS=0).  Same split fp32
+    arithmetic except the order of the squeeze sums, which moves a few hi/lo roundings (17-bit
+    values): the two differ by about their own distance from the fp32 oracle (~1e-5 of the scale,
+    tools/diag_ir_ws.py), so the bar is the parity bar, 1e-4."""
+    fr = torch.from_numpy(synth.synth_frames(1, n, hw=hw, seed=7)[0]).to(DEV)
+    ws = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    monkeypatch.setenv("M2S_IR_WS", "0")
+    grid = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    for i in (10, 12, 13, 18, 24, 28):  # after blocks 3.1, 3.3, 4.0, 4.5, 5.5, 5.9
+        a, b = ws.probe(fr, i).cpu().numpy(), grid.probe(fr, i).cpu().numpy()
+        assert _rel(a, b) <= 1e-4, f"tap {i}: {_rel(a, b)}"
+    assert _rel(ws.effnet(fr).cpu().numpy(), grid.effnet(fr).cpu().numpy()) <= 1e-4
