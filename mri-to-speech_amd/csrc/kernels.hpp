@@ -128,6 +128,12 @@ bool lstm_persistent_supported(int H);
 size_t lstm_persistent_sync_bytes();
 // `spin_max` bounds each barrier wait (polls with s_sleep 1); on a timeout the kernel stores 1 to
 // `err_host` (pinned, host-mapped) and writes NaN to the rest of the outputs.
+// Small batches (B <= 4): the same recurrence with h exchanged as data-tagged granules instead of a
+// counter barrier, VALU dot products (lstm_persistent.hip).  `sync` = lstm_small_sync_bytes().
+bool lstm_small_supported(int B, int H);
+size_t lstm_small_sync_bytes();
+void launch_lstm_small(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,
+                       unsigned* err_host, hipStream_t s);
 constexpr unsigned LSTM_SPIN_MAX = 1u << 24;
 void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync,
                             unsigned spin_max, unsigned* err_host, hipStream_t s);

@@ -175,9 +175,157 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
   }
 }
 
+
+// ---- small batches (B <= LS_BMAX: the 1 x 1000-frame configs[4] clip, the 1 x 30 configs[0] clip) -----
+// At B = 1 the 32-wide MFMA B tile is 1/32 used and the counter barrier (store drain, agent release,
+// atomic, relaxed polls, acquire + L2 refill of h) cost ~20 us a step.  Here h_t travels as data-
+// tagged 8-byte granules {tag = step + 1, value = h} written by ONE sc1 atomic store each
+// (cdna_hip_programming.md Guideline 16 R2: the data is the flag, no fence, no counter); every
+// workgroup of the direction sweeps the B x 640 granules of h_{t-1} with relaxed agent loads until
+// every tag matches, into LDS.  Granules are double-buffered by step parity (a workgroup can run at
+// most one step ahead of any other: publishing h_{t+1} needs every h_t).  The recurrence products
+// run on VALU: lane (wave, k half, row) holds the same 80 W_hh values as above and forms B fp32 dot
+// products of 80 terms; the 8 K-slice partials of each gate row are summed in LDS in a fixed order.
+constexpr int LS_BMAX = 4;
+
+__global__ void __launch_bounds__(256, 1) lstm_small_kernel(const float* __restrict__ pre, const float* __restrict__ whh,
+                                                            float* hs, int B, int T, unsigned long long* gran,
+                                                            unsigned* err, unsigned spin_max, unsigned* err_host) {
+  __shared__ __attribute__((aligned(16))) float hsh[LS_BMAX][LP_H];  // h_{t-1}, all units
+  __shared__ float red[8][32][LS_BMAX];                              // [K slice][gate row][sequence]
+  __shared__ float cst[LP_U][LS_BMAX];
+  __shared__ int abort_flag;
+  const int H = LP_H;
+  const int dir = blockIdx.x / (H / LP_U), ug = blockIdx.x - dir * (H / LP_U);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kk = lane >> 5, l32 = lane & 31;
+  const int kbase = wave * LP_KW + kk * LP_KH;
+  float* hsd = hs + (size_t)dir * B * T * H;
+  unsigned long long* gd = gran + (size_t)dir * 2 * LS_BMAX * H;
+
+  float wa[LP_KH];
+  {
+    const int r = l32, g = r / LP_U, u = ug * LP_U + (r % LP_U);
+    const float* wr = whh + ((size_t)dir * 4 * H + (size_t)g * H + u) * H + kbase;
+#pragma unroll
+    for (int s = 0; s < LP_KH; s += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(wr + s);
+      wa[s] = v.x;
+      wa[s + 1] = v.y;
+      wa[s + 2] = v.z;
+      wa[s + 3] = v.w;
+    }
+  }
+  if (tid < LP_U * LS_BMAX) (&cst[0][0])[tid] = 0.f;
+  if (tid == 0) abort_flag = 0;
+  __syncthreads();
+
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? step : T - 1 - step;
+    float p[LS_BMAX] = {0.f, 0.f, 0.f, 0.f};
+    if (step > 0) {
+      // ---- h_{t-1}: sweep the direction's granules (tag == step) into LDS -----------------------
+      const unsigned long long* src = gd + (size_t)((step - 1) & 1) * LS_BMAX * H;
+      bool ok = true;
+      for (int i = tid; i < B * H && ok; i += 256) {
+        unsigned spins = 0;
+        unsigned long long x;
+        while (((x = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != (unsigned)step) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > spin_max || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            abort_flag = 1;
+            ok = false;
+            break;
+          }
+        }
+        hsh[i / H][i % H] = __uint_as_float((unsigned)x);
+      }
+      __syncthreads();
+      if (abort_flag) {  // a peer stopped publishing: flag the host, poison the remaining outputs, leave
+        if (tid == 0 && err_host) __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int st = step; st < T; ++st) {
+          const int tt = dir == 0 ? st : T - 1 - st;
+          for (int q = tid; q < LP_U * B; q += 256)
+            hsd[((size_t)(q / LP_U) * T + tt) * H + ug * LP_U + q % LP_U] = __builtin_nanf("");
+        }
+        return;
+      }
+      // ---- this lane's 80-term K-slice dot products for gate row l32 -----------------------------
+#pragma unroll
+      for (int b = 0; b < LS_BMAX; ++b) {
+        if (b >= B) break;
+        const float* hb = &hsh[b][kbase];
+        float a = 0.f;
+#pragma unroll
+        for (int s = 0; s < LP_KH; s += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(hb + s);
+          a += wa[s] * v.x;
+          a += wa[s + 1] * v.y;
+          a += wa[s + 2] * v.z;
+          a += wa[s + 3] * v.w;
+        }
+        p[b] = a;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < LS_BMAX; ++b) red[wave * 2 + kk][l32][b] = p[b];
+    __syncthreads();
+    // ---- cell update for (unit, sequence); publish h_t as granules (tag = step + 1) ---------------
+    if (tid < LP_U * B) {
+      const int u = tid % LP_U, b = tid / LP_U, unit = ug * LP_U + u;
+      float gs[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int r = g * LP_U + u;
+        gs[g] = ((red[0][r][b] + red[1][r][b]) + (red[2][r][b] + red[3][r][b])) +
+                ((red[4][r][b] + red[5][r][b]) + (red[6][r][b] + red[7][r][b]));
+      }
+      const float* pr = pre + ((size_t)b * T + t) * 8 * H + (size_t)dir * 4 * H;
+      const float gi = sigmoid_exact(pr[unit] + gs[0]);
+      const float gf = sigmoid_exact(pr[H + unit] + gs[1]);
+      const float gg = tanhf(pr[2 * H + unit] + gs[2]);
+      const float go = sigmoid_exact(pr[3 * H + unit] + gs[3]);
+      const float c = step > 0 ? gf * cst[u][b] + gi * gg : gi * gg;
+      cst[u][b] = c;
+      const float h = go * tanhf(c);
+      hsd[((size_t)b * T + t) * H + unit] = h;
+      if (step + 1 < T)
+        __hip_atomic_store(gd + (size_t)(step & 1) * LS_BMAX * H + (size_t)b * H + unit,
+                           ((unsigned long long)(step + 1) << 32) | __float_as_uint(h), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();  // red and hsh are rewritten next step
+  }
+}
+
 }  // namespace
 
 bool lstm_persistent_supported(int H) { return H == LP_H; }
+
+bool lstm_small_supported(int B, int H) { return H == LP_H && B >= 1 && B <= LS_BMAX; }
+
+size_t lstm_small_sync_bytes() { return 256 + (size_t)2 * 2 * LS_BMAX * LP_H * sizeof(unsigned long long); }
+
+void launch_lstm_small(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,
+                       unsigned* err_host, hipStream_t s) {
+  M2S_CHECK(lstm_small_supported(B, H) && T > 0, "lstm_small: unsupported shape");
+  const int grid = 2 * (H / LP_U);
+  static const int resident = [] {
+    int dev = 0, cus = 0, per_cu = 0;
+    M2S_HIP(hipGetDevice(&dev));
+    M2S_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    M2S_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&lstm_small_kernel), 256, 0));
+    return cus * per_cu;
+  }();
+  M2S_CHECK(grid <= resident, "lstm_small: grid not co-resident on this device");
+  // [256 B: error word][granules 2 dir x 2 parity x LS_BMAX x H]: every tag restarts at 0 each call
+  M2S_HIP(hipMemsetAsync(sync, 0, lstm_small_sync_bytes(), s));
+  unsigned* err = static_cast<unsigned*>(sync);
+  unsigned long long* gran = reinterpret_cast<unsigned long long*>(static_cast<char*>(sync) + 256);
+  hipLaunchKernelGGL(lstm_small_kernel, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, T, gran, err, spin_max, err_host);
+  M2S_HIP(hipGetLastError());
+}
 
 size_t lstm_persistent_sync_bytes() { return 256; }
 

@@ -278,10 +278,11 @@ def test_pipeline_end_to_end(rt, ac_state, dtype):
 
 
 # ------------------------------------------------------------------------------ persistent BiLSTM
-@pytest.mark.parametrize("B,T", [(1, 1000), (3, 64), (70, 6)])
+@pytest.mark.parametrize("B,T", [(1, 1000), (3, 64), (4, 40), (70, 6)])
 def test_bilstm_persistent_long_and_wide(rt, ac_state, monkeypatch, B, T):
     """One-launch recurrence (lstm_persistent.hip) vs the oracle and vs the per-step kernel:
-    a 1000-frame clip (configs[4] length), a batch above the 64-sequence launch limit."""
+    a 1000-frame clip (configs[4] length; B <= 4 runs the granule-exchange lstm_small_kernel, B = 4
+    its largest batch), a batch above the 64-sequence launch limit."""
     sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
     x = torch.from_numpy(np.random.default_rng(B * 7 + T).normal(0, 0.5, (B, T, 208)).astype(np.float32))
     monkeypatch.setenv("M2S_LSTM_PERSISTENT", "1")
