@@ -15,7 +15,8 @@ hi + lo and every product the three exact bf16 MFMA terms hi*hi + hi*lo + lo*hi 
 (include/m2s.h).  The line carries its measured error against the fp32 CPU oracle on clip 0 of the
 same workload (``parity``), next to the fp32 tolerances of tests/test_gpu_configs.py.  At N = 1 a
 second, shorter run of the bf16 path (configs[1]'s dtype) is reported under ``bf16`` with its own
-error; it is not the headline.
+error, and one of the fp8 path (configs[4]'s precision: e4m3 MFMA operands) under ``fp8`` with its
+error and cosine similarity; neither is the headline.
 
 Launch: ``python bench.py`` (N=1) or
 ``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N``.
@@ -43,7 +44,9 @@ HOP = 420
 SR = 11413
 # dense MFMA peaks (MI355X_MICROARCH.md): per ALGORITHMIC flop, so bf16x3 (three bf16 MFMAs per
 # product) peaks at a third of the bf16 rate
-PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "bf16x3": 2500.0 / 3}
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "bf16x3": 2500.0 / 3,
+               # non-scaled v_mfma_f32_16x16x32_fp8_fp8 runs at the bf16 rate (MI355X_MICROARCH.md)
+               "fp8": 2500.0}
 PEAK_HBM_GBS = 8000.0
 FP32_TOL = {"mel_norm": 1e-4, "mel_log": 5e-4, "wav": 2e-4}  # tests/test_gpu_configs.py
 PRECISION = {
@@ -51,6 +54,8 @@ PRECISION = {
               "BiLSTM/head/glue exact fp32",
     "fp32": "exact f32 MFMA products (v_mfma_f32_16x16x4_f32), fp32 storage",
     "bf16": "bf16 storage and operands, fp32 accumulate; BiLSTM/head/glue fp32",
+    "fp8": "e4m3 MFMA operands (per-output-channel weight scales) for the backbone and MRF convs, bf16 "
+           "storage, SE / conv_pre / upsamplers bf16; BiLSTM/head/glue fp32",
 }
 
 MFMA_KERNELS = ("conv_gemm_kernel", "conv_halo_kernel", "conv_igemm_kernel", "ir_pwdw", "lstm_persistent_kernel",
@@ -87,13 +92,13 @@ def parse(argv=None):
     p.add_argument("--clips", type=int, default=64, help="clips per GPU")
     p.add_argument("--frames", type=int, default=30, help="frames per clip")
     p.add_argument("--hw", type=int, default=256)
-    p.add_argument("--dtype", default="bf16x3", choices=["bf16x3", "fp32", "bf16"])
+    p.add_argument("--dtype", default="bf16x3", choices=["bf16x3", "fp32", "bf16", "fp8"])
     p.add_argument("--chunk", type=int, default=1920, help="frames per CNN pass (1920 = one pass over the 64x30 step)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-profile", action="store_true")
     p.add_argument("--no-parity", action="store_true", help="skip the oracle check of clip 0")
-    p.add_argument("--no-compare", action="store_true", help="skip the secondary bf16 line (N = 1)")
+    p.add_argument("--no-compare", action="store_true", help="skip the secondary bf16 / fp8 lines (N = 1)")
     return p.parse_args(argv)
 
 
@@ -154,6 +159,17 @@ def parity_vs(ref, out, clip=0):
     res = {f"{k}_max_abs": float(np.abs(got[k] - ref[k]).max()) for k in got}
     res["wav_snr_db"] = round(float(10 * np.log10(np.sum(rw ** 2) / max(np.sum((w - rw) ** 2), 1e-30))), 2)
     res["within_fp32_tol"] = all(res[f"{k}_max_abs"] <= t for k, t in FP32_TOL.items())
+    return res
+
+
+def cosine_vs(ref, out, clip=0):
+    """Cosine similarity of mel_norm and wav against the oracle (the fp8 tolerance)."""
+    res = {}
+    for k in ("mel_norm", "wav"):
+        a = out[k][clip:clip + 1].float().cpu().numpy().astype(np.float64).ravel()
+        b = ref[k].astype(np.float64).ravel()
+        res[f"{k}_cos"] = round(float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b) + 1e-30)), 6)
+    res["within_cos_0.99"] = all(v >= 0.99 for v in res.values())
     return res
 
 
@@ -298,18 +314,21 @@ def main():
     if rank == 0 and not args.no_parity:  # clip 0 of this rank's workload through the fp32 oracle
         ref0 = oracle_clip(ac_sd, gen_sd, mean, std, frames[:1].cpu().numpy())
         result["parity"] = dict(parity_vs(ref0, out), clip=0, tolerance=FP32_TOL, reference="fp32 CPU oracle")
-    if world == 1 and not args.no_compare and args.dtype != "bf16":
+    if world == 1 and not args.no_compare:  # secondary lines: the narrower dtypes on the same workload
         del pipe
-        bpipe = build("bf16")
-        for _ in range(args.warmup):
-            step(bpipe)
-        k = max(5, args.steps // 2)
-        el = timed_loop(lambda: step(bpipe), k, world, sync, device)
-        result["bf16"] = {"value": round(B * T * k / el, 2), "ms_per_step": round(1000.0 * el / k, 3), "steps": k,
-                          "precision": PRECISION["bf16"]}
-        if ref0 is not None:
-            result["bf16"]["parity"] = parity_vs(ref0, out)
-        del bpipe
+        for dt in ("bf16", "fp8"):
+            if dt == args.dtype:
+                continue
+            p2 = build(dt)
+            for _ in range(args.warmup):
+                step(p2)
+            k = max(5, args.steps // 2)
+            el = timed_loop(lambda: step(p2), k, world, sync, device)
+            result[dt] = {"value": round(B * T * k / el, 2), "ms_per_step": round(1000.0 * el / k, 3), "steps": k,
+                          "precision": PRECISION[dt]}
+            if ref0 is not None:
+                result[dt]["parity"] = dict(parity_vs(ref0, out), **cosine_vs(ref0, out))
+            del p2
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, ac_sd, gen_sd, mean, std)
     if rank == 0:

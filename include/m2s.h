@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define M2S_ABI_VERSION 2
+#define M2S_ABI_VERSION 3
 
 enum m2s_status { M2S_OK = 0, M2S_E_ARG = 1, M2S_E_HIP = 2, M2S_E_STATE = 3, M2S_E_NODEV = 4, M2S_E_INTERNAL = 5 };
 /* compute dtype of the convolution stacks (BiLSTM, head and glue always run in fp32):
@@ -39,8 +39,12 @@ enum m2s_status { M2S_OK = 0, M2S_E_ARG = 1, M2S_E_HIP = 2, M2S_E_STATE = 3, M2S
  *   M2S_DT_BF16   bf16 storage and operands, fp32 accumulation
  *   M2S_DT_BF16X3 split fp32: every activation / weight is a bf16 pair hi + lo (17 significant
  *                 bits), products are the three bf16 MFMA terms hi*hi + hi*lo + lo*hi with fp32
- *                 accumulation; meets the fp32 tolerances of the parity tests */
-enum m2s_dtype { M2S_DT_F32 = 0, M2S_DT_BF16 = 1, M2S_DT_BF16X3 = 2 };
+ *                 accumulation; meets the fp32 tolerances of the parity tests
+ *   M2S_DT_FP8    e4m3 operands (configs[4]): the backbone convs and the MRF resblock convs run
+ *                 v_mfma_f32_16x16x32_fp8_fp8 on OCP e4m3fn weights with per-output-channel fp32
+ *                 scales and activations rounded to e4m3 at the operand read; bf16 storage, SE
+ *                 excitation, conv_pre / upsamplers and conv_post stay bf16 (ABI 3) */
+enum m2s_dtype { M2S_DT_F32 = 0, M2S_DT_BF16 = 1, M2S_DT_BF16X3 = 2, M2S_DT_FP8 = 3 };
 /* host tensor element types */
 enum m2s_elem { M2S_ELEM_F32 = 0, M2S_ELEM_I64 = 1 };
 

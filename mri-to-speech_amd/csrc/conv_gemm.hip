@@ -105,6 +105,26 @@ __device__ __forceinline__ void scale_split(bf16x8& h, bf16x8& l, const float* s
   resplit_frag(v, h, l);
 }
 
+// 8 bf16 -> 8 OCP e4m3fn (gfx950 v_cvt_pk_fp8_f32, round to nearest even), clamped to +-448 (the
+// largest finite e4m3: the conversion has no saturating mode)
+__device__ __forceinline__ long fp8x8(bf16x8 v) {
+  const uint4 u = __builtin_bit_cast(uint4, v);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+  int q[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float f[4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      f[2 * j] = fminf(fmaxf(__uint_as_float(w[2 * h + j] << 16), -448.f), 448.f);
+      f[2 * j + 1] = fminf(fmaxf(__uint_as_float(w[2 * h + j] & 0xffff0000u), -448.f), 448.f);
+    }
+    int r = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+    q[h] = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], r, true);
+  }
+  return (long)(((unsigned long)(uint32_t)q[1] << 32) | (uint32_t)q[0]);
+}
+
 __device__ __forceinline__ void ld4f(const bf16_t* p, float* v) {
   const uint2 u = *reinterpret_cast<const uint2*>(p);
   v[0] = __uint_as_float(u.x << 16);
@@ -127,18 +147,19 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * ROW + ((ch
 // SP = 1: split-fp32 operands (m2s_common.hpp sp_t): every activation and weight row is [hi | lo],
 // each K step DMAs both halves into two planes of the slot and runs the three MFMA terms
 // hi*hi + hi*lo + lo*hi (the dropped lo*lo term is below 2^-16 of the product).
+// SP = 2: e4m3 operands over bf16 storage (conv_igemm.hpp launch_conv_gemm, a.wscale).
 template <int BM, int BN, int MT, int NT, int S, int KIND, int XF, int SP>
 __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 2 : 1)) conv_gemm_kernel(const ConvArgs a, int n_tiles, int se_imgs) {
   constexpr int WN = BN / (NT * 16);
   constexpr int WM = 4 / WN;
   static_assert(WM * WN == 4 && WM * MT * 16 == BM, "bad tile");
-  constexpr int R = SP ? 2 : 1;                    // planes per operand row
+  constexpr int R = SP == 1 ? 2 : 1;               // planes per operand row
   constexpr int A_PER_WAVE = BM / 64;              // 16-row DMA blocks per wave for A
   constexpr int B_BLOCKS = BN / 16;                // 16-row DMA blocks for B
   constexpr int B_PER_WAVE = (B_BLOCKS + 3) / 4;   // waves >= B_BLOCKS issue into a scratch block
   constexpr int SLOT = (R * (BM + BN) + 16) * ROW; // +16 rows: scratch for surplus B DMAs
   constexpr int PER_STAGE = R * (A_PER_WAVE + B_PER_WAVE);
-  constexpr bool PRE = SP && XF == IN_SE_SCALE;    // split SE scale applied in LDS (below)
+  constexpr bool PRE = SP == 1 && XF == IN_SE_SCALE;  // split SE scale applied in LDS (below)
   constexpr bool SE = XF == IN_SE_SCALE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* se_tab = reinterpret_cast<float*>(smem + S * SLOT);
@@ -237,7 +258,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
       const bool v = s_tap < 32 && ((rmask[j] >> s_tap) & 1u);
       const bf16_t* src = X + (unsigned)(rbase[j] + s_off);
       dma16(v ? static_cast<const void*>(src) : static_cast<const void*>(zp), As + (wave * A_PER_WAVE + j) * 16 * ROW);
-      if constexpr (SP)
+      if constexpr (SP == 1)
         dma16(v ? static_cast<const void*>(src + a.cs_in) : static_cast<const void*>(zp),
               As + (BM + (wave * A_PER_WAVE + j) * 16) * ROW);
     }
@@ -246,7 +267,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
       const int blk = wave * B_PER_WAVE + j;
       const void* src = bsrc[j] ? (const void*)(bsrc[j] + st * 32) : (const void*)zp;
       dma16(src, blk < B_BLOCKS ? Bs + blk * 16 * ROW : As + R * (BM + BN) * ROW);
-      if constexpr (SP)
+      if constexpr (SP == 1)
         dma16(bsrc[j] ? (const void*)(bsrc[j] + st * 32 + a.kp) : (const void*)zp,
               blk < B_BLOCKS ? Bs + (BN + blk * 16) * ROW : As + R * (BM + BN) * ROW);
     }
@@ -270,7 +291,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
     for (int i = tid; i < se_imgs * a.cs_in; i += 256) {
       const int im = i / a.cs_in, c = i - (i / a.cs_in) * a.cs_in;
       const bf16_t* g = static_cast<const bf16_t*>(a.in_scale) + (size_t)(img0 + im) * xs + c;
-      se_tab[i] = (img0 + im) * a.OH < a.M ? (SP ? bf2f(g[0]) + bf2f(g[a.cs_in]) : bf2f(g[0])) : 0.f;
+      se_tab[i] = (img0 + im) * a.OH < a.M ? (SP == 1 ? bf2f(g[0]) + bf2f(g[a.cs_in]) : bf2f(g[0])) : 0.f;
     }
   }
   // SE scale on the weight fragments when the tile is one image (its k-scales are shared by every
@@ -301,7 +322,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi)
       bx[mi] = *reinterpret_cast<const bf16x8*>(As + swz(wm * MT * 16 + mi * 16 + r16, g));
-    if constexpr (SP) {
+    if constexpr (SP == 1) {
       bf16x8 afl[NT], bxl[MT];
 #pragma unroll
       for (int ni = 0; ni < NT; ++ni)
@@ -336,6 +357,19 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
 #pragma unroll
         for (int mi = 0; mi < MT; ++mi) bx[mi] = scale_frag(bx[mi], se_tab + frow_img[mi] * a.cs_in + st * 32 + g * 8);
       }
+    }
+    if constexpr (SP == 2) {  // e4m3: weights are on the grid (exact), activations round here
+      long a8[NT], b8[MT];
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) a8[ni] = fp8x8(af[ni]);
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) b8[mi] = fp8x8(bx[mi]);
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi)
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a8[ni], b8[mi], acc[ni][mi], 0, 0, 0);
+      return;
     }
 #pragma unroll
     for (int ni = 0; ni < NT; ++ni)
@@ -444,6 +478,13 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
       if (n4 >= a.cs_out) continue;
       const float4 bb = *reinterpret_cast<const float4*>(a.bias + n4);
       float v[4] = {acc[ni][mi][0] + bb.x, acc[ni][mi][1] + bb.y, acc[ni][mi][2] + bb.z, acc[ni][mi][3] + bb.w};
+      if constexpr (SP == 2) {  // e4m3 weights carry a per-output-channel scale
+        const float4 ws = *reinterpret_cast<const float4*>(a.wscale + n4);
+        v[0] = fmaf(acc[ni][mi][0], ws.x, bb.x);
+        v[1] = fmaf(acc[ni][mi][1], ws.y, bb.y);
+        v[2] = fmaf(acc[ni][mi][2], ws.z, bb.z);
+        v[3] = fmaf(acc[ni][mi][3], ws.w, bb.w);
+      }
       if (a.act == ACT_SILU) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = silu(v[j]);
@@ -457,7 +498,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
       if (Rs) {
         float r[4];
         ld4f(Rs + orow + n4, r);
-        if constexpr (SP) {
+        if constexpr (SP == 1) {
           float rl[4];
           ld4f(Rs + orow + a.cs_out + n4, rl);
 #pragma unroll
@@ -469,7 +510,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
       if (a.accum) {
         float p[4];
         ld4f(Y + orow + n4, p);
-        if constexpr (SP) {
+        if constexpr (SP == 1) {
           float pl[4];
           ld4f(Y + orow + a.cs_out + n4, pl);
 #pragma unroll
@@ -482,7 +523,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
           for (int j = 0; j < 4; ++j) v[j] = v[j] / a.accum_div;
         }
       }
-      if constexpr (SP) {
+      if constexpr (SP == 1) {
         uint2 hi, lo;
         split4(v, hi, lo);
         *reinterpret_cast<uint2*>(Y + orow + n4) = hi;
@@ -513,8 +554,8 @@ template <int BM, int BN, int MT, int NT, int KIND, int XF, int SP>
 void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
   // keep two workgroups' LDS per CU (128 x 256: the SE gate table too, and 256 registers a wave);
   // split operands double the slot, so they run two stages
-  constexpr int S = SP ? 2 : (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
-  constexpr int R = SP ? 2 : 1;
+  constexpr int S = SP == 1 ? 2 : (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
+  constexpr int R = SP == 1 ? 2 : 1;
   static bool attr = [] {
     M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF, SP>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -533,7 +574,7 @@ void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
   char name[96];
   static const bool detail = getenv("M2S_PROF_DETAIL") != nullptr;
   if (detail)  // per-layer records for analysis: K x N and rows per launch
-    snprintf(name, sizeof(name), "conv_gemm<%s,%dx%d%s> K%d N%d M%d", kname(KIND), BM, BN, SP ? ",x3" : "", a.kp, a.cs_out, a.M);
+    snprintf(name, sizeof(name), "conv_gemm<%s,%dx%d%s> K%d N%d M%d", kname(KIND), BM, BN, SP == 1 ? ",x3" : SP == 2 ? ",e4m3" : "", a.kp, a.cs_out, a.M);
   else
     snprintf(name, sizeof(name), "conv_gemm_kernel<%d, %d, %d, %d, %d, %d, %d, %d>", BM, BN, MT, NT, S, KIND, XF, SP);
   ProfScope ps(name, flops, bytes, s);
@@ -543,14 +584,14 @@ void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
 template <int KIND, int XF, int SP>
 void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
   const int n = a.cs_out;
-  if constexpr (SP) {  // split operands: 16/32/64-wide tiles for narrow outputs, else 128 x 128
+  if constexpr (SP != 0) {  // split / e4m3 operands: 16/32/64-wide tiles for narrow outputs, else 128 x 128
     if (n <= 16)
-      return launch_tile<256, 16, 4, 1, KIND, XF, 1>(a, s, phases, flops, bytes);
+      return launch_tile<256, 16, 4, 1, KIND, XF, SP>(a, s, phases, flops, bytes);
     if (n <= 32)
-      return launch_tile<256, 32, 4, 2, KIND, XF, 1>(a, s, phases, flops, bytes);
+      return launch_tile<256, 32, 4, 2, KIND, XF, SP>(a, s, phases, flops, bytes);
     if (n <= 64 || (n % 128 != 0 && ceil_div(n, 64) * 64 < ceil_div(n, 128) * 128))
-      return launch_tile<256, 64, 4, 4, KIND, XF, 1>(a, s, phases, flops, bytes);
-    return launch_tile<128, 128, 4, 4, KIND, XF, 1>(a, s, phases, flops, bytes);
+      return launch_tile<256, 64, 4, 4, KIND, XF, SP>(a, s, phases, flops, bytes);
+    return launch_tile<128, 128, 4, 4, KIND, XF, SP>(a, s, phases, flops, bytes);
   } else {
   if constexpr (KIND == KIND_GEMM || KIND == KIND_CONV2D) if (a.M >= 256 * 256 && n > 128 &&
                                                                ((n <= 256 && a.kp >= 512) || KIND == KIND_GEMM)) {
@@ -610,12 +651,24 @@ void launch_conv_gemm(const ConvArgs& a, bool split, hipStream_t s, double flops
   M2S_CHECK(a.kp % 32 == 0 && a.kp >= a.ntaps * a.cs_in, "conv_gemm: kp");
   M2S_CHECK(a.kind != KIND_CONV2D || a.ks == 3, "conv_gemm: 2-D kernels are 3x3 (1x1 runs as GEMM)");
   if (a.M <= 0) return;
+  M2S_CHECK(!(split && a.wscale), "conv_gemm: e4m3 operands take bf16 storage");
   if (split) {
     switch (a.kind) {
       case KIND_CONV2D: launch_kind<KIND_CONV2D, 1>(a, s, 1, flops, bytes); break;
       case KIND_CONV1D: launch_kind<KIND_CONV1D, 1>(a, s, 1, flops, bytes); break;
       case KIND_CONVT: launch_kind<KIND_CONVT, 1>(a, s, a.ct_u, flops, bytes); break;
       case KIND_GEMM: launch_kind<KIND_GEMM, 1>(a, s, 1, flops, bytes); break;
+      default: M2S_CHECK(false, "conv_gemm: bad kind");
+    }
+    M2S_HIP(hipGetLastError());
+    return;
+  }
+  if (a.wscale) {  // e4m3 operands
+    switch (a.kind) {
+      case KIND_CONV2D: launch_kind<KIND_CONV2D, 2>(a, s, 1, flops, bytes); break;
+      case KIND_CONV1D: launch_kind<KIND_CONV1D, 2>(a, s, 1, flops, bytes); break;
+      case KIND_CONVT: launch_kind<KIND_CONVT, 2>(a, s, a.ct_u, flops, bytes); break;
+      case KIND_GEMM: launch_kind<KIND_GEMM, 2>(a, s, 1, flops, bytes); break;
       default: M2S_CHECK(false, "conv_gemm: bad kind");
     }
     M2S_HIP(hipGetLastError());

@@ -30,6 +30,7 @@ struct ConvArgs {
   const void* res;      // residual, same layout as y (or null)
   void* y;              // output, channel-last, channel stride cs_out
   const void* in_scale; // IN_SE_SCALE: [img][cs_in] in the compute dtype (SE gates)
+  const float* wscale;  // fp8 operands (M2S_DT_FP8): [n_pad] per-output-channel weight scales, else null
   int kind;
   int M;                // GEMM rows (output positions per phase)
   int cs_in, cs_out;    // channel strides
@@ -54,7 +55,10 @@ struct ConvArgs {
 // f32-MFMA parity path) runs the direct-load kernel of conv_igemm.hip.
 template <typename T>
 void launch_conv(const ConvArgs& a, hipStream_t s, double flops = 0.0, double bytes = 0.0);
-// split: x, w, res, y and in_scale hold [hi | lo] rows (m2s_common.hpp sp_t); w rows are 2 * kp long
+// split: x, w, res, y and in_scale hold [hi | lo] rows (m2s_common.hpp sp_t); w rows are 2 * kp long.
+// a.wscale set (bf16 storage only): e4m3 operands - w holds e4m3-grid values (exact in bf16) of
+// w / wscale[n], the activation fragments are rounded to e4m3 after the LDS read, the products run
+// on v_mfma_f32_16x16x32_fp8_fp8 and the epilogue multiplies by wscale[n].
 void launch_conv_gemm(const ConvArgs& a, bool split, hipStream_t s, double flops, double bytes);
 // bf16 3x3 stride-1 convs with cs_in in {32, 64}: persistent LDS-resident-weight kernel
 // (conv_halo.hip); launch_conv_gemm routes them there.

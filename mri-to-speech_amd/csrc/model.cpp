@@ -89,8 +89,20 @@ static std::string tname(const char* base, const char* extra = "") {
 }
 
 static int kc_of(int dtype) { return dtype == M2S_DT_F32 ? Elem<float>::KC : Elem<bf16_t>::KC; }
-// bytes per activation element of a dtype's storage (split fp32: hi + lo)
-static size_t act_bytes(int dtype) { return dtype == M2S_DT_BF16 ? 2 : 4; }
+// bytes per activation element of a dtype's storage (split fp32: hi + lo; e4m3 operands keep bf16)
+static size_t act_bytes(int dtype) { return dtype == M2S_DT_BF16 || dtype == M2S_DT_FP8 ? 2 : 4; }
+
+// OCP e4m3fn rounding of a float (round to nearest even; 3 mantissa bits, exponents -6..8 with
+// subnormals down to 2^-9, largest finite 448): the grid gfx950's v_cvt_pk_fp8_f32 rounds onto.
+static float e4m3_host(float x) {
+  if (!(x == x) || x == 0.f) return 0.f;
+  const float a = std::fabs(x);
+  if (a >= 448.f) return std::copysign(448.f, x);
+  int e;
+  std::frexp(a, &e);                       // a = m * 2^e, m in [0.5, 1): leading bit 2^(e-1)
+  const float step = std::ldexp(1.f, std::max(e - 1, -6) - 3);
+  return std::copysign(std::nearbyint(a / step) * step, x);
+}
 
 // fp32 -> split pair (hi, lo) on the host, as the device's split4
 static void split_host(float f, uint16_t* hi, uint16_t* lo);
@@ -119,7 +131,20 @@ static void pack_conv(Arena& ar, int dtype, PConv& p, Get get, Bias bias) {
       for (int t = 0; t < p.ntaps; ++t)
         for (int c = 0; c < p.cin; ++c)
           w[((size_t)ph * p.n_pad + n) * p.kp + (size_t)t * p.cs_in + c] = get(ph, n, t, c);
-  if (dtype == M2S_DT_BF16) {
+  if (dtype == M2S_DT_FP8) {  // per output channel: s = amax / 448, w / s on the e4m3 grid (exact in bf16)
+    std::vector<float> sc(p.n_pad, 1.f);
+    for (int n = 0; n < p.n_pad; ++n) {
+      float amax = 0.f;
+      for (int ph = 0; ph < p.phases; ++ph)
+        for (int k = 0; k < p.kp; ++k) amax = std::max(amax, std::fabs(w[((size_t)ph * p.n_pad + n) * p.kp + k]));
+      if (amax > 0.f) sc[n] = amax / 448.f;
+    }
+    std::vector<uint16_t> h(w.size());
+    for (size_t i = 0; i < w.size(); ++i) h[i] = f2bf_host(e4m3_host(w[i] / sc[(i / p.kp) % p.n_pad]));
+    p.w_off = ar.add_vec(h);
+    p.ws_off = ar.add_vec(sc);
+    p.fp8 = true;
+  } else if (dtype == M2S_DT_BF16) {
     std::vector<uint16_t> h(w.size());
     for (size_t i = 0; i < w.size(); ++i) h[i] = f2bf_host(w[i]);
     p.w_off = ar.add_vec(h);
@@ -158,6 +183,7 @@ static ConvArgs conv_args(const PConv& p) {
   a.ct_k = p.ct_k;
   a.OH = 1;
   a.accum_div = 1.f;
+  a.wscale = p.wscale;
   return a;
 }
 
@@ -221,7 +247,7 @@ static BN fold_bn(const StateDict& sd, const std::string& p, int c) {
 
 Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int device)
     : dtype_(dtype), device_(device), n_mels_(n_mels), hidden_(hidden) {
-  M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16 || dtype == M2S_DT_BF16X3, "bad dtype");
+  M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16 || dtype == M2S_DT_BF16X3 || dtype == M2S_DT_FP8, "bad dtype");
   M2S_CHECK(n_mels > 0 && hidden > 0 && hidden % 8 == 0, "bad n_mels / rnn_hidden");
   if (const char* e = std::getenv("M2S_IR_FUSED")) ir_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_IR_WS")) ir_ws_ = std::strcmp(e, "0") != 0;
@@ -424,13 +450,15 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
         const float* b2 = need(sd, q + "se.conv_expand.bias", {m}).data;
         // SE excitation as two GEMMs over all images: (N x mid) . W1^T -> SiLU -> . W2^T -> sigmoid
         const int rd = b.rd;
-        b.se1 = make_pconv(KIND_GEMM, m, rd, 1, dtype);
+        // (fp8 engines keep the SE excitation in bf16: a gate error scales the whole block output)
+        const int se_dt = dtype == M2S_DT_FP8 ? M2S_DT_BF16 : dtype;
+        b.se1 = make_pconv(KIND_GEMM, m, rd, 1, se_dt);
         b.se1.macs_per_row = (double)m * rd;
-        pack_conv(arena_, dtype, b.se1, [&](int, int n, int, int c) { return w1[(size_t)n * m + c]; },
+        pack_conv(arena_, se_dt, b.se1, [&](int, int n, int, int c) { return w1[(size_t)n * m + c]; },
                   [&](int n) { return b1[n]; });
-        b.se2 = make_pconv(KIND_GEMM, rd, m, 1, dtype);
+        b.se2 = make_pconv(KIND_GEMM, rd, m, 1, se_dt);
         b.se2.macs_per_row = (double)m * rd;
-        pack_conv(arena_, dtype, b.se2, [&](int, int n, int, int c) { return w2[(size_t)n * rd + c]; },
+        pack_conv(arena_, se_dt, b.se2, [&](int, int n, int, int c) { return w2[(size_t)n * rd + c]; },
                   [&](int n) { return b2[n]; });
         conv1x1(b.c2, q + "conv_pwl.weight", m, b.cout, fold_bn(sd, q + "bn3", b.cout));
       }
@@ -546,7 +574,7 @@ size_t Acoustic::workspace_bytes(int B, int T, int H, int W) const {
 
 void Acoustic::effnet(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe,
                       int* probe_dims, Workspace& ws, hipStream_t s) {
-  if (dtype_ == M2S_DT_BF16)
+  if (dtype_ == M2S_DT_BF16 || dtype_ == M2S_DT_FP8)
     effnet_t<bf16_t>(frames, N, H, W, feats, stop_after, probe, probe_dims, ws, s);
   else if (dtype_ == M2S_DT_BF16X3)
     effnet_t<sp_t>(frames, N, H, W, feats, stop_after, probe, probe_dims, ws, s);
@@ -578,7 +606,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
     same_pad(W, 3, 2, &ow, &pl);
     // stem + blocks.0 (two 3x3 ConvBnAct at stride 1: 32 -> 16, 16 -> 16 + skip) in one kernel
     constexpr bool SPL = std::is_same<T, sp_t>::value;
-    const bool front = (std::is_same<T, bf16_t>::value || SPL) && stem_fused_ && !(probe && stop_after >= 0 && stop_after < 2) &&
+    const bool front = ((std::is_same<T, bf16_t>::value && dtype_ == M2S_DT_BF16) || SPL) && stem_fused_ && !(probe && stop_after >= 0 && stop_after < 2) &&
                        blocks_.size() >= 2 && blocks_[0].type == 0 && blocks_[0].stride == 1 && !blocks_[0].skip &&
                        blocks_[0].cout == 16 && blocks_[0].c1.cs_in == 32 && blocks_[0].c1.kp == 288 &&
                        blocks_[1].type == 0 && blocks_[1].stride == 1 && blocks_[1].skip && blocks_[1].cout == 16 &&
@@ -677,7 +705,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
       } else {
         const int cs = chan_stride(b.mid);
         constexpr bool SPL = std::is_same<T, sp_t>::value;
-        constexpr bool FUSABLE = std::is_same<T, bf16_t>::value || SPL;
+        const bool FUSABLE = (std::is_same<T, bf16_t>::value && dtype_ == M2S_DT_BF16) || SPL;
         // bf16 feeds the fused kernel bf16 depthwise taps (dword halves), split fp32 the fp32 taps
         const void* wdw = arena_.ptr(SPL ? b.dw_w : b.dw_w2);
         if (SPL && b.stride == 1 && ir_fused_ && ir_ws_ && ir_ws_supported(nh, nw, b.c1.cs_in, b.c1.kp, cs)) {
@@ -829,20 +857,22 @@ static std::vector<float> fold_wn(const StateDict& sd, const std::string& p, std
 
 Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int device)
     : h_(h), dtype_(dtype), device_(device) {
-  M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16 || dtype == M2S_DT_BF16X3, "bad dtype");
+  M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16 || dtype == M2S_DT_BF16X3 || dtype == M2S_DT_FP8, "bad dtype");
   M2S_CHECK(h.resblock == 1 || h.resblock == 2, "resblock must be 1 or 2");
+  // fp8 engines: e4m3 resblock (MRF) convs; conv_pre and the upsamplers stay bf16
+  const int io_dt = dtype == M2S_DT_FP8 ? M2S_DT_BF16 : dtype;
   if (const char* e = std::getenv("M2S_MRF_FUSED")) mrf_fused_ = std::strcmp(e, "0") != 0;
   M2S_CHECK(h.n_up >= 1 && h.n_up <= 8 && h.n_kernels >= 1 && h.n_kernels <= 8, "bad generator config");
   const int c0 = h.upsample_initial_channel;
   {  // conv_pre: Conv1d(num_mels, c0, 7), no weight norm (models.py:94)
     const HostTensor& w = need(sd, "conv_pre.weight", {c0, h.num_mels, 7});
     const HostTensor& b = need(sd, "conv_pre.bias", {c0});
-    pre_ = make_pconv(KIND_CONV1D, h.num_mels, c0, 7, dtype);
+    pre_ = make_pconv(KIND_CONV1D, h.num_mels, c0, 7, io_dt);
     pre_.ks = 7;
     pre_.pad_left = 0;  // F.pad(x, (0, 6)): look-ahead of 6 frames, zeros past the end
     pre_.macs_per_row = (double)c0 * h.num_mels * 7;
     const int ci = h.num_mels;
-    pack_conv(arena_, dtype, pre_, [&](int, int n, int t, int c) { return w.data[((size_t)n * ci + c) * 7 + t]; },
+    pack_conv(arena_, io_dt, pre_, [&](int, int n, int t, int c) { return w.data[((size_t)n * ci + c) * 7 + t]; },
               [&](int n) { return b.data[n]; });
   }
   hop_ = 1;
@@ -859,14 +889,14 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
     const std::string p = "ups." + std::to_string(i);
     std::vector<float> w = fold_wn(sd, p, {ci, co, k});  // ConvTranspose1d weight (in, out, k)
     const HostTensor& b = need(sd, p + ".bias", {co});
-    PConv pc = make_pconv(KIND_CONVT, ci, co, (k + u - 1) / u, dtype);
+    PConv pc = make_pconv(KIND_CONVT, ci, co, (k + u - 1) / u, io_dt);
     pc.phases = u;
     pc.ct_u = u;
     pc.ct_pad = (k - u) / 2;
     pc.ct_k = k;
     pc.macs_per_row = (double)ci * co * k / u;  // per output position, averaged over phases
     const int pad = pc.ct_pad;
-    pack_conv(arena_, dtype, pc,
+    pack_conv(arena_, io_dt, pc,
               [&](int ph, int n, int t, int c) {
                 const int j = (ph + pad) % u + t * u;  // tap t of phase ph uses kernel index j
                 return j < k ? w[((size_t)c * co + n) * k + j] : 0.f;
@@ -966,7 +996,7 @@ size_t Vocoder::workspace_bytes(int B, int T) const {
 void Vocoder::forward(const float* mel, int layout, int B, int T, float* wav, Workspace& ws, hipStream_t s) {
   M2S_CHECK(B > 0 && T > 0, "vocoder: empty input");
   const int cs = chan_stride(h_.num_mels);
-  if (dtype_ == M2S_DT_BF16) {
+  if (dtype_ == M2S_DT_BF16 || dtype_ == M2S_DT_FP8) {
     bf16_t* mn = ws.take<bf16_t>((size_t)B * T * cs);
     launch_mel_to_nlc<bf16_t>(mel, B, h_.num_mels, T, layout, mn, cs, s);
     run_t<bf16_t>(mn, B, T, wav, ws, s);
@@ -986,7 +1016,7 @@ void Vocoder::forward_from_norm(const float* mel_norm, const float* mean, const 
   M2S_CHECK(B > 0 && T > 0, "vocoder: empty input");
   const int nm = h_.num_mels, cs = chan_stride(nm);
   ws.take<char>((size_t)B * T * cs * act_bytes(dtype_));  // same carve as forward()
-  if (dtype_ == M2S_DT_BF16) {
+  if (dtype_ == M2S_DT_BF16 || dtype_ == M2S_DT_FP8) {
     ProfScope ps("mel_glue_kernel<unsigned short>", 0.0, 4.0 * B * T * nm * 4, s);
     launch_mel_glue<bf16_t>(mel_norm, B * T, nm, mean, std_, mel_db, mel_log, static_cast<bf16_t*>(ln_buf), cs, s);
   } else if (dtype_ == M2S_DT_BF16X3) {
@@ -996,7 +1026,7 @@ void Vocoder::forward_from_norm(const float* mel_norm, const float* mean, const 
     ProfScope ps("mel_glue_kernel<float>", 0.0, 4.0 * B * T * nm * 4, s);
     launch_mel_glue<float>(mel_norm, B * T, nm, mean, std_, mel_db, mel_log, static_cast<float*>(ln_buf), cs, s);
   }
-  if (dtype_ == M2S_DT_BF16)
+  if (dtype_ == M2S_DT_BF16 || dtype_ == M2S_DT_FP8)
     run_t<bf16_t>(ln_buf, B, T, wav, ws, s);
   else if (dtype_ == M2S_DT_BF16X3)
     run_t<sp_t>(ln_buf, B, T, wav, ws, s);

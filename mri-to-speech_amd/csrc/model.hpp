@@ -49,12 +49,15 @@ struct PConv {
   int dil = 1, pad_left = 0;
   int ct_u = 1, ct_pad = 0, ct_k = 1;
   double macs_per_row = 0;  // algorithmic MACs per output position (all phases)
-  size_t w_off = 0, b_off = 0;
+  size_t w_off = 0, b_off = 0, ws_off = 0;
+  bool fp8 = false;                // M2S_DT_FP8: e4m3-grid weights (bf16 storage) + per-channel scales
   const void* w = nullptr;
   const float* b = nullptr;
+  const float* wscale = nullptr;   // [n_pad] when fp8
   void resolve(const Arena& a) {
     w = a.ptr(w_off);
     b = static_cast<const float*>(a.ptr(b_off));
+    wscale = fp8 ? static_cast<const float*>(a.ptr(ws_off)) : nullptr;
   }
 };
 

@@ -95,7 +95,7 @@ def main(argv=None):
     parser.add_argument("--input_mels_dir", default="test_mel_files")
     parser.add_argument("--output_dir", default="generated_files_from_mel")
     parser.add_argument("--checkpoint_file", required=True)
-    parser.add_argument("--dtype", choices=["bf16x3", "fp32", "bf16"], default=None, help="m2s compute dtype")
+    parser.add_argument("--dtype", choices=["bf16x3", "fp32", "bf16", "fp8"], default=None, help="m2s compute dtype")
     a = parser.parse_args(argv)
     config_file = os.path.join(os.path.split(a.checkpoint_file)[0], "config.json")
     with open(config_file) as f:

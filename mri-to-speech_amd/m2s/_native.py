@@ -14,9 +14,11 @@ import numpy as np
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libm2s.so")
 
-F32, BF16, BF16X3 = 0, 1, 2
-# "bf16x3": split fp32 (hi + lo bf16 pairs, three-term MFMA products), fp32 tolerance (include/m2s.h)
-DTYPES = {"fp32": F32, "float32": F32, "f32": F32, "bf16": BF16, "bfloat16": BF16, "bf16x3": BF16X3}
+F32, BF16, BF16X3, FP8 = 0, 1, 2, 3
+# "bf16x3": split fp32 (hi + lo bf16 pairs, three-term MFMA products), fp32 tolerance;
+# "fp8": e4m3 MFMA operands with per-channel weight scales (configs[4]; include/m2s.h)
+DTYPES = {"fp32": F32, "float32": F32, "f32": F32, "bf16": BF16, "bfloat16": BF16, "bf16x3": BF16X3,
+          "fp8": FP8, "e4m3": FP8}
 ELEM_F32, ELEM_I64 = 0, 1
 
 
@@ -83,7 +85,7 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.m2s_abi_version() != 2:
+    if L.m2s_abi_version() != 3:
         raise M2SError("libm2s ABI version mismatch")
     _lib = L
     return L

@@ -169,7 +169,7 @@ def main(argv=None):
     parser.add_argument("--config", default="config_custom.json", help="HiFi-GAN config file")
     parser.add_argument("--output_dir", default="mel_synthesis_result", help="Output directory")
     parser.add_argument("--max_files", default=20, type=int, help="Maximum number of files to process (if directory)")
-    parser.add_argument("--dtype", choices=["bf16x3", "fp32", "bf16"], default=None, help="m2s compute dtype")
+    parser.add_argument("--dtype", choices=["bf16x3", "fp32", "bf16", "fp8"], default=None, help="m2s compute dtype")
     args = parser.parse_args(argv)
     with open(args.config) as f:
         h = AttrDict(json.loads(f.read()))

@@ -126,7 +126,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     parser.add_argument("--mri_code_dir", help="Directory containing mri_acoustic_model.py (if not importable by default).")
     parser.add_argument("--cpu", action="store_true", help="Rejected: m2s has no CPU execution path.")
     parser.add_argument("--overwrite", action="store_true", help="Regenerate files even if they already exist.")
-    parser.add_argument("--dtype", choices=["bf16x3", "fp32", "bf16"], default=None, help="m2s compute dtype (default fp32)")
+    parser.add_argument("--dtype", choices=["bf16x3", "fp32", "bf16", "fp8"], default=None, help="m2s compute dtype (default fp32)")
     parser.add_argument("--batch", type=int, default=16, help="clips of equal length per forward call")
     return parser.parse_args(argv)
 

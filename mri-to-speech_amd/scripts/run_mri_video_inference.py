@@ -281,7 +281,7 @@ def parse_args(argv=None):
     p.add_argument("--n-mels", type=int, default=64)
     p.add_argument("--rnn-hidden", type=int, default=640)
     p.add_argument("--dropout", type=float, default=0.5)
-    p.add_argument("--dtype", choices=["bf16x3", "fp32", "bf16"], default=None,
+    p.add_argument("--dtype", choices=["bf16x3", "fp32", "bf16", "fp8"], default=None,
                    help="m2s compute dtype (default: M2S_DTYPE or bf16x3)")
     p.add_argument("--decode-chunk", type=int, default=64, help="frames per decode / H2D chunk")
     return p.parse_args(argv)

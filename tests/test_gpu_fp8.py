@@ -1,0 +1,73 @@
+"""fp8 path (configs[4]: "fp8 MFMA CNN encoder + HiFi-GAN MRF dilated-conv path, >=1000-frame clips").
+
+M2S_DT_FP8 (include/m2s.h): the backbone convs and the MRF resblock convs run e4m3 x e4m3 MFMA
+(v_mfma_f32_16x16x32_fp8_fp8) on OCP e4m3fn weights with per-output-channel fp32 scales, activations
+rounded to e4m3 at the operand read.  Tolerance: cosine similarity >= 0.99 against
+the fp32 oracle for the mel at 1 x 1000 frames; the vocoder's wav is held to the same cosine.  The
+measured values are printed (pytest -s).  GPU box only.
+"""
+import numpy as np
+import pytest
+import torch
+
+from m2s import synth
+from m2s.config import HIFIGAN_H
+from oracle import acoustic, effnet, hifigan
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+COS_MIN = 0.99
+
+
+def _cos(a, b):
+    a, b = np.asarray(a, np.float64).ravel(), np.asarray(b, np.float64).ravel()
+    return float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b) + 1e-30))
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from m2s import runtime
+    return runtime
+
+
+@pytest.fixture(scope="module")
+def clip1000():
+    """1 x 1000 frames at 256 x 256 (configs[4] length) and the oracle's features, mel."""
+    st = synth.synth_acoustic_state(11)
+    sd = {k: torch.from_numpy(v) for k, v in st.items()}
+    fr = synth.synth_frames(1, 1000, seed=5)
+    torch.set_num_threads(16)
+    f = torch.cat([effnet.effnet_gap(sd, torch.from_numpy(fr[0, i:i + 100])) for i in range(0, 1000, 100)]).view(1, 1000, -1)
+    mn = acoustic.head(sd, acoustic.bilstm_summerge(sd, f)).numpy()
+    return st, fr, f.numpy(), mn
+
+
+def test_effnet_fp8_features_cosine(rt, clip1000):
+    st, fr, f_ref, _ = clip1000
+    eng = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    f = eng.effnet(torch.from_numpy(fr[0]).to(DEV)).cpu().numpy()
+    c = _cos(f, f_ref[0])
+    print(f"\nfp8 effnet GAP features (1000 frames): cos {c:.5f}, rel max {np.abs(f - f_ref[0]).max() / np.abs(f_ref).max():.3e}")
+    assert c >= COS_MIN
+
+
+def test_acoustic_fp8_mel_cosine_1x1000(rt, clip1000):
+    st, fr, _, mn_ref = clip1000
+    eng = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    mn = eng.forward(torch.from_numpy(fr).to(DEV)).cpu().numpy()
+    c = _cos(mn, mn_ref)
+    per_frame = min(_cos(mn[0, t], mn_ref[0, t]) for t in range(0, 1000, 37))
+    print(f"\nfp8 mel_norm 1x1000: cos {c:.5f} (worst sampled frame {per_frame:.5f}), max|d| {np.abs(mn - mn_ref).max():.3e}")
+    assert c >= COS_MIN
+
+
+def test_vocoder_fp8_wav_cosine_1x1000(rt):
+    sd = synth.synth_generator_state(5, HIFIGAN_H)
+    mel = synth.synth_mel_log(1, 64, 1000, seed=9)
+    ref = hifigan.generator({k: torch.from_numpy(v) for k, v in sd.items()}, HIFIGAN_H, torch.from_numpy(mel)).numpy()
+    voc = rt.VocoderEngine(sd, HIFIGAN_H, dtype="fp8", device=DEV)
+    wav = voc.forward(torch.from_numpy(mel).to(DEV)).cpu().numpy()
+    c = _cos(wav, ref)
+    snr = 10 * np.log10((ref ** 2).sum() / max(((wav.reshape(ref.shape) - ref) ** 2).sum(), 1e-30))
+    print(f"\nfp8 vocoder 1x1000 frames: wav cos {c:.5f}, SNR {snr:.1f} dB")
+    assert c >= COS_MIN
