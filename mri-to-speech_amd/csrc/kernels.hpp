@@ -104,6 +104,11 @@ void launch_er_sp(const void* x, int N, int H, int W, int cs_in, int mid, int cs
 // (ers2_fused.hip)
 bool ers2_fused_supported(int OH, int OW, int cs_in, int mid, int cs_out, int kp_exp, int kp_pwl);
 int ers2_exp_elems(int cs_in, int mid);
+// split fp32 blocks.1.0 (16 -> 64 -> 32): wexp [hi/lo][k-step][n16][lane][8], wpwl [hi/lo][n16][k-step][lane][8]
+bool ers2_sp_supported(int OH, int OW, int cs_in, int mid, int cs_out);
+void launch_ers2_sp(const void* x, int N, int H, int W, int OH, int OW, int pad_t, int pad_l, int cs_in, int mid,
+                    int cs_out, const void* wexp, const float* bexp, const void* wpwl, const float* bpwl, void* y,
+                    double flops, double bytes, hipStream_t s);
 void launch_ers2_fused(const bf16_t* x, int N, int H, int W, int OH, int OW, int pad_t, int pad_l, int cs_in, int mid,
                        int cs_out, const bf16_t* wexp, const float* bexp, const bf16_t* wpwl, const float* bpwl,
                        bf16_t* y, double flops, double bytes, hipStream_t s);

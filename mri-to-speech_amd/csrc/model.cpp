@@ -337,6 +337,39 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
                 }
           b.er_sp_w = arena_.add_vec(st);
           b.er_sp = true;
+        } else if (dtype == M2S_DT_BF16X3 && b.stride == 2 && k == 3 &&
+                   ers2_sp_supported(8, 16, b.c1.cs_in, b.mid, chan_stride(b.cout))) {
+          // ers2_sp_kernel (ers2_fused.hip): conv_exp [hi/lo][k-step][n16][lane][8] (lane groups 0-1:
+          // tap 2s, 2-3: tap 2s + 1), conv_pwl [hi/lo][n16][k-step][lane][8] with the permuted K
+          const int csi = b.c1.cs_in, cso = chan_stride(b.cout), ks_n = (9 * csi + 31) / 32, ntn = b.mid / 16;
+          const int onn = cso / 16, pkn = b.mid / 32;
+          const float* we = need(sd, q + "conv_exp.weight", {b.mid, cin, 3, 3}).data;
+          const float* wq = need(sd, q + "conv_pwl.weight", {b.cout, b.mid, 1, 1}).data;
+          const BN e1 = fold_bn(sd, q + "bn1", b.mid), e2 = fold_bn(sd, q + "bn2", b.cout);
+          const size_t fe_half = (size_t)ks_n * ntn * 64 * 8, fp_half = (size_t)onn * pkn * 64 * 8;
+          std::vector<uint16_t> fe(2 * fe_half, 0), fp(2 * fp_half, 0);
+          for (int s2 = 0; s2 < ks_n; ++s2)
+            for (int nt = 0; nt < ntn; ++nt)
+              for (int ln = 0; ln < 64; ++ln)
+                for (int e = 0; e < 8; ++e) {
+                  const int g8 = ln >> 4, n = nt * 16 + (ln & 15), t = 2 * s2 + (g8 >> 1), c = 8 * (g8 & 1) + e;
+                  const float v = t < 9 && c < cin ? we[((size_t)n * cin + c) * 9 + t] * e1.a[n] : 0.f;
+                  const size_t i = (((size_t)s2 * ntn + nt) * 64 + ln) * 8 + e;
+                  split_host(v, &fe[i], &fe[fe_half + i]);
+                }
+          for (int on = 0; on < onn; ++on)
+            for (int ks = 0; ks < pkn; ++ks)
+              for (int ln = 0; ln < 64; ++ln)
+                for (int e = 0; e < 8; ++e) {
+                  const int n = on * 16 + (ln & 15), g4 = 4 * (ln >> 4);
+                  const int c = 32 * ks + (e < 4 ? g4 + e : 16 + g4 + e - 4);
+                  const float v = n < b.cout ? wq[(size_t)n * b.mid + c] * e2.a[n] : 0.f;
+                  const size_t i = (((size_t)on * pkn + ks) * 64 + ln) * 8 + e;
+                  split_host(v, &fp[i], &fp[fp_half + i]);
+                }
+          b.er_wexp = arena_.add_vec(fe);
+          b.er_wpwl = arena_.add_vec(fp);
+          b.ers_sp = true;
         } else if (dtype == M2S_DT_BF16 && b.stride == 1 && b.skip && k == 3 &&
             er_fused_supported(64, 64, cin, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
           // er_fused.hip operand orders: conv_exp [tap][n16][lane][8] (lane = (k8 group, row));
@@ -670,6 +703,12 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         const double px = (double)nc * nh * nw;
         launch_er_sp(cur, nc, nh, nw, b.c1.cs_in, b.mid, chan_stride(b.cout), arena_.ptr(b.er_sp_w), b.c1.b, b.c2.b, nxt,
                      2.0 * px * b.mid * (9.0 * b.cin + b.cout), 4.0 * px * (b.c1.cs_in + chan_stride(b.cout)), s);
+      } else if (b.type == 1 && std::is_same<T, sp_t>::value && er_fused_ && b.ers_sp && b.stride == 2 &&
+                 ers2_sp_supported(nh, nw, b.c1.cs_in, b.mid, chan_stride(b.cout))) {
+        const double px = (double)nc * nh * nw;
+        launch_ers2_sp(cur, nc, oh, ow, nh, nw, qt, ql, b.c1.cs_in, b.mid, chan_stride(b.cout), arena_.ptr(b.er_wexp),
+                       b.c1.b, arena_.ptr(b.er_wpwl), b.c2.b, nxt, 2.0 * px * b.mid * (9.0 * b.cin + b.cout),
+                       4.0 * ((double)nc * oh * ow * b.c1.cs_in + px * chan_stride(b.cout)), s);
       } else if (b.type == 1 && std::is_same<T, bf16_t>::value && er_fused_ && b.er_frag &&
                  er_fused_supported(nh, nw, b.cin, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
         const double px = (double)nc * nh * nw;

@@ -118,6 +118,7 @@ class Acoustic {
     bool er_frag = false;
     size_t er_sp_w = 0;  // split fp32 er stride 1: er_sp_fused.hip stage stream
     bool er_sp = false;
+    bool ers_sp = false;  // split fp32 er stride 2 (blocks.1.0): er_wexp / er_wpwl in [hi/lo] fragment order
   };
   template <typename T>
   void effnet_t(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe, int* probe_dims,
