@@ -554,7 +554,7 @@ template <int BM, int BN, int MT, int NT, int KIND, int XF, int SP>
 void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
   // keep two workgroups' LDS per CU (128 x 256: the SE gate table too, and 256 registers a wave);
   // split operands double the slot, so they run two stages
-  constexpr int S = SP == 1 ? 2 : (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
+  constexpr int S = SP == 1 ? (BM == 128 && BN == 64 && XF != IN_SE_SCALE ? 3 : 2) : (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
   constexpr int R = SP == 1 ? 2 : 1;
   static bool attr = [] {
     M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF, SP>),
@@ -587,10 +587,14 @@ void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, 
   if constexpr (SP != 0) {  // split / e4m3 operands: 16/32/64-wide tiles for narrow outputs, else 128 x 128
     if (n <= 16)
       return launch_tile<256, 16, 4, 1, KIND, XF, SP>(a, s, phases, flops, bytes);
-    if (n <= 32)
+    if (n <= 32)  // (a 128 x 32 tile at three stages: 0.1 ms per step slower on the C = 32 MRF convs)
       return launch_tile<256, 32, 4, 2, KIND, XF, SP>(a, s, phases, flops, bytes);
-    if (n <= 64 || (n % 128 != 0 && ceil_div(n, 64) * 64 < ceil_div(n, 128) * 128))
+    if (n <= 64 || (n % 128 != 0 && ceil_div(n, 64) * 64 < ceil_div(n, 128) * 128)) {
+      // split 64-wide outputs: 128 x 64 at three stages (77 KB, two workgroups per CU) instead of
+      // 256 x 64 at two (84 KB, one per CU): the C = 64 MRF convs 3.7 -> 3.1 ms per step
+      if (SP == 1 && n <= 64) return launch_tile<128, 64, 4, 2, KIND, XF, SP>(a, s, phases, flops, bytes);
       return launch_tile<256, 64, 4, 4, KIND, XF, SP>(a, s, phases, flops, bytes);
+    }
     return launch_tile<128, 128, 4, 4, KIND, XF, SP>(a, s, phases, flops, bytes);
   } else {
   if constexpr (KIND == KIND_GEMM || KIND == KIND_CONV2D) if (a.M >= 256 * 256 && n > 128 &&
