@@ -49,16 +49,16 @@ void launch_ir_pwdw_s2(const void* x, int N, int cs_in, int kp, const void* wpw,
                        const float* bdw, int IH, int IW, int OH, int OW, int pad_t, int pad_l, int cs_mid, void* y,
                        void* se_mean, bool split, double flops, double bytes, hipStream_t s);
 
-// bf16 fused HiFi-GAN ResBlock1 (all (c1, c2) pairs of one resblock + the MRF running sum) for C in
-// {32, 64}: x (B, L, C) -> S (B, L, C) with S = x' (accum 0), S += x' (1), S = (S + x') / div (2).
-// (mrf_fused.hip)
-// w1/w2 are in fragment order: [rb1_frag_taps(C, k)][C/16][C/32][64 lanes][8] bf16, element
-// (tap t, n16, k32, lane, e) = W[n16*16 + lane%16][k32*32 + 8*(lane/16) + e][t] (zero taps past k).
-bool rb1_fused_supported(int C, int cs, int k, const int* dil, int np, int kp);
-int rb1_frag_taps(int C, int k);
+// Fused HiFi-GAN ResBlock1 (all (c1, c2) pairs of one resblock + the MRF running sum), bf16 for C in
+// {32, 64} or split fp32 (split: x, S as [hi C | lo C] per position) for C = 32:
+// x (B, L, C) -> S (B, L, C) with S = x' (accum 0), S += x' (1), S = (S + x') / div (2).  (mrf_fused.hip)
+// w1/w2 are in fragment order: [rb1_frag_taps(C, k, split)][hi/lo if split][C/16][C/32][64 lanes][8] bf16,
+// element (tap t, n16, k32, lane, e) = W[n16*16 + lane%16][k32*32 + 8*(lane/16) + e][t] (zero taps past k).
+bool rb1_fused_supported(int C, int cs, int k, const int* dil, int np, int kp, bool split);
+int rb1_frag_taps(int C, int k, bool split);
 void launch_rb1_fused(const bf16_t* x, bf16_t* s, int B, int L, int C, int k, int np, const int* dil,
                       const bf16_t* const* w1, const float* const* b1, const bf16_t* const* w2,
-                      const float* const* b2, int kp, int accum, float div, double flops, double bytes,
+                      const float* const* b2, int kp, int accum, float div, bool split, double flops, double bytes,
                       hipStream_t st);
 
 // conv_stem + bn1 + SiLU + blocks.0.0 (3x3 32->16 + SiLU) + blocks.0.1 (3x3 16->16 + SiLU + skip) in

@@ -961,21 +961,30 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
                   [&](int n) { return bv.data[n]; });
         return c;
       };
-      const bool frag = dtype == M2S_DT_BF16 && h.resblock == 1 &&
-                        rb1_fused_supported(co, chan_stride(co), kk, rb.dil.data(), (int)rb.dil.size(), kk * co);
+      const bool fsplit = dtype == M2S_DT_BF16X3;
+      const bool frag = (dtype == M2S_DT_BF16 || fsplit) && h.resblock == 1 &&
+                        rb1_fused_supported(co, chan_stride(co), kk, rb.dil.data(), (int)rb.dil.size(), kk * co, fsplit);
       auto mk_frag = [&](const std::string& name) {  // fragment order of mrf_fused.hip
         std::vector<float> wv = fold_wn(sd, name, {co, co, kk});
-        const int taps = rb1_frag_taps(co, kk), nt16 = co / 16, k32 = co / 32;
-        std::vector<uint16_t> f((size_t)taps * nt16 * k32 * 64 * 8);
+        const int taps = rb1_frag_taps(co, kk, fsplit), nt16 = co / 16, k32 = co / 32, hr = fsplit ? 2 : 1;
+        std::vector<uint16_t> f((size_t)taps * hr * nt16 * k32 * 64 * 8);
         size_t o = 0;
         for (int t = 0; t < taps; ++t)
-          for (int nt = 0; nt < nt16; ++nt)
-            for (int kc = 0; kc < k32; ++kc)
-              for (int ln = 0; ln < 64; ++ln)
-                for (int e = 0; e < 8; ++e) {
-                  const int n = nt * 16 + (ln & 15), c = kc * 32 + 8 * (ln >> 4) + e;
-                  f[o++] = t < kk ? f2bf_host(wv[((size_t)n * co + c) * kk + t]) : 0;
-                }
+          for (int half = 0; half < hr; ++half)
+            for (int nt = 0; nt < nt16; ++nt)
+              for (int kc = 0; kc < k32; ++kc)
+                for (int ln = 0; ln < 64; ++ln)
+                  for (int e = 0; e < 8; ++e) {
+                    const int n = nt * 16 + (ln & 15), c = kc * 32 + 8 * (ln >> 4) + e;
+                    const float w = t < kk ? wv[((size_t)n * co + c) * kk + t] : 0.f;
+                    if (fsplit) {
+                      uint16_t hi, lo;
+                      split_host(w, &hi, &lo);
+                      f[o++] = half ? lo : hi;
+                    } else {
+                      f[o++] = f2bf_host(w);
+                    }
+                  }
         return arena_.add_vec(f);
       };
       for (size_t d = 0; d < rb.dil.size(); ++d) {
@@ -1108,7 +1117,8 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
       const T* hcur = X;
       const int np = (int)rb.dil.size();
       const int accum = j == 0 ? 0 : (j == nk - 1 ? 2 : 1);
-      if (std::is_same<T, bf16_t>::value && mrf_fused_ && !rb.f1.empty()) {
+      constexpr bool SPL = std::is_same<T, sp_t>::value;
+      if ((std::is_same<T, bf16_t>::value || SPL) && mrf_fused_ && !rb.f1.empty()) {
         // one launch for the whole resblock + MRF sum (mrf_fused.hip)
         const bf16_t* w1[8];
         const bf16_t* w2[8];
@@ -1124,9 +1134,10 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
         }
         const int C = rb.c1[0].cout;
         const double rows = (double)B * L;
-        const double bytes = 2.0 * rows * C * (2 + (accum ? 1 : 0)) + 2.0 * np * 2 * C * C * rb.k;
+        const double bytes = (SPL ? 2.0 : 1.0) * (2.0 * rows * C * (2 + (accum ? 1 : 0)) + 2.0 * np * 2 * C * C * rb.k);
         launch_rb1_fused(reinterpret_cast<const bf16_t*>(X), reinterpret_cast<bf16_t*>(S), B, L, C, rb.k, np,
-                         rb.dil.data(), w1, b1, w2, b2, rb.c1[0].kp, accum, (float)nk, 2.0 * macs * rows, bytes, s);
+                         rb.dil.data(), w1, b1, w2, b2, rb.c1[0].kp, accum, (float)nk, SPL, 2.0 * macs * rows, bytes,
+                         s);
         continue;
       }
       for (int p = 0; p < np; ++p) {

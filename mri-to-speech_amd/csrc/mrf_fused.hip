@@ -26,6 +26,11 @@
 // ds_read_b128.  The ring runs across conv boundaries: the next conv's first weights land while
 // the current one finishes.  8 waves; subtile (16 rows) s belongs to wave s % 8 in every conv, so
 // a lane's residual rows are the rows it writes.
+//
+// Split fp32 (SP = 1, m2s_common.hpp sp_t; C = 32): x, S and the LDS images carry hi and lo halves
+// (NPL hi planes then NPL lo planes), the weights hi and lo fragments per tap ([tap][hi/lo][n16][k32]
+// [lane][8], two taps per 8 KB stage), every product is the three MFMA terms, activations are formed in
+// fp32 from hi + lo and re-split when stored; x is recovered from A = lrelu(x) in fp32 (10 a for a < 0).
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -64,9 +69,9 @@ constexpr int RB_NW = 8;          // waves per workgroup
 constexpr int RB_STAGE = 8192;    // bytes per weight stage = one 1 KB piece per wave
 constexpr int RB_SLOTS = 3;       // weight ring depth
 
-template <int C>
+template <int C, int SP = 0>
 constexpr int rb_tg() {  // taps per weight stage
-  return RB_STAGE / (C * C * 2);
+  return RB_STAGE / (C * C * 2 * (SP ? 2 : 1));
 }
 
 __device__ __forceinline__ void dma16(const void* src, void* lds_wave_base) {
@@ -90,11 +95,11 @@ struct Ring {
   }
 };
 
-template <int C, int K, int TOUT, int PASS>
+template <int C, int K, int TOUT, int PASS, int SP>
 __device__ __forceinline__ void conv_pass(const RbArgs& a, const Ring& ring, int conv, const char* in, char* io,
                                           const float* bias_lds, int d, int lo_out, int R, int PLANE, int wave,
                                           int g, int r16, int lane, int clip, int t0) {
-  constexpr int NT = C / 16, KC = C / 32, TG = rb_tg<C>();
+  constexpr int NT = C / 16, KC = C / 32, TG = rb_tg<C, SP>(), HR = SP ? 2 : 1, NPL = C / 8;
   constexpr int NS = (K + TG - 1) / TG;
   constexpr int MS = (RB_HMAX + TOUT + 16 * RB_NW - 1) / (16 * RB_NW);  // subtiles per wave at most
   const int s_lo = lo_out >> 4, s_hi = R >> 4;
@@ -120,12 +125,14 @@ __device__ __forceinline__ void conv_pass(const RbArgs& a, const Ring& ring, int
     for (int tl = 0; tl < TG; ++tl) {
       const int j = ls * TG + tl;  // tap
       if (j >= K) break;
-      bf16x8 wf[NT][KC];
+      bf16x8 wf[NT][KC], wl[SP ? NT : 1][SP ? KC : 1];
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-        for (int kc = 0; kc < KC; ++kc)
-          wf[nt][kc] = *reinterpret_cast<const bf16x8*>(ws + ((tl * NT + nt) * KC + kc) * 1024);
+        for (int kc = 0; kc < KC; ++kc) {
+          wf[nt][kc] = *reinterpret_cast<const bf16x8*>(ws + (((tl * HR) * NT + nt) * KC + kc) * 1024);
+          if constexpr (SP) wl[nt][kc] = *reinterpret_cast<const bf16x8*>(ws + (((tl * HR + 1) * NT + nt) * KC + kc) * 1024);
+        }
       const int shift = (K - 1 - j) * d;
 #pragma unroll
       for (int i = 0; i < MS; ++i) {
@@ -135,6 +142,14 @@ __device__ __forceinline__ void conv_pass(const RbArgs& a, const Ring& ring, int
 #pragma unroll
           for (int kc = 0; kc < KC; ++kc) {
             const bf16x8 b = *reinterpret_cast<const bf16x8*>(in + (kc * 4 + g) * PLANE + row * 16);
+            if constexpr (SP) {
+              const bf16x8 bl = *reinterpret_cast<const bf16x8*>(in + (NPL + kc * 4 + g) * PLANE + row * 16);
+#pragma unroll
+              for (int nt = 0; nt < NT; ++nt) {
+                acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[nt][kc], b, acc[i][nt], 0, 0, 0);
+                acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nt][kc], bl, acc[i][nt], 0, 0, 0);
+              }
+            }
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
               acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nt][kc], b, acc[i][nt], 0, 0, 0);
@@ -158,67 +173,114 @@ __device__ __forceinline__ void conv_pass(const RbArgs& a, const Ring& ring, int
       float v[4] = {acc[i][nt][0] + bb.x, acc[i][nt][1] + bb.y, acc[i][nt][2] + bb.z, acc[i][nt][3] + bb.w};
       if constexpr (PASS != PASS_C1) {  // residual: x recovered from A = lrelu(x) at this row
         const uint2 u = *reinterpret_cast<const uint2*>(p);
-        v[0] += unlrelu01(lo16(u.x));
-        v[1] += unlrelu01(hi16(u.x));
-        v[2] += unlrelu01(lo16(u.y));
-        v[3] += unlrelu01(hi16(u.y));
+        float x[4] = {lo16(u.x), hi16(u.x), lo16(u.y), hi16(u.y)};
+        if constexpr (SP) {
+          const uint2 ul = *reinterpret_cast<const uint2*>(p + NPL * PLANE);
+          x[0] += lo16(ul.x);
+          x[1] += hi16(ul.x);
+          x[2] += lo16(ul.y);
+          x[3] += hi16(ul.y);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] += unlrelu01(x[q]);
       }
       if constexpr (PASS != PASS_LAST) {
-        uint2 o = make_uint2(0u, 0u);
+        float o[4] = {0.f, 0.f, 0.f, 0.f};
         if (t >= 0) {
-          o.x = pack_bf16x2(lrelu01(v[0]), lrelu01(v[1]));
-          o.y = pack_bf16x2(lrelu01(v[2]), lrelu01(v[3]));
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = lrelu01(v[q]);
         }
-        *reinterpret_cast<uint2*>(p) = o;
+        if constexpr (SP) {
+          uint2 oh, ol;
+          split4(o, oh, ol);
+          *reinterpret_cast<uint2*>(p) = oh;
+          *reinterpret_cast<uint2*>(p + NPL * PLANE) = ol;
+        } else {
+          *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+        }
       } else if (r >= a.H && t < a.L) {
-        bf16_t* sp = a.s + ((size_t)clip * a.L + t) * C + n;
+        bf16_t* sp = a.s + ((size_t)clip * a.L + t) * C * HR + n;
         if (a.accum) {
           const uint2 u = *reinterpret_cast<const uint2*>(sp);
           v[0] += lo16(u.x);
           v[1] += hi16(u.x);
           v[2] += lo16(u.y);
           v[3] += hi16(u.y);
+          if constexpr (SP) {
+            const uint2 ul = *reinterpret_cast<const uint2*>(sp + C);
+            v[0] += lo16(ul.x);
+            v[1] += hi16(ul.x);
+            v[2] += lo16(ul.y);
+            v[3] += hi16(ul.y);
+          }
           if (a.accum == 2) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = v[q] / a.div;
           }
         }
-        *reinterpret_cast<uint2*>(sp) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        if constexpr (SP) {
+          uint2 oh, ol;
+          split4(v, oh, ol);
+          *reinterpret_cast<uint2*>(sp) = oh;
+          *reinterpret_cast<uint2*>(sp + C) = ol;
+        } else {
+          *reinterpret_cast<uint2*>(sp) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        }
       }
     }
   }
 }
 
-template <int C, int K, int TOUT>
+template <int C, int K, int TOUT, int SP>
 __global__ void __launch_bounds__(RB_NW * 64) rb1_fused_kernel(const RbArgs a) {
-  constexpr int NPL = C / 8;  // 16-byte planes
-  constexpr int TG = rb_tg<C>(), NS = (K + TG - 1) / TG;
+  constexpr int NPL = C / 8;  // 16-byte planes (per half when split)
+  constexpr int HR = SP ? 2 : 1;
+  constexpr int TG = rb_tg<C, SP>(), NS = (K + TG - 1) / TG;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int R = a.H + TOUT, ROWS = R + 16, PLANE = ROWS * 16;
   char* wring = smem;
   float* bias_lds = reinterpret_cast<float*>(smem + RB_SLOTS * RB_STAGE);  // [2 np][C]
   char* bufA = smem + RB_SLOTS * RB_STAGE + 2 * RB_MAXP * C * 4;
-  char* bufT = bufA + NPL * PLANE;
+  char* bufT = bufA + HR * NPL * PLANE;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const int clip = blockIdx.x / a.tiles, tile = blockIdx.x - clip * a.tiles;
   const int t0 = tile * TOUT - a.H;  // time of row 0
-  const bf16_t* xc = a.x + (size_t)clip * a.L * C;
+  const bf16_t* xc = a.x + (size_t)clip * a.L * C * HR;
 
   // ---- A = lrelu(x) for rows [-16, R) (guard rows and t outside the clip: zeros); T = 0; biases -
   for (int i = tid; i < ROWS * NPL; i += RB_NW * 64) {
     const int pr = i / NPL, c = i - pr * NPL, t = t0 + pr - 16;
-    uint4 u = make_uint4(0u, 0u, 0u, 0u);
-    if (pr >= 16 && t >= 0 && t < a.L) {
-      u = *reinterpret_cast<const uint4*>(xc + (size_t)t * C + c * 8);
-      u.x = lrelu_pk(u.x);
-      u.y = lrelu_pk(u.y);
-      u.z = lrelu_pk(u.z);
-      u.w = lrelu_pk(u.w);
+    if constexpr (SP) {
+      uint2 h0 = make_uint2(0u, 0u), l0 = h0, h1 = h0, l1 = h0;
+      if (pr >= 16 && t >= 0 && t < a.L) {
+        const uint4 uh = *reinterpret_cast<const uint4*>(xc + (size_t)t * 2 * C + c * 8);
+        const uint4 ul = *reinterpret_cast<const uint4*>(xc + (size_t)t * 2 * C + C + c * 8);
+        float v[8] = {lo16(uh.x) + lo16(ul.x), hi16(uh.x) + hi16(ul.x), lo16(uh.y) + lo16(ul.y),
+                      hi16(uh.y) + hi16(ul.y), lo16(uh.z) + lo16(ul.z), hi16(uh.z) + hi16(ul.z),
+                      lo16(uh.w) + lo16(ul.w), hi16(uh.w) + hi16(ul.w)};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = lrelu01(v[q]);
+        split4(v, h0, l0);
+        split4(v + 4, h1, l1);
+      }
+      *reinterpret_cast<uint4*>(bufA + c * PLANE + pr * 16) = make_uint4(h0.x, h0.y, h1.x, h1.y);
+      *reinterpret_cast<uint4*>(bufA + (NPL + c) * PLANE + pr * 16) = make_uint4(l0.x, l0.y, l1.x, l1.y);
+      *reinterpret_cast<uint4*>(bufT + c * PLANE + pr * 16) = make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4*>(bufT + (NPL + c) * PLANE + pr * 16) = make_uint4(0u, 0u, 0u, 0u);
+    } else {
+      uint4 u = make_uint4(0u, 0u, 0u, 0u);
+      if (pr >= 16 && t >= 0 && t < a.L) {
+        u = *reinterpret_cast<const uint4*>(xc + (size_t)t * C + c * 8);
+        u.x = lrelu_pk(u.x);
+        u.y = lrelu_pk(u.y);
+        u.z = lrelu_pk(u.z);
+        u.w = lrelu_pk(u.w);
+      }
+      *reinterpret_cast<uint4*>(bufA + c * PLANE + pr * 16) = u;
+      *reinterpret_cast<uint4*>(bufT + c * PLANE + pr * 16) = make_uint4(0u, 0u, 0u, 0u);
     }
-    *reinterpret_cast<uint4*>(bufA + c * PLANE + pr * 16) = u;
-    *reinterpret_cast<uint4*>(bufT + c * PLANE + pr * 16) = make_uint4(0u, 0u, 0u, 0u);
   }
   for (int i = tid; i < 2 * a.np * C; i += RB_NW * 64) {
     const int c = i / C, n = i - c * C;
@@ -239,39 +301,42 @@ __global__ void __launch_bounds__(RB_NW * 64) rb1_fused_kernel(const RbArgs a) {
     const int lo_t = lo_x + (K - 1) * d;   // ... of c1's output
     const int lo_y = lo_t + (K - 1);       // ... of c2's output (the next x)
     tot -= d + 1;
-    conv_pass<C, K, TOUT, PASS_C1>(a, ring, 2 * p, bufA, bufT, bias_lds + 2 * p * C, d, lo_t, R, PLANE, wave, g, r16,
+    conv_pass<C, K, TOUT, PASS_C1, SP>(a, ring, 2 * p, bufA, bufT, bias_lds + 2 * p * C, d, lo_t, R, PLANE, wave, g, r16,
                                    lane, clip, t0);
     __syncthreads();
     if (p + 1 < a.np) {
-      conv_pass<C, K, TOUT, PASS_C2>(a, ring, 2 * p + 1, bufT, bufA, bias_lds + (2 * p + 1) * C, 1, lo_y, R, PLANE,
+      conv_pass<C, K, TOUT, PASS_C2, SP>(a, ring, 2 * p + 1, bufT, bufA, bias_lds + (2 * p + 1) * C, 1, lo_y, R, PLANE,
                                      wave, g, r16, lane, clip, t0);
       __syncthreads();
     } else {
-      conv_pass<C, K, TOUT, PASS_LAST>(a, ring, 2 * p + 1, bufT, bufA, bias_lds + (2 * p + 1) * C, 1, lo_y, R, PLANE,
+      conv_pass<C, K, TOUT, PASS_LAST, SP>(a, ring, 2 * p + 1, bufT, bufA, bias_lds + (2 * p + 1) * C, 1, lo_y, R, PLANE,
                                        wave, g, r16, lane, clip, t0);
     }
   }
 }
 
-template <int C, int K, int TOUT>
+template <int C, int K, int TOUT, int SP>
 void launch_cfg(const RbArgs& a, int B, hipStream_t s, double flops, double bytes) {
-  constexpr int NPL = C / 8;
-  const size_t lds = RB_SLOTS * RB_STAGE + 2 * RB_MAXP * C * 4 + 2 * (size_t)NPL * (a.H + TOUT + 16) * 16;
+  constexpr int NPL = C / 8, HR = SP ? 2 : 1;
+  const size_t lds = RB_SLOTS * RB_STAGE + 2 * RB_MAXP * C * 4 + 2 * (size_t)HR * NPL * (a.H + TOUT + 16) * 16;
   M2S_CHECK(lds <= 160 * 1024, "rb1_fused: LDS budget");
   static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&rb1_fused_kernel<C, K, TOUT>),
+    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&rb1_fused_kernel<C, K, TOUT, SP>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     return true;
   }();
   (void)attr;
   char name[64];
-  snprintf(name, sizeof(name), "rb1_fused_kernel<%d, %d, %d>", C, K, TOUT);
+  snprintf(name, sizeof(name), "rb1_fused_kernel<%d, %d, %d, %d>", C, K, TOUT, SP);
   ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((rb1_fused_kernel<C, K, TOUT>), dim3(B * a.tiles), dim3(RB_NW * 64), lds, s, a);
+  hipLaunchKernelGGL((rb1_fused_kernel<C, K, TOUT, SP>), dim3(B * a.tiles), dim3(RB_NW * 64), lds, s, a);
   M2S_HIP(hipGetLastError());
 }
 
-int rb_tg_host(int C) { return C == 32 ? rb_tg<32>() : rb_tg<64>(); }
+int rb_tg_host(int C, bool split) {
+  if (split) return rb_tg<32, 1>();
+  return C == 32 ? rb_tg<32>() : rb_tg<64>();
+}
 
 int rb_history(int k, const int* dil, int np) {
   int h = 0;
@@ -286,10 +351,11 @@ constexpr int rb_tout() {
 
 }  // namespace
 
-int rb1_frag_taps(int C, int k) { return round_up(k, rb_tg_host(C)); }
+int rb1_frag_taps(int C, int k, bool split) { return round_up(k, rb_tg_host(C, split)); }
 
-bool rb1_fused_supported(int C, int cs, int k, const int* dil, int np, int kp) {
+bool rb1_fused_supported(int C, int cs, int k, const int* dil, int np, int kp, bool split) {
   if (!(C == 32 || C == 64) || cs != C || np < 1 || np > RB_MAXP || kp != k * C) return false;
+  if (split && C != 32) return false;  // C = 64 split images + ring exceed the LDS budget at TOUT = 256
   if (!(k == 3 || k == 5 || k == 7 || k == 11)) return false;
   for (int p = 0; p < np; ++p)
     if (dil[p] < 1) return false;
@@ -298,9 +364,9 @@ bool rb1_fused_supported(int C, int cs, int k, const int* dil, int np, int kp) {
 
 void launch_rb1_fused(const bf16_t* x, bf16_t* s, int B, int L, int C, int k, int np, const int* dil,
                       const bf16_t* const* w1, const float* const* b1, const bf16_t* const* w2,
-                      const float* const* b2, int kp, int accum, float div, double flops, double bytes,
+                      const float* const* b2, int kp, int accum, float div, bool split, double flops, double bytes,
                       hipStream_t st) {
-  M2S_CHECK(rb1_fused_supported(C, C, k, dil, np, kp), "rb1_fused: unsupported resblock");
+  M2S_CHECK(rb1_fused_supported(C, C, k, dil, np, kp, split), "rb1_fused: unsupported resblock");
   M2S_CHECK(B > 0 && L > 0 && (double)B * L * C < 2147483647.0, "rb1_fused: shape");
   RbArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -319,21 +385,29 @@ void launch_rb1_fused(const bf16_t* x, bf16_t* s, int B, int L, int C, int k, in
   a.H = rb_history(k, dil, np);
   a.accum = accum;
   a.div = div;
-  if (C == 32) {
+  if (split) {
     a.tiles = ceil_div(L, rb_tout<32>());
     switch (k) {
-      case 3: launch_cfg<32, 3, rb_tout<32>()>(a, B, st, flops, bytes); break;
-      case 5: launch_cfg<32, 5, rb_tout<32>()>(a, B, st, flops, bytes); break;
-      case 7: launch_cfg<32, 7, rb_tout<32>()>(a, B, st, flops, bytes); break;
-      default: launch_cfg<32, 11, rb_tout<32>()>(a, B, st, flops, bytes); break;
+      case 3: launch_cfg<32, 3, rb_tout<32>(), 1>(a, B, st, flops, bytes); break;
+      case 5: launch_cfg<32, 5, rb_tout<32>(), 1>(a, B, st, flops, bytes); break;
+      case 7: launch_cfg<32, 7, rb_tout<32>(), 1>(a, B, st, flops, bytes); break;
+      default: launch_cfg<32, 11, rb_tout<32>(), 1>(a, B, st, flops, bytes); break;
+    }
+  } else if (C == 32) {
+    a.tiles = ceil_div(L, rb_tout<32>());
+    switch (k) {
+      case 3: launch_cfg<32, 3, rb_tout<32>(), 0>(a, B, st, flops, bytes); break;
+      case 5: launch_cfg<32, 5, rb_tout<32>(), 0>(a, B, st, flops, bytes); break;
+      case 7: launch_cfg<32, 7, rb_tout<32>(), 0>(a, B, st, flops, bytes); break;
+      default: launch_cfg<32, 11, rb_tout<32>(), 0>(a, B, st, flops, bytes); break;
     }
   } else {
     a.tiles = ceil_div(L, rb_tout<64>());
     switch (k) {
-      case 3: launch_cfg<64, 3, rb_tout<64>()>(a, B, st, flops, bytes); break;
-      case 5: launch_cfg<64, 5, rb_tout<64>()>(a, B, st, flops, bytes); break;
-      case 7: launch_cfg<64, 7, rb_tout<64>()>(a, B, st, flops, bytes); break;
-      default: launch_cfg<64, 11, rb_tout<64>()>(a, B, st, flops, bytes); break;
+      case 3: launch_cfg<64, 3, rb_tout<64>(), 0>(a, B, st, flops, bytes); break;
+      case 5: launch_cfg<64, 5, rb_tout<64>(), 0>(a, B, st, flops, bytes); break;
+      case 7: launch_cfg<64, 7, rb_tout<64>(), 0>(a, B, st, flops, bytes); break;
+      default: launch_cfg<64, 11, rb_tout<64>(), 0>(a, B, st, flops, bytes); break;
     }
   }
 }

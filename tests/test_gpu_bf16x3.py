@@ -61,7 +61,24 @@ def test_vocoder_bf16x3_vs_oracle_shapes(rt, B, T):
     np.testing.assert_allclose(wav, ref, atol=1e-4, rtol=0)
 
 
-@pytest.mark.parametrize("hw", [(256, 256), (96, 80), (67, 101)])
+@pytest.mark.parametrize("B,T", [(1, 1), (3, 17), (2, 64)])
+def test_vocoder_bf16x3_mrf_fused(rt, monkeypatch, B, T):
+    """Split fused ResBlock1 (mrf_fused.hip SP = 1, the C = 32 stage) against the oracle at the fp32
+    bar and against the per-conv split path: a clip shorter than one tile, ragged last tiles, several
+    clips.  Both are split fp32; they differ only by where the hi/lo re-splits round (~1e-6)."""
+    sd = synth.synth_generator_state(7, HIFIGAN_H)
+    mel = synth.synth_mel_log(B, 64, T, seed=B * 10 + T)
+    ref = hifigan.generator({k: torch.from_numpy(v) for k, v in sd.items()}, HIFIGAN_H, torch.from_numpy(mel)).numpy()
+    monkeypatch.setenv("M2S_MRF_FUSED", "1")
+    fused = rt.VocoderEngine(sd, HIFIGAN_H, dtype="bf16x3", device=DEV).forward(torch.from_numpy(mel).to(DEV))
+    monkeypatch.setenv("M2S_MRF_FUSED", "0")
+    plain = rt.VocoderEngine(sd, HIFIGAN_H, dtype="bf16x3", device=DEV).forward(torch.from_numpy(mel).to(DEV))
+    fused, plain = fused.cpu().numpy(), plain.cpu().numpy()
+    np.testing.assert_allclose(fused, ref, atol=1e-4, rtol=0)
+    np.testing.assert_allclose(fused, plain, atol=2e-5, rtol=0)
+
+
+@pytest.mark.parametrize("hw",[(256, 256), (96, 80), (67, 101)])
 def test_effnet_bf16x3_every_block(rt, ac_state, hw):
     sd = {k: torch.from_numpy(v) for k, v in ac_state.items()}
     fr = torch.from_numpy(synth.synth_frames(1, 3, hw=hw, seed=4)[0])
