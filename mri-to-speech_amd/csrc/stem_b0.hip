@@ -18,6 +18,13 @@
 // Split fp32 (SP = 1, m2s_common.hpp sp_t): S and A keep a hi and a lo plane set (double the LDS,
 // two workgroups per CU), the conv weights come as [hi kp | lo kp] rows (A fragments hi and lo
 // resident), every product is the three MFMA terms and y is written as (N, OH, OW, [hi 16 | lo 16]).
+//
+// Persistent: a workgroup per CU slot walks a sequence of tiles with its weights resident (loaded
+// once), and the frame pixels of its next tile's phase 1 are loaded into registers right after the
+// current tile's phase 1 (they land while phases 2 and 3 run).  Launched one workgroup per tile, a
+// tile's life was a chain of exposed latencies (weights from L2, frame from HBM, two barriers): 16 us
+// per workgroup at two per CU.  Tiles are dealt per XCD in contiguous ranges, so the workgroups of
+// one XCD work on neighbouring tiles of the same frames at any time (shared halos stay in its L2).
 #include <algorithm>
 #include <cstdio>
 
@@ -29,7 +36,12 @@ namespace {
 
 constexpr int SB_TW = 16;           // output tile width (one MFMA position subtile per tile row)
 constexpr int SB_SW = SB_TW + 4;    // S row width
-constexpr int SB_AW = SB_TW + 2;    // A row width
+constexpr int SB_AV = SB_TW + 2;    // A row width (valid pixels)
+// A rows are stored at the S pitch: a phase-2 subtile of 16 consecutive A positions then reads 16
+// consecutive S pixels for every tap (conflict-free planes).  At the 18-pixel pitch a subtile crossed
+// an A row break and its S pixels jumped by 2 there: 2-way bank conflicts on most phase-2 reads
+// (SQ_LDS_BANK_CONFLICT 1.4x the LDS-active cycles).  Columns 18-19 of A are computed and ignored.
+constexpr int SB_AW = SB_SW;
 
 struct StemB0Args {
   const float* frames;  // (N, H, W) fp32
@@ -41,6 +53,7 @@ struct StemB0Args {
   const float* b1;
   bf16_t* y;            // (N, OH, OW, 16) (SP: (N, OH, OW, [hi 16 | lo 16]))
   int N, H, W, OH, OW, pad_t, pad_l, kp0, kp1, tiles_x, tiles_y;
+  int per_xcd;  // tiles per XCD range (gridDim.x is a multiple of 8)
 };
 
 __device__ __forceinline__ bf16x8 frag(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
@@ -51,7 +64,7 @@ __device__ __forceinline__ f32x4 mma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl
 }
 
 template <int TH, int SP>
-__global__ void __launch_bounds__(256, SP ? 2 : 4) stem_b0_kernel(const StemB0Args a) {
+__global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Args a) {
   constexpr int SH = TH + 4, AH = TH + 2;
   constexpr int SPIX = SH * SB_SW, APIX = AH * SB_AW;
   constexpr int APIX_PAD = (APIX + 15) / 16 * 16;
@@ -61,197 +74,227 @@ __global__ void __launch_bounds__(256, SP ? 2 : 4) stem_b0_kernel(const StemB0Ar
   constexpr int AMS = (ASUB + 3) / 4;                         // ... per wave, at most
   constexpr int OMS = TH / 4;                                 // output subtiles (rows) per wave
   constexpr int R = SP ? 2 : 1;  // plane sets: hi (+ lo)
-  __shared__ __attribute__((aligned(16))) char sS[R * 4 * SPLANE];
+  __shared__ __attribute__((aligned(16))) char sS[R * 4 * SPLANE + 256];  // + the overrun of columns 18-19
   __shared__ __attribute__((aligned(16))) char sA[R * 2 * APLANE];
   constexpr int SLO = 4 * SPLANE, ALO = 2 * APLANE;  // offset of the lo plane set
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
-  const int tpi = a.tiles_x * a.tiles_y;
-  // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so consecutive blockIdx land
-  // on different L2s and neighbouring tiles re-fetched their shared frame halo from HBM (2.8x the
-  // frame bytes).  Remapped, each XCD walks a contiguous run of tiles (neighbours share its L2).
-  const int nwg = gridDim.x, xq = nwg / 8, xr = nwg % 8, xcd = blockIdx.x % 8;
-  const int wid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + blockIdx.x / 8;
-  const int n = wid / tpi, tr = wid - n * tpi;
-  const int ty0 = (tr / a.tiles_x) * TH, tx0 = (tr - (tr / a.tiles_x) * a.tiles_x) * SB_TW;
+  const int tpi = a.tiles_x * a.tiles_y, total = a.N * tpi;
+  // tiles of XCD x (= blockIdx % 8, where the hardware deals consecutive blocks round-robin):
+  // [x * per_xcd, (x + 1) * per_xcd); its gx workgroups take consecutive tiles of that range
+  const int gx = gridDim.x / 8, xcd = blockIdx.x % 8;
+  const int t_end = min(total, (xcd + 1) * a.per_xcd);
+  auto tile_of = [&](int t, int& n, int& ty0, int& tx0) {
+    n = t / tpi;
+    const int tr = t - n * tpi;
+    ty0 = (tr / a.tiles_x) * TH;
+    tx0 = (tr - (tr / a.tiles_x) * a.tiles_x) * SB_TW;
+  };
 
-  // ---- phase 1: stem (fp32 VALU) -> S -------------------------------------------------------
-  // threads [0, SPIX/2) take S pixels i and i + SPIX/2: straight-line code, so every weight is one
-  // scalar load feeding two FMAs and nothing keeps the 288 weights live in registers
-  const float* fr = a.frames + (size_t)n * a.H * a.W;
+  // ---- phase-1 inputs: threads [0, SPIX/2) take S pixels i and i + SPIX/2 ---------------------
   static_assert(SPIX % 2 == 0 && SPIX / 2 <= 256, "stem tile");
-  if (tid < SPIX / 2) {
-    float in[2][9];
-    bool ok[2];
-    int pix[2];
+  const bool p1 = tid < SPIX / 2;
+  float in[2][9];
+  auto load_in = [&](int t) {
+    int n, ty0, tx0;
+    tile_of(t, n, ty0, tx0);
+    const float* fr = a.frames + (size_t)n * a.H * a.W;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int i = tid + h * (SPIX / 2);
-      pix[h] = i;
       const int sy = i / SB_SW, sx = i - (i / SB_SW) * SB_SW;
       const int oy = ty0 - 2 + sy, ox = tx0 - 2 + sx;  // stem output pixel
-      ok[h] = oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW;
+      const bool ok = oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW;
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
           const int iy = oy * 2 - a.pad_t + ky, ix = ox * 2 - a.pad_l + kx;
-          in[h][ky * 3 + kx] =
-              (ok[h] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) ? fr[(size_t)iy * a.W + ix] : 0.f;
+          in[h][ky * 3 + kx] = (ok && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) ? fr[(size_t)iy * a.W + ix] : 0.f;
         }
     }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t v[2][4], vl[2][4];
-#pragma unroll
-      for (int j = 0; j < 8; j += 2) {
-        const float bj0 = a.b9[q * 8 + j], bj1 = a.b9[q * 8 + j + 1];
-        float a0 = bj0, a1 = bj1, c0 = bj0, c1 = bj1;
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const float w0 = a.w9[(q * 8 + j) * 9 + t], w1 = a.w9[(q * 8 + j + 1) * 9 + t];
-          a0 += w0 * in[0][t];
-          a1 += w1 * in[0][t];
-          c0 += w0 * in[1][t];
-          c1 += w1 * in[1][t];
-        }
-        const float s0 = silu(a0), s1 = silu(a1), t0 = silu(c0), t1 = silu(c1);
-        v[0][j / 2] = ok[0] ? pack_bf16x2(s0, s1) : 0u;
-        v[1][j / 2] = ok[1] ? pack_bf16x2(t0, t1) : 0u;
-        if constexpr (SP) {  // lo halves: v - hi
-          vl[0][j / 2] = ok[0] ? pack_bf16x2(s0 - __uint_as_float(v[0][j / 2] << 16),
-                                             s1 - __uint_as_float(v[0][j / 2] & 0xffff0000u)) : 0u;
-          vl[1][j / 2] = ok[1] ? pack_bf16x2(t0 - __uint_as_float(v[1][j / 2] << 16),
-                                             t1 - __uint_as_float(v[1][j / 2] & 0xffff0000u)) : 0u;
-        }
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        *reinterpret_cast<uint4*>(sS + q * SPLANE + pix[h] * 16) = make_uint4(v[h][0], v[h][1], v[h][2], v[h][3]);
-        if constexpr (SP)
-          *reinterpret_cast<uint4*>(sS + SLO + q * SPLANE + pix[h] * 16) =
-              make_uint4(vl[h][0], vl[h][1], vl[h][2], vl[h][3]);
-      }
-    }
-  }
-  // resident weights of both convs (A fragments), in flight across the barrier
+  };
+  int t = xcd * a.per_xcd + (int)blockIdx.x / 8;
+  if (p1 && t < t_end) load_in(t);
+
+  // resident weights of both convs (A fragments)
   bf16x8 wf0[9], wf1[5], wl0[SP ? 9 : 1], wl1[SP ? 5 : 1];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const bf16_t* w = a.w0 + (size_t)r16 * a.kp0 * R + t * 32 + 8 * g;
-    wf0[t] = *reinterpret_cast<const bf16x8*>(w);
-    if constexpr (SP) wl0[t] = *reinterpret_cast<const bf16x8*>(w + a.kp0);
+  for (int k = 0; k < 9; ++k) {
+    const bf16_t* w = a.w0 + (size_t)r16 * a.kp0 * R + k * 32 + 8 * g;
+    wf0[k] = *reinterpret_cast<const bf16x8*>(w);
+    if constexpr (SP) wl0[k] = *reinterpret_cast<const bf16x8*>(w + a.kp0);
   }
 #pragma unroll
-  for (int t = 0; t < 5; ++t) {
-    const bf16_t* w = a.w1 + (size_t)r16 * a.kp1 * R + t * 32 + 8 * g;
-    wf1[t] = *reinterpret_cast<const bf16x8*>(w);
-    if constexpr (SP) wl1[t] = *reinterpret_cast<const bf16x8*>(w + a.kp1);
+  for (int k = 0; k < 5; ++k) {
+    const bf16_t* w = a.w1 + (size_t)r16 * a.kp1 * R + k * 32 + 8 * g;
+    wf1[k] = *reinterpret_cast<const bf16x8*>(w);
+    if constexpr (SP) wl1[k] = *reinterpret_cast<const bf16x8*>(w + a.kp1);
   }
+  // the stem's weights and biases in LDS (uniform-address reads broadcast): read from global inside
+  // the tile loop they were vector loads (the loop's stores of y rule out scalar loads), each tile
+  // waiting on ~100 of them
+  __shared__ float sw9[288 + 32];
+  for (int i = tid; i < 320; i += 256) sw9[i] = i < 288 ? a.w9[i] : a.b9[i - 288];
+  const float4 bb0 = *reinterpret_cast<const float4*>(a.b0 + 4 * g);
+  const float4 bb1 = *reinterpret_cast<const float4*>(a.b1 + 4 * g);
   __syncthreads();
 
-  // ---- phase 2: blocks.0.0 (32 -> 16) on MFMA -> A --------------------------------------------
-  {
-    int sbase[AMS];
+  for (; t < t_end; t += gx) {
+    int n, ty0, tx0;
+    tile_of(t, n, ty0, tx0);
+    // ---- phase 1: stem (fp32 VALU) -> S -----------------------------------------------------
+    // (S is free: every wave passed this tile's predecessor's phase-2/3 barrier before reaching here.)
+    if (p1) {
+      bool ok[2];
+      int pix[2];
 #pragma unroll
-    for (int i = 0; i < AMS; ++i) {
-      const int pa = min(16 * (wave + 4 * i) + r16, APIX - 1);
-      const int ay = pa / SB_AW, ax = pa - (pa / SB_AW) * SB_AW;
-      sbase[i] = (ay * SB_SW + ax) * 16 + g * SPLANE;
+      for (int h = 0; h < 2; ++h) {
+        const int i = tid + h * (SPIX / 2);
+        pix[h] = i;
+        const int sy = i / SB_SW, sx = i - (i / SB_SW) * SB_SW;
+        const int oy = ty0 - 2 + sy, ox = tx0 - 2 + sx;
+        ok[h] = oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t v[2][4], vl[2][4];
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const float bj0 = sw9[288 + q * 8 + j], bj1 = sw9[288 + q * 8 + j + 1];
+          float a0 = bj0, a1 = bj1, c0 = bj0, c1 = bj1;
+#pragma unroll
+          for (int k = 0; k < 9; ++k) {
+            const float w0 = sw9[(q * 8 + j) * 9 + k], w1 = sw9[(q * 8 + j + 1) * 9 + k];
+            a0 += w0 * in[0][k];
+            a1 += w1 * in[0][k];
+            c0 += w0 * in[1][k];
+            c1 += w1 * in[1][k];
+          }
+          const float s0 = silu(a0), s1 = silu(a1), t0 = silu(c0), t1 = silu(c1);
+          v[0][j / 2] = ok[0] ? pack_bf16x2(s0, s1) : 0u;
+          v[1][j / 2] = ok[1] ? pack_bf16x2(t0, t1) : 0u;
+          if constexpr (SP) {  // lo halves: v - hi
+            vl[0][j / 2] = ok[0] ? pack_bf16x2(s0 - __uint_as_float(v[0][j / 2] << 16),
+                                               s1 - __uint_as_float(v[0][j / 2] & 0xffff0000u)) : 0u;
+            vl[1][j / 2] = ok[1] ? pack_bf16x2(t0 - __uint_as_float(v[1][j / 2] << 16),
+                                               t1 - __uint_as_float(v[1][j / 2] & 0xffff0000u)) : 0u;
+          }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          *reinterpret_cast<uint4*>(sS + q * SPLANE + pix[h] * 16) = make_uint4(v[h][0], v[h][1], v[h][2], v[h][3]);
+          if constexpr (SP)
+            *reinterpret_cast<uint4*>(sS + SLO + q * SPLANE + pix[h] * 16) =
+                make_uint4(vl[h][0], vl[h][1], vl[h][2], vl[h][3]);
+        }
+      }
+      // the next tile's frame pixels, in flight through phases 2 and 3
+      if (t + gx < t_end) load_in(t + gx);
     }
-    f32x4 acc[AMS];
-#pragma unroll
-    for (int i = 0; i < AMS; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int toff = ((t / 3) * SB_SW + (t % 3)) * 16;
+    __syncthreads();
+
+    // ---- phase 2: blocks.0.0 (32 -> 16) on MFMA -> A ------------------------------------------
+    {
+      int sbase[AMS];
 #pragma unroll
       for (int i = 0; i < AMS; ++i) {
-        if (wave + 4 * i < ASUB) {
-          const bf16x8 b = frag(sS + sbase[i] + toff);
-          if constexpr (SP)
-            acc[i] = mma3(wf0[t], wl0[t], b, frag(sS + SLO + sbase[i] + toff), acc[i]);
-          else
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[t], b, acc[i], 0, 0, 0);
-        }
+        const int pa = min(16 * (wave + 4 * i) + r16, APIX - 1);
+        sbase[i] = pa * 16 + g * SPLANE;  // (A and S share the pitch; the taps of columns 18-19 may read
+                                          // into the next plane or the pad: ignored results)
       }
-    }
-    const float4 bb = *reinterpret_cast<const float4*>(a.b0 + 4 * g);
+      f32x4 acc[AMS];
 #pragma unroll
-    for (int i = 0; i < AMS; ++i) {
-      const int pa = 16 * (wave + 4 * i) + r16;
-      if (wave + 4 * i >= ASUB || pa >= APIX) continue;
-      const int ay = pa / SB_AW, ax = pa - (pa / SB_AW) * SB_AW;
-      const int oy = ty0 - 1 + ay, ox = tx0 - 1 + ax;
-      uint2 u = make_uint2(0u, 0u), ul = make_uint2(0u, 0u);
-      if (oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW) {
-        const float v[4] = {silu(acc[i][0] + bb.x), silu(acc[i][1] + bb.y), silu(acc[i][2] + bb.z),
-                            silu(acc[i][3] + bb.w)};
-        if constexpr (SP) {
-          split4(v, u, ul);
-        } else {
-          u.x = pack_bf16x2(v[0], v[1]);
-          u.y = pack_bf16x2(v[2], v[3]);
+      for (int i = 0; i < AMS; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int toff = ((k / 3) * SB_SW + (k % 3)) * 16;
+#pragma unroll
+        for (int i = 0; i < AMS; ++i) {
+          if (wave + 4 * i < ASUB) {
+            const bf16x8 b = frag(sS + sbase[i] + toff);
+            if constexpr (SP)
+              acc[i] = mma3(wf0[k], wl0[k], b, frag(sS + SLO + sbase[i] + toff), acc[i]);
+            else
+              acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[k], b, acc[i], 0, 0, 0);
+          }
         }
       }
-      *reinterpret_cast<uint2*>(sA + (g >> 1) * APLANE + pa * 16 + (g & 1) * 8) = u;
-      if constexpr (SP) *reinterpret_cast<uint2*>(sA + ALO + (g >> 1) * APLANE + pa * 16 + (g & 1) * 8) = ul;
+#pragma unroll
+      for (int i = 0; i < AMS; ++i) {
+        const int pa = 16 * (wave + 4 * i) + r16;
+        const int ay = pa / SB_AW, ax = pa - (pa / SB_AW) * SB_AW;
+        if (wave + 4 * i >= ASUB || pa >= APIX || ax >= SB_AV) continue;
+        const int oy = ty0 - 1 + ay, ox = tx0 - 1 + ax;
+        uint2 u = make_uint2(0u, 0u), ul = make_uint2(0u, 0u);
+        if (oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW) {
+          const float v[4] = {silu(acc[i][0] + bb0.x), silu(acc[i][1] + bb0.y), silu(acc[i][2] + bb0.z),
+                              silu(acc[i][3] + bb0.w)};
+          if constexpr (SP) {
+            split4(v, u, ul);
+          } else {
+            u.x = pack_bf16x2(v[0], v[1]);
+            u.y = pack_bf16x2(v[2], v[3]);
+          }
+        }
+        *reinterpret_cast<uint2*>(sA + (g >> 1) * APLANE + pa * 16 + (g & 1) * 8) = u;
+        if constexpr (SP) *reinterpret_cast<uint2*>(sA + ALO + (g >> 1) * APLANE + pa * 16 + (g & 1) * 8) = ul;
+      }
     }
-  }
-  __syncthreads();
+    __syncthreads();
 
-  // ---- phase 3: blocks.0.1 (16 -> 16) + skip on MFMA -> y -------------------------------------
-  {
-    // K step st covers taps 2st (lanes g < 2) and 2st + 1 (g >= 2), 16 channels each; the pad tap 9
-    // (zero weights) reads tap 0's pixel so the product stays finite
-    int toff[5];
+    // ---- phase 3: blocks.0.1 (16 -> 16) + skip on MFMA -> y -----------------------------------
+    {
+      // K step st covers taps 2st (lanes g < 2) and 2st + 1 (g >= 2), 16 channels each; the pad tap
+      // 9 (zero weights) reads tap 0's pixel so the product stays finite
+      int toff[5];
 #pragma unroll
-    for (int st = 0; st < 5; ++st) {
-      int t = 2 * st + (g >> 1);
-      if (t > 8) t = 0;
-      toff[st] = ((t / 3) * SB_AW + (t % 3)) * 16 + (g & 1) * APLANE;
-    }
-    f32x4 acc[OMS];
+      for (int st = 0; st < 5; ++st) {
+        int k = 2 * st + (g >> 1);
+        if (k > 8) k = 0;
+        toff[st] = ((k / 3) * SB_AW + (k % 3)) * 16 + (g & 1) * APLANE;
+      }
+      f32x4 acc[OMS];
 #pragma unroll
-    for (int i = 0; i < OMS; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < OMS; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int st = 0; st < 5; ++st)
+      for (int st = 0; st < 5; ++st)
+#pragma unroll
+        for (int i = 0; i < OMS; ++i) {
+          const int row = wave + 4 * i;  // output tile row = subtile
+          const char* p = sA + (row * SB_AW + r16) * 16 + toff[st];
+          if constexpr (SP)
+            acc[i] = mma3(wf1[st], wl1[st], frag(p), frag(p + ALO), acc[i]);
+          else
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[st], frag(p), acc[i], 0, 0, 0);
+        }
+      const int ox = tx0 + r16;
 #pragma unroll
       for (int i = 0; i < OMS; ++i) {
-        const int row = wave + 4 * i;  // output tile row = subtile
-        const char* p = sA + (row * SB_AW + r16) * 16 + toff[st];
-        if constexpr (SP)
-          acc[i] = mma3(wf1[st], wl1[st], frag(p), frag(p + ALO), acc[i]);
-        else
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[st], frag(p), acc[i], 0, 0, 0);
-      }
-    const float4 bb = *reinterpret_cast<const float4*>(a.b1 + 4 * g);
-    const int ox = tx0 + r16;
+        const int row = wave + 4 * i, oy = ty0 + row;
+        if (oy >= a.OH || ox >= a.OW) continue;
+        const int soff = (g >> 1) * APLANE + ((row + 1) * SB_AW + r16 + 1) * 16 + (g & 1) * 8;
+        float r[4];
+        unpack_bf16x4(*reinterpret_cast<const uint2*>(sA + soff), r);
+        if constexpr (SP) {
+          float rl[4];
+          unpack_bf16x4(*reinterpret_cast<const uint2*>(sA + ALO + soff), rl);
 #pragma unroll
-    for (int i = 0; i < OMS; ++i) {
-      const int row = wave + 4 * i, oy = ty0 + row;
-      if (oy >= a.OH || ox >= a.OW) continue;
-      const int soff = (g >> 1) * APLANE + ((row + 1) * SB_AW + r16 + 1) * 16 + (g & 1) * 8;
-      float r[4];
-      unpack_bf16x4(*reinterpret_cast<const uint2*>(sA + soff), r);
-      if constexpr (SP) {
-        float rl[4];
-        unpack_bf16x4(*reinterpret_cast<const uint2*>(sA + ALO + soff), rl);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) r[j] += rl[j];
-      }
-      const float v[4] = {silu(acc[i][0] + bb.x) + r[0], silu(acc[i][1] + bb.y) + r[1], silu(acc[i][2] + bb.z) + r[2],
-                          silu(acc[i][3] + bb.w) + r[3]};
-      bf16_t* yo = a.y + (((size_t)n * a.OH + oy) * a.OW + ox) * 16 * R + 4 * g;
-      if constexpr (SP) {
-        uint2 h, l;
-        split4(v, h, l);
-        *reinterpret_cast<uint2*>(yo) = h;
-        *reinterpret_cast<uint2*>(yo + 16) = l;
-      } else {
-        *reinterpret_cast<uint2*>(yo) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+          for (int j = 0; j < 4; ++j) r[j] += rl[j];
+        }
+        const float v[4] = {silu(acc[i][0] + bb1.x) + r[0], silu(acc[i][1] + bb1.y) + r[1],
+                            silu(acc[i][2] + bb1.z) + r[2], silu(acc[i][3] + bb1.w) + r[3]};
+        bf16_t* yo = a.y + (((size_t)n * a.OH + oy) * a.OW + ox) * 16 * R + 4 * g;
+        if constexpr (SP) {
+          uint2 h, l;
+          split4(v, h, l);
+          *reinterpret_cast<uint2*>(yo) = h;
+          *reinterpret_cast<uint2*>(yo + 16) = l;
+        } else {
+          *reinterpret_cast<uint2*>(yo) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        }
       }
     }
   }
@@ -285,12 +328,24 @@ void launch_stem_b0(const float* frames, int N, int H, int W, int OH, int OW, in
   a.tiles_x = ceil_div(OW, SB_TW);
   a.tiles_y = ceil_div(OH, TH);
   M2S_CHECK((double)N * a.tiles_x * a.tiles_y < 2147483647.0, "stem_b0: grid");
+  // persistent grid: the resident workgroups of the device (two per CU split, three bf16), a multiple
+  // of 8 (one equal share per XCD); small inputs take fewer
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    M2S_HIP(hipGetDevice(&dev));
+    M2S_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev));
+    return v;
+  }();
+  const int total = N * a.tiles_x * a.tiles_y;
+  a.per_xcd = ceil_div(total, 8);
+  const int per_cu = split ? 2 : 3;
+  const int grid = 8 * std::max(1, std::min(ceil_div(cus * per_cu, 8), a.per_xcd));
   if (split) {
     ProfScope ps("stem_b0_kernel<16, 1>", flops, bytes, s);
-    hipLaunchKernelGGL((stem_b0_kernel<TH, 1>), dim3(N * a.tiles_x * a.tiles_y), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((stem_b0_kernel<TH, 1>), dim3(grid), dim3(256), 0, s, a);
   } else {
     ProfScope ps("stem_b0_kernel<16, 0>", flops, bytes, s);
-    hipLaunchKernelGGL((stem_b0_kernel<TH, 0>), dim3(N * a.tiles_x * a.tiles_y), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((stem_b0_kernel<TH, 0>), dim3(grid), dim3(256), 0, s, a);
   }
   M2S_HIP(hipGetLastError());
 }
