@@ -1172,7 +1172,7 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
       }
     }
   }
-  ProfScope ps(tname<T>("conv_post_kernel"), 2.0 * B * L * post_c_ * 7, (sizeof(T) * Elem<T>::R) * (double)B * L * post_c_ + 4.0 * B * L, s);
+  ProfScope ps(tname<T>(post_c_ <= 64 ? "conv_post_tile_kernel" : "conv_post_kernel"), 2.0 * B * L * post_c_ * 7, (sizeof(T) * Elem<T>::R) * (double)B * L * post_c_ + 4.0 * B * L, s);
   launch_conv_post<T>(S, B, L, post_c_, chan_stride(post_c_), static_cast<const float*>(arena_.ptr(post_w_)), post_b_,
                       wav, s);
 }
