@@ -60,26 +60,31 @@ __global__ void __launch_bounds__(256) se_excite_kernel(const bf16_t* __restrict
   constexpr int R = SP ? 2 : 1;
   constexpr int UB = SP ? 4 : 8;  // k-steps of loads in flight per batch
   __shared__ __attribute__((aligned(16))) bf16_t hid[R][SE_IMG][SE_HROW];
+  __shared__ __attribute__((aligned(16))) f32x4 part[4][64];  // K-split partial sums
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const int n0 = blockIdx.x * SE_IMG;
   const bool img_ok = n0 + r16 < N;
 
-  // ---- conv_reduce + SiLU: wave w owns hidden rows [16w, 16w + 16) ------------------------------
+  // ---- conv_reduce + SiLU: RT = ceil(rd / 16) row tiles; the 4 waves split K 4 / RT ways --------
+  // (wave w: row tile w % RT, k-steps w / RT, w / RT + KSP, ...), partials summed in LDS in a fixed
+  // order.  One wave per row tile walked all cs_mid / 32 k-steps alone with two or three waves idle.
   {
-    const int row = 16 * wave + r16;
+    const int RT = (rd + 15) / 16, KSP = 4 / RT;
+    const int rt = wave % RT, kq = wave / RT;
+    const int row = 16 * rt + r16;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (16 * wave < rd) {
+    if (kq < KSP) {
       const bf16_t* wr = w1 + (size_t)row * kp1 * R + 8 * g;
       const bf16_t* mr = mean + (size_t)(n0 + r16) * cs_mid * R + 8 * g;
       // UB k-steps of loads in flight per batch: the chain is load-latency bound, not MFMA bound
       const bool rok = row < rd;
-      for (int k0 = 0; k0 < cs_mid; k0 += UB * 32) {
+      for (int k0 = 32 * kq; k0 < cs_mid; k0 += UB * 32 * KSP) {
         bf16x8 a[UB], b[UB], al[UB], bl[UB];
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
-          const int k = k0 + 32 * u;
+          const int k = k0 + 32 * KSP * u;
           a[u] = ld8(wr + k, rok && k < cs_mid);
           b[u] = ld8(mr + k, img_ok && k < cs_mid);
           if constexpr (SP) {
@@ -91,14 +96,22 @@ __global__ void __launch_bounds__(256) se_excite_kernel(const bf16_t* __restrict
         for (int u = 0; u < UB; ++u) acc = mma<SP>(a[u], al[u], b[u], bl[u], acc);
       }
     }
-    // lane holds hidden rows 16w + 4g .. + 3 of image r16
-    float h[4];
+    part[wave][lane] = acc;
+    __syncthreads();
+    if (wave < RT) {
+      for (int q = 1; q < KSP; ++q) acc += part[wave + RT * q][lane];
+      // lane holds hidden rows 16w + 4g .. + 3 of image r16
+      float h[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = 16 * wave + 4 * g + j;
-      h[j] = r < rd ? silu(acc[j] + b1[r]) : 0.f;
+      for (int j = 0; j < 4; ++j) {
+        const int r = 16 * wave + 4 * g + j;
+        h[j] = r < rd ? silu(acc[j] + b1[r]) : 0.f;
+      }
+      st4<SP>(&hid[0][r16][16 * wave + 4 * g], SE_IMG * SE_HROW, h);
+    } else if (wave < 4 && 16 * wave < SE_RDMAX) {  // rows past rd: zeros (read by the expand's k-steps)
+      const float z[4] = {0.f, 0.f, 0.f, 0.f};
+      st4<SP>(&hid[0][r16][16 * wave + 4 * g], SE_IMG * SE_HROW, z);
     }
-    st4<SP>(&hid[0][r16][16 * wave + 4 * g], SE_IMG * SE_HROW, h);
   }
   __syncthreads();
 
@@ -111,12 +124,14 @@ __global__ void __launch_bounds__(256) se_excite_kernel(const bf16_t* __restrict
   }
   const int nks = kp2 / 32;
   const int ntile = cs_mid / 16;
-  // 4 channel tiles per batch, all their weight fragments loaded before the MFMAs
-  for (int t0 = wave; t0 < ntile; t0 += 4 * 4) {
+  // channel tiles dealt over the gridDim.y workgroups of these images and their 4 waves (tile
+  // 4 * (y + gridDim.y * v) + wave); 4 tiles per batch, all their weight fragments loaded first
+  const int ts = 4 * gridDim.y;
+  for (int t0 = 4 * blockIdx.y + wave; t0 < ntile; t0 += 4 * ts) {
     bf16x8 a[4][SE_RDMAX / 32], al[4][SE_RDMAX / 32];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int c = 16 * (t0 + 4 * u) + r16;  // weight row of this lane's A fragment
+      const int c = 16 * (t0 + ts * u) + r16;  // weight row of this lane's A fragment
 #pragma unroll
       for (int ks = 0; ks < SE_RDMAX / 32; ++ks) {
         const bf16_t* wp = w2 + (size_t)c * kp2 * R + 32 * ks + 8 * g;
@@ -126,7 +141,7 @@ __global__ void __launch_bounds__(256) se_excite_kernel(const bf16_t* __restrict
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int t = t0 + 4 * u;
+      const int t = t0 + ts * u;
       if (t >= ntile) break;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -154,7 +169,17 @@ void launch_se_excite(const void* mean, int N, int mid, int cs_mid, const void* 
   ProfScope ps(split ? "se_excite_kernel<1>" : "se_excite_kernel<0>", 2.0 * 2.0 * N * mid * rd,
                es * (2.0 * N * cs_mid) + es * 2.0 * mid * rd, s);
   auto k = split ? se_excite_kernel<1> : se_excite_kernel<0>;
-  hipLaunchKernelGGL(k, dim3(ceil_div(N, SE_IMG)), dim3(256), 0, s, static_cast<const bf16_t*>(mean), N, mid, cs_mid,
+  // expand tiles split over ES workgroups per 16 images (each recomputes the reduce) while the grid
+  // stays within one workgroup per CU: 1920 images were 120 workgroups (0.67 ms per step); ES = 2
+  // gives 0.50, and ES = 3 / 4 / 8 (past one per CU) 0.64 / 0.61 / 0.87
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    M2S_HIP(hipGetDevice(&dev));
+    M2S_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev));
+    return v;
+  }();
+  const int nwg = ceil_div(N, SE_IMG), ES = std::max(1, std::min(std::min(cus / nwg, cs_mid / 64), 8));
+  hipLaunchKernelGGL(k, dim3(nwg, ES), dim3(256), 0, s, static_cast<const bf16_t*>(mean), N, mid, cs_mid,
                      static_cast<const bf16_t*>(w1), kp1, b1, rd, static_cast<const bf16_t*>(w2), kp2, b2,
                      static_cast<bf16_t*>(gate));
   M2S_HIP(hipGetLastError());
