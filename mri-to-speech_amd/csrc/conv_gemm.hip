@@ -15,6 +15,8 @@
 // one M tile run on one XCD (shared A rows stay in that XCD's L2).
 #include "conv_igemm.hpp"
 
+#include <cstring>
+
 #include "prof.hpp"
 
 namespace m2s {
@@ -149,7 +151,9 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * ROW + ((ch
 // hi*hi + hi*lo + lo*hi (the dropped lo*lo term is below 2^-16 of the product).
 // SP = 2: e4m3 operands over bf16 storage (conv_igemm.hpp launch_conv_gemm, a.wscale).
 template <int BM, int BN, int MT, int NT, int S, int KIND, int XF, int SP>
-__global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 2 : 1)) conv_gemm_kernel(const ConvArgs a, int n_tiles, int se_imgs) {
+__global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 2 : 1)) conv_gemm_kernel(const ConvBatch ab, int n_tiles, int se_imgs) {
+  // KIND_CONV1D launches may batch convs of one shape over grid.z (launch_conv_gemm_batch)
+  const ConvArgs& a = ab.a[KIND == KIND_CONV1D ? blockIdx.z : 0];
   constexpr int WN = BN / (NT * 16);
   constexpr int WM = 4 / WN;
   static_assert(WM * WN == 4 && WM * MT * 16 == BM, "bad tile");
@@ -175,7 +179,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
   const int wid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + orig / 8;
   const int mt = wid / n_tiles, nt = wid - (wid / n_tiles) * n_tiles;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int phase = blockIdx.z;
+  const int phase = KIND == KIND_CONVT ? (int)blockIdx.z : 0;
 
   const bf16_t* __restrict__ X = static_cast<const bf16_t*>(a.x);
   const bf16_t* __restrict__ W = static_cast<const bf16_t*>(a.w) + (size_t)phase * a.n_pad * a.kp * R;
@@ -485,16 +489,19 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
         v[2] = fmaf(acc[ni][mi][2], ws.z, bb.z);
         v[3] = fmaf(acc[ni][mi][3], ws.w, bb.w);
       }
-      if (a.act == ACT_SILU) {
+      auto apply_act = [&]() {
+        if (a.act == ACT_SILU) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = silu(v[j]);
-      } else if (a.act == ACT_LRELU) {
+          for (int j = 0; j < 4; ++j) v[j] = silu(v[j]);
+        } else if (a.act == ACT_LRELU) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * a.act_slope;
-      } else if (a.act == ACT_SIGMOID) {
+          for (int j = 0; j < 4; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * a.act_slope;
+        } else if (a.act == ACT_SIGMOID) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = sigmoidf_(v[j]);
-      }
+          for (int j = 0; j < 4; ++j) v[j] = sigmoidf_(v[j]);
+        }
+      };
+      if (!a.act_after_res) apply_act();
       if (Rs) {
         float r[4];
         ld4f(Rs + orow + n4, r);
@@ -503,6 +510,10 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
           ld4f(Rs + orow + a.cs_out + n4, rl);
 #pragma unroll
           for (int j = 0; j < 4; ++j) r[j] += rl[j];
+        }
+        if (a.res_unslope != 0.f) {  // the residual was stored as lrelu(x): invert it
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r[j] = r[j] > 0.f ? r[j] : r[j] * a.res_unslope;
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] += r[j];
@@ -523,6 +534,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
           for (int j = 0; j < 4; ++j) v[j] = v[j] / a.accum_div;
         }
       }
+      if (a.act_after_res) apply_act();
       if constexpr (SP == 1) {
         uint2 hi, lo;
         split4(v, hi, lo);
@@ -551,7 +563,8 @@ const char* kname(int k) {
 inline int se_images(int BM, int OH) { return BM % OH == 0 ? BM / OH : OH % BM == 0 ? 1 : (BM + OH - 1) / OH + 1; }
 
 template <int BM, int BN, int MT, int NT, int KIND, int XF, int SP>
-void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
+void launch_tile(const ConvBatch& b, hipStream_t s, int phases, double flops, double bytes) {
+  const ConvArgs& a = b.a[0];
   // keep two workgroups' LDS per CU (128 x 256: the SE gate table too, and 256 registers a wave);
   // split operands double the slot, so they run two stages
   constexpr int S = SP == 1 ? (BM == 128 && BN == 64 && XF != IN_SE_SCALE ? 3 : 2) : (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
@@ -578,12 +591,12 @@ void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
   else
     snprintf(name, sizeof(name), "conv_gemm_kernel<%d, %d, %d, %d, %d, %d, %d, %d>", BM, BN, MT, NT, S, KIND, XF, SP);
   ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF, SP>), grid, dim3(256), lds, s, a, n_tiles, se_imgs);
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF, SP>), grid, dim3(256), lds, s, b, n_tiles, se_imgs);
 }
 
 template <int KIND, int XF, int SP>
-void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
-  const int n = a.cs_out;
+void launch_kind_xf(const ConvBatch& a, hipStream_t s, int phases, double flops, double bytes) {
+  const int n = a.a[0].cs_out;
   if constexpr (SP != 0) {  // split / e4m3 operands: 16/32/64-wide tiles for narrow outputs, else 128 x 128
     if (n <= 16)
       return launch_tile<256, 16, 4, 1, KIND, XF, SP>(a, s, phases, flops, bytes);
@@ -597,8 +610,8 @@ void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, 
     }
     return launch_tile<128, 128, 4, 4, KIND, XF, SP>(a, s, phases, flops, bytes);
   } else {
-  if constexpr (KIND == KIND_GEMM || KIND == KIND_CONV2D) if (a.M >= 256 * 256 && n > 128 &&
-                                                               ((n <= 256 && a.kp >= 512) || KIND == KIND_GEMM)) {
+  if constexpr (KIND == KIND_GEMM || KIND == KIND_CONV2D) if (a.a[0].M >= 256 * 256 && n > 128 &&
+                                                               ((n <= 256 && a.a[0].kp >= 512) || KIND == KIND_GEMM)) {
     // long-K 1x1 GEMMs and 3x3 convs with 129..256 outputs: one 256-wide n tile reads (gathers)
     // the activations once instead of twice (b5 conv_pwl 1248 -> 208: 13.5 -> 10.0 ms per 4 steps;
     // b2 conv_exp 3x3 56 -> 224: 1.10 -> 0.91 ms per launch); also every wide 1x1 GEMM (the
@@ -607,7 +620,7 @@ void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, 
     return launch_tile<128, 256, 4, 8, KIND, XF, 0>(a, s, phases, flops, bytes);
   }
   if constexpr (KIND == KIND_GEMM)
-    if (a.M >= 256 * 256 && n > 64 && n <= 128 && a.kp >= 384) {
+    if (a.a[0].M >= 256 * 256 && n > 64 && n <= 128 && a.a[0].kp >= 384) {
       // 256 rows x 128 outputs at two waves per SIMD: the weight tile (K x 128) is re-read from L2
       // once per 256 rows instead of per 128 (the SE-scaled conv_pwl of blocks.3/4: K 416..736)
       return launch_tile<256, 128, 8, 4, KIND, XF, 0>(a, s, phases, flops, bytes);
@@ -625,14 +638,20 @@ void launch_kind_xf(const ConvArgs& a, hipStream_t s, int phases, double flops, 
 
 // Only the (kind, input transform) pairs the hot path uses are instantiated.
 template <int KIND, int SP>
-void launch_kind(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
-  if (a.in_xform == IN_NONE) {
+void launch_kind(const ConvArgs& a0, hipStream_t s, int phases, double flops, double bytes, const ConvBatch* batch = nullptr) {
+  ConvBatch bl;
+  if (!batch) {
+    std::memset(&bl, 0, sizeof(bl));
+    bl.a[0] = a0;
+  }
+  const ConvBatch& a = batch ? *batch : bl;
+  if (a0.in_xform == IN_NONE) {
     launch_kind_xf<KIND, IN_NONE, SP>(a, s, phases, flops, bytes);
   } else if constexpr (KIND == KIND_CONV1D || KIND == KIND_CONVT) {
-    M2S_CHECK(a.in_xform == IN_LRELU, "conv_gemm: 1-D kinds take LeakyReLU inputs only");
+    M2S_CHECK(a0.in_xform == IN_LRELU, "conv_gemm: 1-D kinds take LeakyReLU inputs only");
     launch_kind_xf<KIND, IN_LRELU, SP>(a, s, phases, flops, bytes);
   } else if constexpr (KIND == KIND_GEMM) {
-    M2S_CHECK(a.in_xform == IN_SE_SCALE, "conv_gemm: GEMM kind takes SE-scaled inputs only");
+    M2S_CHECK(a0.in_xform == IN_SE_SCALE, "conv_gemm: GEMM kind takes SE-scaled inputs only");
     launch_kind_xf<KIND, IN_SE_SCALE, SP>(a, s, phases, flops, bytes);
   } else {
     M2S_CHECK(false, "conv_gemm: 2-D convs take untransformed inputs");
@@ -640,6 +659,26 @@ void launch_kind(const ConvArgs& a, hipStream_t s, int phases, double flops, dou
 }
 
 }  // namespace
+
+void launch_conv_gemm_batch(const ConvArgs* as, int n, hipStream_t s, double flops, double bytes) {
+  M2S_CHECK(n >= 1 && n <= CONV_BATCH, "conv_gemm batch: 1..CONV_BATCH convs");
+  const ConvArgs& a = as[0];
+  M2S_CHECK(a.kind == KIND_CONV1D && a.cs_in >= 32 && a.cs_in % 32 == 0 && a.cs_out % 4 == 0, "conv_gemm batch: 1-D convs, cs_in % 32 == 0");
+  ConvBatch b;
+  std::memset(&b, 0, sizeof(b));
+  for (int i = 0; i < n; ++i) {
+    const ConvArgs& c = as[i];
+    M2S_CHECK(c.kind == a.kind && c.M == a.M && c.cs_in == a.cs_in && c.cs_out == a.cs_out && c.n_pad == a.n_pad &&
+                  c.in_xform == a.in_xform && c.L_in == a.L_in && c.L_out == a.L_out,
+              "conv_gemm batch: convs of one shape");
+    M2S_CHECK(c.kp % 32 == 0 && c.kp >= c.ntaps * c.cs_in && c.ntaps <= 31, "conv_gemm batch: kp / taps");
+    M2S_CHECK((double)(c.M / c.L_out) * c.L_in * c.cs_in * 2 < 2147483647.0, "conv_gemm batch: 32-bit offsets");
+    b.a[i] = c;
+  }
+  if (a.M <= 0) return;
+  launch_kind<KIND_CONV1D, 1>(a, s, n, flops, bytes, &b);
+  M2S_HIP(hipGetLastError());
+}
 
 void launch_conv_gemm(const ConvArgs& a, bool split, hipStream_t s, double flops, double bytes) {
   M2S_CHECK(a.cs_in % 8 == 0 && a.cs_out % 4 == 0, "conv_gemm: channel strides");

@@ -48,6 +48,17 @@ struct ConvArgs {
   int in_xform; float in_slope;
   int accum;            // 0: y = v ; 1: y = y_prev + v ; 2: y = (y_prev + v) / accum_div
   float accum_div;
+  // split conv_gemm only (the pre-activated MRF chain, model.cpp Vocoder::run_t):
+  float res_unslope;    // != 0: res holds lrelu(x); x = r > 0 ? r : r * res_unslope (slope 0.1 -> 10)
+  int act_after_res;    // act applied after the residual add (y = lrelu(v + x)) instead of before it
+};
+
+// Up to CONV_BATCH 1-D convs of one shape (same kind, M, cs_in, cs_out, n_pad; own x / w / bias / res
+// / y / taps / dilation) in ONE launch, grid.z = batch index: the independent resblocks of an MRF
+// stage (models.py:119-125) share a launch so their tiles fill the chip together.
+constexpr int CONV_BATCH = 3;
+struct ConvBatch {
+  ConvArgs a[CONV_BATCH];
 };
 
 // flops / bytes: algorithmic work of this launch, recorded by the profiler (m2s_prof_*).
@@ -60,6 +71,9 @@ void launch_conv(const ConvArgs& a, hipStream_t s, double flops = 0.0, double by
 // w / wscale[n], the activation fragments are rounded to e4m3 after the LDS read, the products run
 // on v_mfma_f32_16x16x32_fp8_fp8 and the epilogue multiplies by wscale[n].
 void launch_conv_gemm(const ConvArgs& a, bool split, hipStream_t s, double flops, double bytes);
+// n (1..CONV_BATCH) split-fp32 KIND_CONV1D convs of one shape in one launch; put the longest K first
+// (blocks dispatch in z order, so the longest tiles start first and the short ones fill the tail).
+void launch_conv_gemm_batch(const ConvArgs* a, int n, hipStream_t s, double flops, double bytes);
 // bf16 3x3 stride-1 convs with cs_in in {32, 64}: persistent LDS-resident-weight kernel
 // (conv_halo.hip); launch_conv_gemm routes them there.
 bool conv_halo_supported(const ConvArgs& a);

@@ -8,6 +8,7 @@
 //   * LSTM b_ih + b_hh.
 #include "model.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -187,8 +188,10 @@ static ConvArgs conv_args(const PConv& p) {
   return a;
 }
 
+// algorithmic work of one conv launch (profiler records): flops, and compulsory traffic = input
+// once, output once (+ residual / accumulator read), weights once
 template <typename T>
-static void run_conv(const ConvArgs& a, const PConv& p, hipStream_t s) {
+static void conv_cost(const ConvArgs& a, const PConv& p, double* flops_out, double* bytes_out) {
   const double rows = (double)a.M;
   const double flops = 2.0 * p.macs_per_row * rows;
   const double es = sizeof(T) * Elem<T>::R;
@@ -199,6 +202,14 @@ static void run_conv(const ConvArgs& a, const PConv& p, hipStream_t s) {
   const double out_rows = rows * (p.kind == KIND_CONVT ? p.ct_u : 1);
   const double bytes = es * (in_rows * p.cin + out_rows * p.cout * (1 + (a.res ? 1 : 0) + (a.accum ? 1 : 0)) +
                              (double)p.phases * p.cout * p.ntaps * p.cin);
+  *flops_out = flops;
+  *bytes_out = bytes;
+}
+
+template <typename T>
+static void run_conv(const ConvArgs& a, const PConv& p, hipStream_t s) {
+  double flops, bytes;
+  conv_cost<T>(a, p, &flops, &bytes);
   launch_conv<T>(a, s, flops, bytes);
 }
 
@@ -901,6 +912,7 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
   // fp8 engines: e4m3 resblock (MRF) convs; conv_pre and the upsamplers stay bf16
   const int io_dt = dtype == M2S_DT_FP8 ? M2S_DT_BF16 : dtype;
   if (const char* e = std::getenv("M2S_MRF_FUSED")) mrf_fused_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_MRF_BATCH")) mrf_batch_ = std::strcmp(e, "0") != 0;
   M2S_CHECK(h.n_up >= 1 && h.n_up <= 8 && h.n_kernels >= 1 && h.n_kernels <= 8, "bad generator config");
   const int c0 = h.upsample_initial_channel;
   {  // conv_pre: Conv1d(num_mels, c0, 7), no weight norm (models.py:94)
@@ -1037,7 +1049,7 @@ size_t Vocoder::workspace_bytes(int B, int T) const {
   const size_t es = act_bytes(dtype_);
   Workspace ws(nullptr, 0);
   ws.take<char>((size_t)B * T * chan_stride(h_.num_mels) * es);
-  for (int i = 0; i < 5; ++i) ws.take<char>(act_elems(B, T) * es);
+  for (int i = 0; i < act_buffers(); ++i) ws.take<char>(act_elems(B, T) * es);
   return ws.used();
 }
 
@@ -1082,13 +1094,82 @@ void Vocoder::forward_from_norm(const float* mel_norm, const float* mean, const 
     run_t<float>(ln_buf, B, T, wav, ws, s);
 }
 
+int Vocoder::act_buffers() const { return dtype_ == M2S_DT_BF16X3 ? 5 + 3 * CONV_BATCH : 5; }
+
+// Split-fp32 ResBlock1 stage with the resblocks batched (conv_gemm batch launches, grid.z = resblock):
+// X holds a0 = lrelu(x) (the upsampler's epilogue applied it), so no conv re-applies LeakyReLU to its
+// operand fragments per K step; each c2 recovers its residual x from lrelu(x) (slope 0.1 is
+// invertible: x = a > 0 ? a : 10 a) and stores lrelu(xt + x) for the next pair's c1.  Per pair:
+// one launch for the c1 of every resblock, one for the c2 (the last pair's c2 accumulates the MRF
+// sum S = (x_0 + x_1 + ...) / num_kernels in resblock order, models.py:119-125, so it stays serial).
+template <typename T>
+void Vocoder::mrf_stage_batched(int i, const T* X, T* S, T* const (*Bt)[3], int B, int L, hipStream_t s) {
+  const int nk = h_.n_kernels, np = (int)rbs_[i * nk].dil.size();
+  int ord[CONV_BATCH];
+  for (int j = 0; j < nk; ++j) ord[j] = j;
+  std::sort(ord, ord + nk, [&](int x, int y) { return rbs_[i * nk + x].c1[0].kp > rbs_[i * nk + y].c1[0].kp; });
+  auto a_in = [&](int j, int p) -> const T* { return p == 0 ? X : Bt[j][1 + ((p - 1) & 1)]; };  // lrelu(x) of pair p
+  for (int p = 0; p < np; ++p) {
+    ConvArgs cs[CONV_BATCH];
+    double fl = 0.0, by = 0.0, f, b;
+    for (int jj = 0; jj < nk; ++jj) {
+      const int j = ord[jj];
+      const RB& rb = rbs_[i * nk + j];
+      ConvArgs c = conv_args(rb.c1[p]);
+      c.x = a_in(j, p);
+      c.y = Bt[j][0];
+      c.L_in = c.L_out = L;
+      c.M = B * L;
+      c.act = ACT_LRELU;
+      c.act_slope = 0.1f;
+      conv_cost<T>(c, rb.c1[p], &f, &b);
+      fl += f;
+      by += b;
+      cs[jj] = c;
+    }
+    launch_conv_gemm_batch(cs, nk, s, fl, by);
+    fl = by = 0.0;
+    for (int jj = 0; jj < nk; ++jj) {
+      const int j = p + 1 < np ? ord[jj] : jj;
+      const RB& rb = rbs_[i * nk + j];
+      ConvArgs c = conv_args(rb.c2[p]);
+      c.x = Bt[j][0];
+      c.res = a_in(j, p);
+      c.res_unslope = 10.f;
+      c.L_in = c.L_out = L;
+      c.M = B * L;
+      if (p + 1 < np) {  // a_{p+1} = lrelu(xt + x)
+        c.y = Bt[j][1 + (p & 1)];
+        c.act = ACT_LRELU;
+        c.act_slope = 0.1f;
+        c.act_after_res = 1;
+        conv_cost<T>(c, rb.c2[p], &f, &b);
+        fl += f;
+        by += b;
+        cs[jj] = c;
+      } else {  // xs = sum_j resblock_j(x); x = xs / num_kernels
+        c.y = S;
+        c.accum = j == 0 ? 0 : (j == nk - 1 ? 2 : 1);
+        c.accum_div = (float)nk;
+        run_conv<T>(c, rb.c2[p], s);
+      }
+    }
+    if (p + 1 < np) launch_conv_gemm_batch(cs, nk, s, fl, by);
+  }
+}
+
 template <typename T>
 void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& ws, hipStream_t s) {
+  constexpr bool SPL = std::is_same<T, sp_t>::value;
   const size_t n = act_elems(B, Tn) * Elem<T>::R;
   T* X = ws.take<T>(n);
   T* Hb[2] = {ws.take<T>(n), ws.take<T>(n)};
   T* T1 = ws.take<T>(n);
   T* S = ws.take<T>(n);
+  T* Bt[CONV_BATCH][3] = {};  // split: per resblock, c1 output and the pair outputs (ping-pong)
+  if (SPL)
+    for (int j = 0; j < CONV_BATCH; ++j)
+      for (int q = 0; q < 3; ++q) Bt[j][q] = ws.take<T>(n);
   int L = Tn;
   {
     ConvArgs a = conv_args(pre_);
@@ -1102,6 +1183,9 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
   const int nk = h_.n_kernels;
   for (int i = 0; i < h_.n_up; ++i) {
     const PConv& up = ups_[i];
+    const bool fused = (std::is_same<T, bf16_t>::value || SPL) && mrf_fused_ && !rbs_[i * nk].f1.empty();
+    bool batched = SPL && mrf_batch_ && !fused && h_.resblock == 1 && nk <= CONV_BATCH && up.cout >= 32 && up.cout % 32 == 0;
+    for (int j = 0; j < nk; ++j) batched = batched && rbs_[i * nk + j].dil.size() == rbs_[i * nk].dil.size();
     ConvArgs a = conv_args(up);
     a.x = S;
     a.y = X;
@@ -1110,14 +1194,21 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
     a.M = B * L;  // rows per phase
     a.in_xform = IN_LRELU;
     a.in_slope = 0.1f;
+    if (batched) {  // X = lrelu(upsampled x): the MRF convs read it as is (mrf_stage_batched)
+      a.act = ACT_LRELU;
+      a.act_slope = 0.1f;
+    }
     run_conv<T>(a, up, s);
     L *= up.ct_u;
+    if (batched) {
+      mrf_stage_batched<T>(i, X, S, Bt, B, L, s);
+      continue;
+    }
     for (int j = 0; j < nk; ++j) {
       const RB& rb = rbs_[i * nk + j];
       const T* hcur = X;
       const int np = (int)rb.dil.size();
       const int accum = j == 0 ? 0 : (j == nk - 1 ? 2 : 1);
-      constexpr bool SPL = std::is_same<T, sp_t>::value;
       if ((std::is_same<T, bf16_t>::value || SPL) && mrf_fused_ && !rb.f1.empty()) {
         // one launch for the whole resblock + MRF sum (mrf_fused.hip)
         const bf16_t* w1[8];

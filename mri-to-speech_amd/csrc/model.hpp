@@ -150,11 +150,15 @@ class Vocoder {
   void forward_from_norm(const float* mel_norm, const float* mean, const float* std_, int B, int T, float* mel_db,
                          float* mel_log, void* ln_buf, float* wav, Workspace& ws, hipStream_t s);
   size_t act_elems(int B, int T) const;
-  bool mrf_fused_ = true;  // bf16: fused ResBlock1 kernel for C in {32, 64} (env M2S_MRF_FUSED=0 disables)
+  bool mrf_fused_ = true;
+  bool mrf_batch_ = true;  // split: resblocks of a conv_gemm MRF stage batched per launch (env M2S_MRF_BATCH=0 disables)  // bf16: fused ResBlock1 kernel for C in {32, 64} (env M2S_MRF_FUSED=0 disables)
 
  private:
   template <typename T>
   void run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& ws, hipStream_t s);
+  template <typename T>
+  void mrf_stage_batched(int i, const T* X, T* S, T* const (*Bt)[3], int B, int L, hipStream_t s);
+  int act_buffers() const;  // activation buffers of act_elems() each in the workspace
   struct RB {
     int k = 3;
     std::vector<int> dil;
