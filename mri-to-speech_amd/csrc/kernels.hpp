@@ -52,6 +52,12 @@ void launch_ir_pwdw_s2(const void* x, int N, int cs_in, int kp, const void* wpw,
 // Fused HiFi-GAN ResBlock1 (all (c1, c2) pairs of one resblock + the MRF running sum), bf16 for C in
 // {32, 64} or split fp32 (split: x, S as [hi C | lo C] per position) for C = 32:
 // x (B, L, C) -> S (B, L, C) with S = x' (accum 0), S += x' (1), S = (S + x') / div (2).  (mrf_fused.hip)
+// Split-fp32 causal dilated Conv1d with the tile's input rows staged once in LDS (conv1d_halo.hip), for the
+// C = 64 / 128 MRF convs; a[i].w in fragment order [tap][C/32][hi/lo][C/16][64 lanes][8] bf16
+// (conv1d_halo_frag_elems), n batched convs of one shape (grid.z).
+bool conv1d_halo_sp_supported(int C, int cs, int k, int dil);
+size_t conv1d_halo_frag_elems(int C, int k);
+void launch_conv1d_halo_sp(const struct ConvArgs* a, int n, hipStream_t s, double flops, double bytes);
 // w1/w2 are in fragment order: [rb1_frag_taps(C, k, split)][hi/lo if split][C/16][C/32][64 lanes][8] bf16,
 // element (tap t, n16, k32, lane, e) = W[n16*16 + lane%16][k32*32 + 8*(lane/16) + e][t] (zero taps past k).
 bool rb1_fused_supported(int C, int cs, int k, const int* dil, int np, int kp, bool split);

@@ -913,6 +913,7 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
   const int io_dt = dtype == M2S_DT_FP8 ? M2S_DT_BF16 : dtype;
   if (const char* e = std::getenv("M2S_MRF_FUSED")) mrf_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_MRF_BATCH")) mrf_batch_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_MRF_HALO")) mrf_halo_ = std::strcmp(e, "0") != 0;
   M2S_CHECK(h.n_up >= 1 && h.n_up <= 8 && h.n_kernels >= 1 && h.n_kernels <= 8, "bad generator config");
   const int c0 = h.upsample_initial_channel;
   {  // conv_pre: Conv1d(num_mels, c0, 7), no weight norm (models.py:94)
@@ -999,6 +1000,26 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
                   }
         return arena_.add_vec(f);
       };
+      // C = 128 stays on conv_gemm: one workgroup per CU there (96 KB image) measured 2.9 vs 2.3 ms per step
+      bool halo = fsplit && h.resblock == 1 && !frag && co == 64;
+      for (size_t d = 0; d < rb.dil.size(); ++d) halo = halo && conv1d_halo_sp_supported(co, chan_stride(co), kk, rb.dil[d]);
+      auto mk_halo = [&](const std::string& name) {  // fragment order of conv1d_halo.hip
+        std::vector<float> wv = fold_wn(sd, name, {co, co, kk});
+        std::vector<uint16_t> f(conv1d_halo_frag_elems(co, kk));
+        size_t o = 0;
+        for (int t = 0; t < kk; ++t)
+          for (int kc = 0; kc < co / 32; ++kc)
+            for (int half = 0; half < 2; ++half)
+              for (int nt = 0; nt < co / 16; ++nt)
+                for (int ln = 0; ln < 64; ++ln)
+                  for (int e = 0; e < 8; ++e) {
+                    const int n = nt * 16 + (ln & 15), c = kc * 32 + 8 * (ln >> 4) + e;
+                    uint16_t hi, lo;
+                    split_host(wv[((size_t)n * co + c) * kk + t], &hi, &lo);
+                    f[o++] = half ? lo : hi;
+                  }
+        return arena_.add_vec(f);
+      };
       for (size_t d = 0; d < rb.dil.size(); ++d) {
         if (h.resblock == 1) {
           rb.c1.push_back(mk(q + ".convs1." + std::to_string(d), rb.dil[d]));
@@ -1006,6 +1027,10 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
           if (frag) {
             rb.f1_off.push_back(mk_frag(q + ".convs1." + std::to_string(d)));
             rb.f2_off.push_back(mk_frag(q + ".convs2." + std::to_string(d)));
+          }
+          if (halo) {
+            rb.h1_off.push_back(mk_halo(q + ".convs1." + std::to_string(d)));
+            rb.h2_off.push_back(mk_halo(q + ".convs2." + std::to_string(d)));
           }
         } else {
           rb.c1.push_back(mk(q + ".convs." + std::to_string(d), rb.dil[d]));
@@ -1032,6 +1057,8 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
     for (auto& c : rb.c2) c.resolve(arena_);
     for (size_t o : rb.f1_off) rb.f1.push_back(static_cast<const bf16_t*>(arena_.ptr(o)));
     for (size_t o : rb.f2_off) rb.f2.push_back(static_cast<const bf16_t*>(arena_.ptr(o)));
+    for (size_t o : rb.h1_off) rb.h1.push_back(static_cast<const bf16_t*>(arena_.ptr(o)));
+    for (size_t o : rb.h2_off) rb.h2.push_back(static_cast<const bf16_t*>(arena_.ptr(o)));
   }
 }
 
@@ -1109,6 +1136,14 @@ void Vocoder::mrf_stage_batched(int i, const T* X, T* S, T* const (*Bt)[3], int 
   for (int j = 0; j < nk; ++j) ord[j] = j;
   std::sort(ord, ord + nk, [&](int x, int y) { return rbs_[i * nk + x].c1[0].kp > rbs_[i * nk + y].c1[0].kp; });
   auto a_in = [&](int j, int p) -> const T* { return p == 0 ? X : Bt[j][1 + ((p - 1) & 1)]; };  // lrelu(x) of pair p
+  bool halo = mrf_halo_;  // input rows staged once per tile (conv1d_halo.hip) where the stage has the weights for it
+  for (int j = 0; j < nk; ++j) halo = halo && !rbs_[i * nk + j].h1.empty();
+  auto launch_batch = [&](ConvArgs* cs, int n, double fl, double by) {
+    if (halo)
+      launch_conv1d_halo_sp(cs, n, s, fl, by);
+    else
+      launch_conv_gemm_batch(cs, n, s, fl, by);
+  };
   for (int p = 0; p < np; ++p) {
     ConvArgs cs[CONV_BATCH];
     double fl = 0.0, by = 0.0, f, b;
@@ -1116,6 +1151,7 @@ void Vocoder::mrf_stage_batched(int i, const T* X, T* S, T* const (*Bt)[3], int 
       const int j = ord[jj];
       const RB& rb = rbs_[i * nk + j];
       ConvArgs c = conv_args(rb.c1[p]);
+      if (halo) c.w = rb.h1[p];
       c.x = a_in(j, p);
       c.y = Bt[j][0];
       c.L_in = c.L_out = L;
@@ -1127,12 +1163,13 @@ void Vocoder::mrf_stage_batched(int i, const T* X, T* S, T* const (*Bt)[3], int 
       by += b;
       cs[jj] = c;
     }
-    launch_conv_gemm_batch(cs, nk, s, fl, by);
+    launch_batch(cs, nk, fl, by);
     fl = by = 0.0;
     for (int jj = 0; jj < nk; ++jj) {
       const int j = p + 1 < np ? ord[jj] : jj;
       const RB& rb = rbs_[i * nk + j];
       ConvArgs c = conv_args(rb.c2[p]);
+      if (halo) c.w = rb.h2[p];
       c.x = Bt[j][0];
       c.res = a_in(j, p);
       c.res_unslope = 10.f;
@@ -1151,10 +1188,15 @@ void Vocoder::mrf_stage_batched(int i, const T* X, T* S, T* const (*Bt)[3], int 
         c.y = S;
         c.accum = j == 0 ? 0 : (j == nk - 1 ? 2 : 1);
         c.accum_div = (float)nk;
-        run_conv<T>(c, rb.c2[p], s);
+        if (halo) {
+          conv_cost<T>(c, rb.c2[p], &f, &b);
+          launch_conv1d_halo_sp(&c, 1, s, f, b);
+        } else {
+          run_conv<T>(c, rb.c2[p], s);
+        }
       }
     }
-    if (p + 1 < np) launch_conv_gemm_batch(cs, nk, s, fl, by);
+    if (p + 1 < np) launch_batch(cs, nk, fl, by);
   }
 }
 

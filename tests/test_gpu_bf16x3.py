@@ -133,14 +133,19 @@ def test_ir_ws_matches_grid_kernel(rt, ac_state, monkeypatch, hw, n):
 
 @pytest.mark.parametrize("B,T", [(1, 5), (3, 17), (4, 40)])
 def test_vocoder_bf16x3_mrf_batched(rt, monkeypatch, B, T):
-    """The batched split MRF stages (one conv_gemm launch per pair for every resblock, grid.z =
-    resblock; LeakyReLU applied once by the producer and inverted for the residual: model.cpp
-    mrf_stage_batched) against the oracle at the fp32 bar and against the per-conv launches."""
+    """The batched split MRF stages (one launch per pair for every resblock, grid.z = resblock;
+    LeakyReLU applied once by the producer and inverted for the residual: model.cpp
+    mrf_stage_batched) against the oracle at the fp32 bar, the C = 64 / 128 halo-staged convs
+    (conv1d_halo.hip) against the same batches through conv_gemm, and against the per-conv launches.
+    T = 5 gives clips shorter than a 128-row tile at C = 128, T = 40 ragged tiles."""
     sd = synth.synth_generator_state(11, HIFIGAN_H)
     mel = synth.synth_mel_log(B, 64, T, seed=B * 7 + T)
     ref = hifigan.generator({k: torch.from_numpy(v) for k, v in sd.items()}, HIFIGAN_H, torch.from_numpy(mel)).numpy()
     monkeypatch.setenv("M2S_MRF_BATCH", "1")
     bat = rt.VocoderEngine(sd, HIFIGAN_H, dtype="bf16x3", device=DEV).forward(torch.from_numpy(mel).to(DEV))
+    monkeypatch.setenv("M2S_MRF_HALO", "0")  # the same batches through conv_gemm's implicit GEMM
+    gem = rt.VocoderEngine(sd, HIFIGAN_H, dtype="bf16x3", device=DEV).forward(torch.from_numpy(mel).to(DEV))
+    np.testing.assert_allclose(bat.cpu().numpy(), gem.cpu().numpy(), atol=2e-5, rtol=0)
     monkeypatch.setenv("M2S_MRF_BATCH", "0")
     per = rt.VocoderEngine(sd, HIFIGAN_H, dtype="bf16x3", device=DEV).forward(torch.from_numpy(mel).to(DEV))
     bat, per = bat.cpu().numpy(), per.cpu().numpy()
