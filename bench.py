@@ -102,29 +102,38 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
+# M2S_BENCH_FORCE_DIST=1 (under torchrun) takes the RCCL path even at one rank, so the collectives of
+# the N-GPU run (broadcast, all-gather, gather, barrier, all-reduce) can be exercised on a 1-GPU box.
+FORCE_DIST = os.environ.get("M2S_BENCH_FORCE_DIST") == "1"
+
+
 def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or FORCE_DIST:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
 
 
+def multi(world):
+    return world > 1 or FORCE_DIST
+
+
 def timed_loop(step, k: int, world: int, sync, device) -> float:
     """Barrier + sync on both sides of exactly `k` steps; the max of the ranks' wall times."""
-    if world > 1:
+    if multi(world):
         dist.barrier()
     sync()
     t0 = time.perf_counter()
     for _ in range(k):
         step()
-    if world > 1:
+    if multi(world):
         dist.barrier()
     sync()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
-    if world > 1:
+    if multi(world):
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     return float(el.item())
 
@@ -260,12 +269,12 @@ def main():
     B, T, HW = args.clips, args.frames, args.hw
     frames = make_frames(B, T, HW, rank, device)
     out = {}
-    if world > 1:  # C3: clip lengths of every rank (the gather is sized from them)
+    if multi(world):  # C3: clip lengths of every rank (the gather is sized from them)
         all_lens = dp.all_gather_lengths([T] * B, device)
 
     def step(p=None):
         out.update((p or pipe).forward(frames))  # torch.ops.m2s.pipeline_forward on the current stream
-        if world > 1:  # C2: wav + dB mel of every clip to rank 0 over RCCL
+        if multi(world):  # C2: wav + dB mel of every clip to rank 0 over RCCL
             dp.gather_results(out["wav"], all_lens, per_step=HOP)
             dp.gather_results(out["mel_db"], all_lens, per_step=1)
 
@@ -333,7 +342,7 @@ def main():
         result["cpu_baseline"] = cpu_baseline(args, ac_sd, gen_sd, mean, std)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if multi(world):
         dist.barrier()
         dist.destroy_process_group()
     # release the engines' device memory while the HIP runtime is still up

@@ -53,7 +53,7 @@ void launch_ir_pwdw_s2(const void* x, int N, int cs_in, int kp, const void* wpw,
 // {32, 64} or split fp32 (split: x, S as [hi C | lo C] per position) for C = 32:
 // x (B, L, C) -> S (B, L, C) with S = x' (accum 0), S += x' (1), S = (S + x') / div (2).  (mrf_fused.hip)
 // Split-fp32 causal dilated Conv1d with the tile's input rows staged once in LDS (conv1d_halo.hip), for the
-// C = 64 / 128 MRF convs; a[i].w in fragment order [tap][C/32][hi/lo][C/16][64 lanes][8] bf16
+// C = 64 MRF convs; a[i].w in fragment order [tap][C/32][hi/lo][C/16][64 lanes][8] bf16
 // (conv1d_halo_frag_elems), n batched convs of one shape (grid.z).
 bool conv1d_halo_sp_supported(int C, int cs, int k, int dil);
 size_t conv1d_halo_frag_elems(int C, int k);

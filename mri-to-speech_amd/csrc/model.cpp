@@ -1000,8 +1000,7 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
                   }
         return arena_.add_vec(f);
       };
-      // C = 128 stays on conv_gemm: one workgroup per CU there (96 KB image) measured 2.9 vs 2.3 ms per step
-      bool halo = fsplit && h.resblock == 1 && !frag && co == 64;
+      bool halo = fsplit && h.resblock == 1 && !frag;
       for (size_t d = 0; d < rb.dil.size(); ++d) halo = halo && conv1d_halo_sp_supported(co, chan_stride(co), kk, rb.dil[d]);
       auto mk_halo = [&](const std::string& name) {  // fragment order of conv1d_halo.hip
         std::vector<float> wv = fold_wn(sd, name, {co, co, kk});

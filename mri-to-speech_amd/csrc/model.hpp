@@ -151,7 +151,7 @@ class Vocoder {
                          float* mel_log, void* ln_buf, float* wav, Workspace& ws, hipStream_t s);
   size_t act_elems(int B, int T) const;
   bool mrf_fused_ = true;
-  bool mrf_halo_ = true;   // split: C = 64 / 128 MRF convs with once-staged input rows (env M2S_MRF_HALO=0: conv_gemm)
+  bool mrf_halo_ = true;   // split: C = 64 MRF convs with once-staged input rows (env M2S_MRF_HALO=0: conv_gemm)
   bool mrf_batch_ = true;  // split: resblocks of a conv_gemm MRF stage batched per launch (env M2S_MRF_BATCH=0 disables)  // bf16: fused ResBlock1 kernel for C in {32, 64} (env M2S_MRF_FUSED=0 disables)
 
  private:

@@ -36,7 +36,7 @@ def shard_clips(lengths: Sequence[int], world: int) -> List[List[int]]:
 
 def broadcast_state(state: Dict[str, np.ndarray], device: torch.device, src: int = 0) -> Dict[str, np.ndarray]:
     """C1.  Non-src ranks may pass a state with the right keys/shapes (e.g. freshly constructed)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return state
     keys = [k for k in state if np.asarray(state[k]).dtype == np.float32]
     sizes = [int(np.asarray(state[k]).size) for k in keys]
