@@ -254,16 +254,19 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
     bsrc[j] = (blk < B_BLOCKS && n < a.n_pad) ? W + (size_t)n * a.kp * R + q * 8 : nullptr;
   }
 
+  // split SE-gated GEMM: the operand is in the interleaved layout (m2s_common.hpp il_st8: per 32-channel
+  // group [hi 32 | lo 32]); the K step's hi chunk q sits at 64 st + 8 q, its lo chunk 32 further
+  constexpr bool IL = PRE && KIND == KIND_GEMM;
   auto issue = [&](int st, int slot) {
     char* As = smem + slot * SLOT;
     char* Bs = As + R * BM * ROW;
 #pragma unroll
     for (int j = 0; j < A_PER_WAVE; ++j) {
       const bool v = s_tap < 32 && ((rmask[j] >> s_tap) & 1u);
-      const bf16_t* src = X + (unsigned)(rbase[j] + s_off);
+      const bf16_t* src = X + (unsigned)(rbase[j] + (IL ? 2 * s_off - q * 8 : s_off));
       dma16(v ? static_cast<const void*>(src) : static_cast<const void*>(zp), As + (wave * A_PER_WAVE + j) * 16 * ROW);
       if constexpr (SP == 1)
-        dma16(v ? static_cast<const void*>(src + a.cs_in) : static_cast<const void*>(zp),
+        dma16(v ? static_cast<const void*>(src + (IL ? 32 : a.cs_in)) : static_cast<const void*>(zp),
               As + (BM + (wave * A_PER_WAVE + j) * 16) * ROW);
     }
 #pragma unroll

@@ -120,8 +120,8 @@ __global__ void __launch_bounds__(256) dwconv_kernel(const T* __restrict__ x, in
         s[j] += acc[j];
       }
       T* o = y + ((long)n * P + p) * cs + c0;
-      if constexpr (R == 2) {
-        act_st8<T>(y, (long)n * P + p, cs, c0, acc);
+      if constexpr (R == 2) {  // split: the SE GEMM's interleaved operand (m2s_common.hpp il_st8)
+        il_st8(reinterpret_cast<sp_t*>(y), (long)n * P + p, cs, c0, acc);
       } else if constexpr (sizeof(T) == 4) {
         *reinterpret_cast<float4*>(o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
         *reinterpret_cast<float4*>(o + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);

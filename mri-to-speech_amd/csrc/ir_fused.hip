@@ -275,7 +275,7 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
           a[j] = silu(a[j]);
           s[j] += a[j];
         }
-        act_st8<sp_t>(ys, (long)(n0 + g) * PO + p, cs_mid, c, a);
+        il_st8(ys, (long)(n0 + g) * PO + p, cs_mid, c, a);  // the SE GEMM's interleaved operand
       }
     } else if (!SP && g < gi && c < cs_mid) {
       uint32_t w[9][8];

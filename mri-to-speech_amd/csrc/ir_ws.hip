@@ -280,7 +280,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
           a[j] = silu(a[j]);
           s[j] += a[j];
         }
-        act_st4<sp_t>(ys, (long)img * P + (long)(r0 + oy) * W + ox, cs_mid, c0 + 4 * cg, a);
+        il_st4(ys, (long)img * P + (long)(r0 + oy) * W + ox, cs_mid, c0 + 4 * cg, a);  // the SE GEMM's interleaved operand
       }
     }
     TR(f + 1, 5);

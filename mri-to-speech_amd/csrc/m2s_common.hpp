@@ -166,6 +166,29 @@ __device__ __forceinline__ void act_st8(T* x, long p, int cs, int c, const float
   }
 }
 
+// Interleaved split layout ("sp32") of the IR blocks' depthwise output, the operand of the SE-gated
+// conv_pwl GEMM (conv_gemm.hip, IN_SE_SCALE with SP = 1): per position and 32-channel group, [hi 32 | lo 32]
+// bf16 (cs % 32 == 0, same footprint as sp_t), so one 32-channel K step of the GEMM reads one 128-byte line
+// per row instead of two half lines (hi at c, lo at cs + c).
+__device__ __forceinline__ uint16_t* il_addr(sp_t* x, long p, int cs, int c) {
+  return reinterpret_cast<uint16_t*>(x) + p * 2 * cs + (c & ~31) * 2 + (c & 31);
+}
+__device__ __forceinline__ void il_st4(sp_t* x, long p, int cs, int c, const float* v) {  // c % 4 == 0
+  uint16_t* u = il_addr(x, p, cs, c);
+  uint2 hi, lo;
+  split4(v, hi, lo);
+  *reinterpret_cast<uint2*>(u) = hi;
+  *reinterpret_cast<uint2*>(u + 32) = lo;
+}
+__device__ __forceinline__ void il_st8(sp_t* x, long p, int cs, int c, const float* v) {  // c % 8 == 0
+  uint16_t* u = il_addr(x, p, cs, c);
+  uint2 h0, l0, h1, l1;
+  split4(v, h0, l0);
+  split4(v + 4, h1, l1);
+  *reinterpret_cast<uint4*>(u) = make_uint4(h0.x, h0.y, h1.x, h1.y);
+  *reinterpret_cast<uint4*>(u + 32) = make_uint4(l0.x, l0.y, l1.x, l1.y);
+}
+
 // bf16-path activations: one v_exp_f32 + one v_rcp_f32 (1 ulp) instead of an IEEE divide and
 // __expf's denormal-range fix-up (a compare + select + multiply per value); e^-x underflowing to
 // 0 or overflowing to inf gives silu = x or -0 as the exact function does.  These run in every
