@@ -20,14 +20,22 @@ __device__ __forceinline__ float silu_t(float v) {
 // weights are staged once per workgroup in LDS.  SE partial sums per (image, pixel block,
 // channel): each thread flushes its 8 sums to LDS when its image changes; the 8 pixel lanes are
 // then added in a fixed order -> psum[n][pb][cs] (deterministic).
-constexpr int DW_PIX = 256, DW_CB = 64, DW_PL = 256 / (DW_CB / 8);
+constexpr int DW_PIX = 256;
 constexpr int DW_MAXG = DW_PIX / 64;  // images per workgroup at most (grouping needs P >= 64)
+// channels per workgroup: 64, or 32 for split storage, whose lo half starts cs * 2 bytes into the row -
+// with cs = 224 that is 64 B off a 128-byte line, so a 64-channel (128 B) lo read touched two lines
+// (PMC: 1.64x the input bytes fetched); 32 channels = 64 B pieces that never cross a line
+template <typename T>
+constexpr int dw_cb() {
+  return Elem<T>::R == 2 ? 32 : 64;
+}
 
 template <typename T, int S>
 __global__ void __launch_bounds__(256) dwconv_kernel(const T* __restrict__ x, int N, int IH, int IW, int OH, int OW,
                                                      int pad_t, int pad_l, int cs, int G,
                                                      const float* __restrict__ w9, const float* __restrict__ bias,
                                                      T* __restrict__ y, float* __restrict__ psum) {
+  constexpr int DW_CB = dw_cb<T>(), DW_PL = 256 / (DW_CB / 8);
   __shared__ float red[DW_MAXG][DW_PL][DW_CB + 1];
   __shared__ __attribute__((aligned(16))) float wsm[10][DW_CB];  // 9 taps + bias
   const int cg = threadIdx.x % (DW_CB / 8), pl = threadIdx.x / (DW_CB / 8);
@@ -179,7 +187,7 @@ void launch_dwconv(const T* x, int N, int IH, int IW, int OH, int OW, int stride
   M2S_CHECK(cs % 8 == 0, "dwconv: cs % 8");
   M2S_CHECK(stride == 1 || stride == 2, "dwconv: stride");
   const int G = dw_group(OH, OW);
-  const dim3 grid(ceil_div(cs, DW_CB), ceil_div(N, G), dw_pixel_blocks(OH, OW));
+  const dim3 grid(ceil_div(cs, dw_cb<T>()), ceil_div(N, G), dw_pixel_blocks(OH, OW));
   if (stride == 1)
     hipLaunchKernelGGL((dwconv_kernel<T, 1>), grid, dim3(256), 0, s, x, N, IH, IW, OH, OW, pad_t, pad_l, cs, G, w9,
                        bias, y, sums);

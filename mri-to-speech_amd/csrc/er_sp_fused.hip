@@ -15,8 +15,10 @@
 // fragments) and a W_lo stage (against the hi fragments); then conv_pwl's W_hi and W_lo stages.  The
 // haloed input tile ((TH+2) x 18 pixels, hi and lo planes of every 8-channel chunk: planar, so a
 // B-fragment read of 16 consecutive pixels is bank-conflict free) is double-buffered: the next tile's
-// lands while this one computes.  One 512-thread workgroup per CU, persistent over the tiles; wave w
-// computes output rows RPW*w .. RPW*w + RPW - 1 of the 16-wide tile.
+// lands while this one computes.  Persistent workgroups of NW waves; wave w computes output rows
+// RPW*w .. RPW*w + RPW - 1 of the 16-wide tile; one 8-wave workgroup per CU.  (Measured: blocks.1 as two
+// independent 4-wave workgroups per CU on 8-row tiles, so that one's bias + SiLU + re-split phase could
+// overlap the other's MFMAs, ran 2.03-2.09 ms per launch against 2.0 for the 8-wave 16-row form.)
 //
 // Waits are counted `s_waitcnt vmcnt`s over a fixed per-wave issue order: per stage PPW ring pieces,
 // at stage 0 the next tile's 6 halo pieces, after the last stage ST output stores (the table in
@@ -69,24 +71,24 @@ struct ErSpArgs {
 
 // TH: tile rows (tile = TH x 16 output pixels); CSI: input channel stride (32 / 64); NT: mid channels / 16;
 // ON: output channel stride / 16 (the skip needs ON * 16 == CSI)
-template <int TH, int CSI, int NT, int ON>
-__global__ void __launch_bounds__(512, 1) er_sp_kernel(const ErSpArgs a) {
+template <int TH, int CSI, int NT, int ON, int NW>
+__global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) er_sp_kernel(const ErSpArgs a) {
   constexpr int TW = 16, HW = TW + 2, HH = TH + 2, HPIX = HH * HW;
   constexpr int HPB = (HPIX + 63) / 64;          // 64-pixel DMA pieces per (plane, chunk)
   constexpr int HPLANE = HPB * 1024;             // bytes per (plane, chunk)
   constexpr int CH = CSI / 8;                    // 16-byte chunks per pixel and plane
   constexpr int HBUF = 2 * CH * HPLANE;          // hi + lo planes
-  constexpr int HP = 2 * CH * HPB / 8;           // halo pieces per wave
-  static_assert((2 * CH * HPB) % 8 == 0, "halo pieces must divide over 8 waves");
-  constexpr int PPW = (NT + 7) / 8;              // ring pieces per wave per stage
-  constexpr int SLOT = PPW * 8 * 1024;
+  constexpr int HP = 2 * CH * HPB / NW;          // halo pieces per wave
+  static_assert((2 * CH * HPB) % NW == 0, "halo pieces must divide over the waves");
+  constexpr int PPW = (NT + NW - 1) / NW;        // ring pieces per wave per stage
+  constexpr int SLOT = PPW * NW * 1024;
   constexpr int KC = CSI / 32, NCE = 9 * KC * 2;  // conv_exp stages (k-step x plane)
   constexpr int MID = NT * 16, KS = MID / 32, PN = ON * KS;
   constexpr int NPS = (PN + NT - 1) / NT;        // conv_pwl stages per plane
   constexpr int NST = NCE + 2 * NPS;
-  constexpr int RPW = TH / 8;                    // output rows (16-pixel subtiles) per wave
+  constexpr int RPW = TH / NW;                   // output rows (16-pixel subtiles) per wave
   constexpr int ST = RPW * ON * 2;               // output stores per wave per tile
-  static_assert(NT % 2 == 0 && ON * 16 == CSI && TH % 8 == 0, "er_sp shape");
+  static_assert(NT % 2 == 0 && ON * 16 == CSI && TH % NW == 0, "er_sp shape");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ring = smem;
@@ -121,7 +123,7 @@ __global__ void __launch_bounds__(512, 1) er_sp_kernel(const ErSpArgs a) {
     }
   };
 
-  for (int i = tid; i < MID; i += 512) bexp_l[i] = a.bexp[i];
+  for (int i = tid; i < MID; i += 64 * NW) bexp_l[i] = a.bexp[i];
   __syncthreads();  // bexp_l is read through lds_f4 (asm: no conservative vmcnt(0) before it)
   float4 bp[ON];
 #pragma unroll
@@ -274,13 +276,13 @@ __global__ void __launch_bounds__(512, 1) er_sp_kernel(const ErSpArgs a) {
   wait_vm<0>();
 }
 
-template <int TH, int CSI, int NT, int ON>
+template <int TH, int CSI, int NT, int ON, int NW>
 void launch_t(const ErSpArgs& a, const char* name, double flops, double bytes, hipStream_t s) {
-  constexpr int HW = 18, HPB = ((TH + 2) * HW + 63) / 64, CH = CSI / 8, PPW = (NT + 7) / 8;
-  const size_t lds = 3 * (size_t)PPW * 8 * 1024 + 2 * (size_t)(2 * CH * HPB * 1024) + NT * 16 * sizeof(float);
-  M2S_CHECK(lds <= 160 * 1024, "er_sp: LDS budget");
+  constexpr int HW = 18, HPB = ((TH + 2) * HW + 63) / 64, CH = CSI / 8, PPW = (NT + NW - 1) / NW;
+  const size_t lds = 3 * (size_t)PPW * NW * 1024 + 2 * (size_t)(2 * CH * HPB * 1024) + NT * 16 * sizeof(float);
+  M2S_CHECK(lds <= (NW == 4 ? 80 : 160) * 1024, "er_sp: LDS budget");
   static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&er_sp_kernel<TH, CSI, NT, ON>),
+    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&er_sp_kernel<TH, CSI, NT, ON, NW>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     return true;
   }();
@@ -291,9 +293,9 @@ void launch_t(const ErSpArgs& a, const char* name, double flops, double bytes, h
     M2S_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev));
     return v > 0 ? v : 256;
   }();
-  const int grid = std::min(a.N * a.tiles_x * a.tiles_y, cus);
+  const int grid = std::min(a.N * a.tiles_x * a.tiles_y, (NW == 4 ? 2 : 1) * cus);
   ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((er_sp_kernel<TH, CSI, NT, ON>), dim3(grid), dim3(512), lds, s, a);
+  hipLaunchKernelGGL((er_sp_kernel<TH, CSI, NT, ON, NW>), dim3(grid), dim3(64 * NW), lds, s, a);
   M2S_HIP(hipGetLastError());
 }
 
@@ -327,9 +329,9 @@ void launch_er_sp(const void* x, int N, int H, int W, int cs_in, int mid, int cs
   a.tiles_x = W / 16;
   a.tiles_y = H / tile_rows(cs_in);
   if (cs_in == 32)
-    launch_t<16, 32, 8, 2>(a, "er_sp_kernel<16, 32, 8, 2>", flops, bytes, s);
+    launch_t<16, 32, 8, 2, 8>(a, "er_sp_kernel<16, 32, 8, 2, 8>", flops, bytes, s);
   else
-    launch_t<8, 64, 14, 4>(a, "er_sp_kernel<8, 64, 14, 4>", flops, bytes, s);
+    launch_t<8, 64, 14, 4, 8>(a, "er_sp_kernel<8, 64, 14, 4, 8>", flops, bytes, s);
 }
 
 }  // namespace m2s
