@@ -193,18 +193,22 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     f32x4 acc[WS_UMAX];
 #pragma unroll
     for (int k = 0; k < WS_UMAX; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // every unit of a wave has the same 16-channel tile (u & 1 == wave & 1: WS_NP is even), so the
+    // weight fragments are read once per k-step, not once per unit
+    static_assert(WS_NP % 2 == 0, "unit -> channel tile");
+    const int wrow = (wave & 1) * 16 + r16;
+    const int wo = wrow * 64 + ((g ^ swz_f((wrow >> 2) & 3)) << 4);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int Lh = ks * 4 + g, Ll = CPP + ks * 4 + g;
       const int ph = ((Lh & ~15) | ((Lh & 15) ^ hxl)) << 4, pl = ((Ll & ~15) | ((Ll & 15) ^ hxl)) << 4;
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(wb + ks * 4096 + wo);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(wb + ks * 4096 + 2048 + wo);
 #pragma unroll
       for (int k = 0; k < WS_UMAX; ++k) {
         const int u = wave + WS_NP * k;
         if (u < nunit) {
-          const int t = u >> 1, row = (u & 1) * 16 + r16;
-          const int o = row * 64 + ((g ^ swz_f((row >> 2) & 3)) << 4);
-          const bf16x8 ah = *reinterpret_cast<const bf16x8*>(wb + ks * 4096 + o);
-          const bf16x8 al = *reinterpret_cast<const bf16x8*>(wb + ks * 4096 + 2048 + o);
+          const int t = u >> 1;
           const char* xr = xs + (t * 16 + r16) * XP;
           const bf16x8 bh = *reinterpret_cast<const bf16x8*>(xr + ph);
           const bf16x8 bl = *reinterpret_cast<const bf16x8*>(xr + pl);
