@@ -136,8 +136,12 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
   // the stem's weights and biases in LDS (uniform-address reads broadcast): read from global inside
   // the tile loop they were vector loads (the loop's stores of y rule out scalar loads), each tile
   // waiting on ~100 of them
-  __shared__ float sw9[288 + 32];
-  for (int i = tid; i < 320; i += 256) sw9[i] = i < 288 ? a.w9[i] : a.b9[i - 288];
+  // split: tap-major ([k][32 channels]), so the two channels of a packed FMA are adjacent (one ds_read_b64
+  // instead of two reads and the moves that pair them: 569 -> 394 v_mov in this variant); bf16 keeps
+  // [32][9] (tap-major there costs it VGPR spills at its 168-register bound)
+  __shared__ __attribute__((aligned(16))) float sw9[288 + 32];
+  for (int i = tid; i < 320; i += 256)
+    sw9[i] = i < 288 ? (SP ? a.w9[(i % 32) * 9 + i / 32] : a.w9[i]) : a.b9[i - 288];
   const float4 bb0 = *reinterpret_cast<const float4*>(a.b0 + 4 * g);
   const float4 bb1 = *reinterpret_cast<const float4*>(a.b1 + 4 * g);
   __syncthreads();
@@ -167,7 +171,15 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
           float a0 = bj0, a1 = bj1, c0 = bj0, c1 = bj1;
 #pragma unroll
           for (int k = 0; k < 9; ++k) {
-            const float w0 = sw9[(q * 8 + j) * 9 + k], w1 = sw9[(q * 8 + j + 1) * 9 + k];
+            float w0, w1;
+            if constexpr (SP) {
+              const float2 w01 = *reinterpret_cast<const float2*>(&sw9[k * 32 + q * 8 + j]);
+              w0 = w01.x;
+              w1 = w01.y;
+            } else {
+              w0 = sw9[(q * 8 + j) * 9 + k];
+              w1 = sw9[(q * 8 + j + 1) * 9 + k];
+            }
             a0 += w0 * in[0][k];
             a1 += w1 * in[0][k];
             c0 += w0 * in[1][k];
