@@ -76,7 +76,7 @@ __global__ void __launch_bounds__(64 * h1_waves<C>(), 2) conv1d_halo_sp_kernel(c
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* img = smem;
   char* ring = smem + 2 * NPL * H1_PLANE;
-  const ConvArgs& a = ab.a[blockIdx.z];
+  const ConvArgs a = ab.a[blockIdx.z];  // a copy: fields land in SGPRs once, not re-loaded per stage
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);

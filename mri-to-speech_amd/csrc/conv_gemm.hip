@@ -153,7 +153,7 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * ROW + ((ch
 template <int BM, int BN, int MT, int NT, int S, int KIND, int XF, int SP>
 __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 2 : 1)) conv_gemm_kernel(const ConvBatch ab, int n_tiles, int se_imgs) {
   // KIND_CONV1D launches may batch convs of one shape over grid.z (launch_conv_gemm_batch)
-  const ConvArgs& a = ab.a[KIND == KIND_CONV1D ? blockIdx.z : 0];
+  const ConvArgs a = ab.a[KIND == KIND_CONV1D ? blockIdx.z : 0];  // a copy: fields land in SGPRs once, not re-loaded per K step
   constexpr int WN = BN / (NT * 16);
   constexpr int WM = 4 / WN;
   static_assert(WM * WN == 4 && WM * MT * 16 == BM, "bad tile");
