@@ -91,6 +91,30 @@ __global__ void __launch_bounds__(64 * h1_waves<C>(), 2) conv1d_halo_sp_kernel(c
   asm volatile("" : "+s"(zp));
   const uint32_t img0 = (uint32_t)(uintptr_t)img, ring0 = (uint32_t)(uintptr_t)ring;
 
+  // ---- the epilogue's residual and MRF-sum operands, fetched first: read at the end of the tile they
+  // were a second exposed HBM round trip (c2 launches ran ~30 % longer than c1) ----
+  bf16_t* __restrict__ Y = static_cast<bf16_t*>(a.y);
+  const bf16_t* __restrict__ Rs = static_cast<const bf16_t*>(a.res);
+  uint2 prh[2][NTW], prl[2][NTW], pyh[2][NTW], pyl[2][NTW];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int t = t0 + 32 * wr + 16 * i + r16;
+    const size_t orow = ((size_t)clip * L + (t < L ? t : 0)) * a.cs_out * 2;
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+      const int n4 = (ntb + nt) * 16 + 4 * g;
+      prh[i][nt] = prl[i][nt] = pyh[i][nt] = pyl[i][nt] = make_uint2(0u, 0u);
+      if (Rs && t < L) {
+        prh[i][nt] = *reinterpret_cast<const uint2*>(Rs + orow + n4);
+        prl[i][nt] = *reinterpret_cast<const uint2*>(Rs + orow + a.cs_out + n4);
+      }
+      if (a.accum && t < L) {
+        pyh[i][nt] = *reinterpret_cast<const uint2*>(Y + orow + n4);
+        pyl[i][nt] = *reinterpret_cast<const uint2*>(Y + orow + a.cs_out + n4);
+      }
+    }
+  }
+
   // ---- the image: piece (plane p, 64-row block rb) = 64 consecutive rows of one plane ----
   {
     constexpr int PIECES = 2 * NPL * (H1_ROWS / 64);
@@ -155,8 +179,6 @@ __global__ void __launch_bounds__(64 * h1_waves<C>(), 2) conv1d_halo_sp_kernel(c
   wait_vm<0>();  // the zero-page stages issued past the end
 
   // ---- epilogue (conv_gemm.hip's, split): lane = 4 consecutive outputs of one position ----
-  bf16_t* __restrict__ Y = static_cast<bf16_t*>(a.y);
-  const bf16_t* __restrict__ Rs = static_cast<const bf16_t*>(a.res);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int t = t0 + 32 * wr + 16 * i + r16;
@@ -176,8 +198,8 @@ __global__ void __launch_bounds__(64 * h1_waves<C>(), 2) conv1d_halo_sp_kernel(c
       if (!a.act_after_res) apply_act();
       if (Rs) {
         float r[4], rl[4];
-        unpack_bf16x4(*reinterpret_cast<const uint2*>(Rs + orow + n4), r);
-        unpack_bf16x4(*reinterpret_cast<const uint2*>(Rs + orow + a.cs_out + n4), rl);
+        unpack_bf16x4(prh[i][nt], r);
+        unpack_bf16x4(prl[i][nt], rl);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           r[j] += rl[j];
@@ -187,8 +209,8 @@ __global__ void __launch_bounds__(64 * h1_waves<C>(), 2) conv1d_halo_sp_kernel(c
       }
       if (a.accum) {
         float p[4], pl[4];
-        unpack_bf16x4(*reinterpret_cast<const uint2*>(Y + orow + n4), p);
-        unpack_bf16x4(*reinterpret_cast<const uint2*>(Y + orow + a.cs_out + n4), pl);
+        unpack_bf16x4(pyh[i][nt], p);
+        unpack_bf16x4(pyl[i][nt], pl);
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = (p[j] + pl[j]) + v[j];
         if (a.accum == 2) {
