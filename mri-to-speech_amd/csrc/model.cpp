@@ -1129,7 +1129,8 @@ int Vocoder::act_buffers() const { return dtype_ == M2S_DT_BF16X3 ? 5 + 3 * CONV
 // one launch for the c1 of every resblock, one for the c2 (the last pair's c2 accumulates the MRF
 // sum S = (x_0 + x_1 + ...) / num_kernels in resblock order, models.py:119-125, so it stays serial).
 template <typename T>
-void Vocoder::mrf_stage_batched(int i, const T* X, T* S, T* const (*Bt)[3], int B, int L, hipStream_t s) {
+void Vocoder::mrf_stage_batched(int i, const T* X, T* S, T* const (*Bt)[3], int B, int L, bool act_out,
+                                hipStream_t s) {
   const int nk = h_.n_kernels, np = (int)rbs_[i * nk].dil.size();
   int ord[CONV_BATCH];
   for (int j = 0; j < nk; ++j) ord[j] = j;
@@ -1187,6 +1188,11 @@ void Vocoder::mrf_stage_batched(int i, const T* X, T* S, T* const (*Bt)[3], int 
         c.y = S;
         c.accum = j == 0 ? 0 : (j == nk - 1 ? 2 : 1);
         c.accum_div = (float)nk;
+        if (act_out && j == nk - 1) {  // S = lrelu(xs / num_kernels) for the next upsampler
+          c.act = ACT_LRELU;
+          c.act_slope = 0.1f;
+          c.act_after_res = 1;
+        }
         if (halo) {
           conv_cost<T>(c, rb.c2[p], &f, &b);
           launch_conv1d_halo_sp(&c, 1, s, f, b);
@@ -1212,6 +1218,18 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
     for (int j = 0; j < CONV_BATCH; ++j)
       for (int q = 0; q < 3; ++q) Bt[j][q] = ws.take<T>(n);
   int L = Tn;
+  const int nk = h_.n_kernels;
+  auto is_batched = [&](int i) {  // stage i's MRF runs as batched split launches (mrf_stage_batched)
+    const PConv& up = ups_[i];
+    const bool fused = (std::is_same<T, bf16_t>::value || SPL) && mrf_fused_ && !rbs_[i * nk].f1.empty();
+    bool b = SPL && mrf_batch_ && !fused && h_.resblock == 1 && nk <= CONV_BATCH && up.cout >= 32 && up.cout % 32 == 0;
+    for (int j = 0; j < nk; ++j) b = b && rbs_[i * nk + j].dil.size() == rbs_[i * nk].dil.size();
+    return b;
+  };
+  // split: the upsampler's input S may already hold lrelu(x) (slope 0.1, models.py:116-117), written so
+  // by its producer's epilogue (conv_pre, or a batched stage's final MRF accumulation), so the
+  // upsampler does not re-apply LeakyReLU to its operand fragments every K step
+  bool s_act = SPL;
   {
     ConvArgs a = conv_args(pre_);
     a.x = mel_nlc;
@@ -1219,22 +1237,25 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
     a.L_in = L;
     a.L_out = L;
     a.M = B * L;
+    if (s_act) {
+      a.act = ACT_LRELU;
+      a.act_slope = 0.1f;
+    }
     run_conv<T>(a, pre_, s);
   }
-  const int nk = h_.n_kernels;
   for (int i = 0; i < h_.n_up; ++i) {
     const PConv& up = ups_[i];
-    const bool fused = (std::is_same<T, bf16_t>::value || SPL) && mrf_fused_ && !rbs_[i * nk].f1.empty();
-    bool batched = SPL && mrf_batch_ && !fused && h_.resblock == 1 && nk <= CONV_BATCH && up.cout >= 32 && up.cout % 32 == 0;
-    for (int j = 0; j < nk; ++j) batched = batched && rbs_[i * nk + j].dil.size() == rbs_[i * nk].dil.size();
+    const bool batched = is_batched(i);
     ConvArgs a = conv_args(up);
     a.x = S;
     a.y = X;
     a.L_in = L;
     a.L_out = L * up.ct_u;
     a.M = B * L;  // rows per phase
-    a.in_xform = IN_LRELU;
-    a.in_slope = 0.1f;
+    if (!s_act) {
+      a.in_xform = IN_LRELU;
+      a.in_slope = 0.1f;
+    }
     if (batched) {  // X = lrelu(upsampled x): the MRF convs read it as is (mrf_stage_batched)
       a.act = ACT_LRELU;
       a.act_slope = 0.1f;
@@ -1242,9 +1263,13 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
     run_conv<T>(a, up, s);
     L *= up.ct_u;
     if (batched) {
-      mrf_stage_batched<T>(i, X, S, Bt, B, L, s);
+      // the last accumulation stores lrelu(S) when the next consumer is an upsampler (conv_post
+      // takes F.leaky_relu's default slope 0.01 on the raw S)
+      s_act = i + 1 < h_.n_up;
+      mrf_stage_batched<T>(i, X, S, Bt, B, L, s_act, s);
       continue;
     }
+    s_act = false;
     for (int j = 0; j < nk; ++j) {
       const RB& rb = rbs_[i * nk + j];
       const T* hcur = X;

@@ -158,7 +158,7 @@ class Vocoder {
   template <typename T>
   void run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& ws, hipStream_t s);
   template <typename T>
-  void mrf_stage_batched(int i, const T* X, T* S, T* const (*Bt)[3], int B, int L, hipStream_t s);
+  void mrf_stage_batched(int i, const T* X, T* S, T* const (*Bt)[3], int B, int L, bool act_out, hipStream_t s);
   int act_buffers() const;  // activation buffers of act_elems() each in the workspace
   struct RB {
     int k = 3;
