@@ -385,6 +385,25 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
         acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ni], bx[mi], acc[ni][mi], 0, 0, 0);
   };
 
+  // split SE GEMM: the skip operand is fetched before the K loop (the epilogue's residual read was an
+  // exposed HBM round trip at the end of every tile)
+  uint2 pres[PRE ? MT : 1][PRE ? NT : 1][2];
+  if constexpr (PRE) {
+    const bf16_t* __restrict__ R0 = static_cast<const bf16_t*>(a.res);
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) {
+        const int m = m0 + wm * MT * 16 + mi * 16 + r16, n4 = n0 + wn * NT * 16 + ni * 16 + 4 * g;
+        pres[mi][ni][0] = pres[mi][ni][1] = make_uint2(0u, 0u);
+        if (R0 && m < a.M && n4 < a.cs_out) {
+          const size_t orow = (size_t)m * a.cs_out * 2;
+          pres[mi][ni][0] = *reinterpret_cast<const uint2*>(R0 + orow + n4);
+          pres[mi][ni][1] = *reinterpret_cast<const uint2*>(R0 + orow + a.cs_out + n4);
+        }
+      }
+  }
+
   if constexpr (PRE) {
     // Split SE-scaled GEMM: the A tile is scaled IN LDS once per K step by the whole workgroup (each
     // thread BM / 64 16-byte hi/lo chunk pairs) between two barriers, instead of per wave on its
@@ -507,12 +526,20 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
       if (!a.act_after_res) apply_act();
       if (Rs) {
         float r[4];
-        ld4f(Rs + orow + n4, r);
-        if constexpr (SP == 1) {
+        if constexpr (PRE) {
           float rl[4];
-          ld4f(Rs + orow + a.cs_out + n4, rl);
+          unpack_bf16x4(pres[mi][ni][0], r);
+          unpack_bf16x4(pres[mi][ni][1], rl);
 #pragma unroll
           for (int j = 0; j < 4; ++j) r[j] += rl[j];
+        } else {
+          ld4f(Rs + orow + n4, r);
+          if constexpr (SP == 1) {
+            float rl[4];
+            ld4f(Rs + orow + a.cs_out + n4, rl);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) r[j] += rl[j];
+          }
         }
         if (a.res_unslope != 0.f) {  // the residual was stored as lrelu(x): invert it
 #pragma unroll
