@@ -385,10 +385,11 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
         acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ni], bx[mi], acc[ni][mi], 0, 0, 0);
   };
 
-  // split SE GEMM: the skip operand is fetched before the K loop (the epilogue's residual read was an
-  // exposed HBM round trip at the end of every tile)
-  uint2 pres[PRE ? MT : 1][PRE ? NT : 1][2];
-  if constexpr (PRE) {
+  // split SE GEMM and split 1-D convs (the MRF c2's residual): the skip operand is fetched before the
+  // K loop (the epilogue's residual read was an exposed HBM round trip at the end of every tile)
+  constexpr bool PREF = PRE || (SP == 1 && KIND == KIND_CONV1D);
+  uint2 pres[PREF ? MT : 1][PREF ? NT : 1][2];
+  if constexpr (PREF) {
     const bf16_t* __restrict__ R0 = static_cast<const bf16_t*>(a.res);
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi)
@@ -526,7 +527,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
       if (!a.act_after_res) apply_act();
       if (Rs) {
         float r[4];
-        if constexpr (PRE) {
+        if constexpr (PREF) {
           float rl[4];
           unpack_bf16x4(pres[mi][ni][0], r);
           unpack_bf16x4(pres[mi][ni][1], rl);
