@@ -87,7 +87,7 @@ def pmc_traffic(kernel):
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--steps", type=int, default=80)  # ~3.4 s timed at ~42 ms per step
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--clips", type=int, default=64, help="clips per GPU")
     p.add_argument("--frames", type=int, default=30, help="frames per clip")
