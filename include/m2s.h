@@ -20,6 +20,14 @@
  *                          models.py:88-109, run_mri_video_inference.py:89-116
  *   m2s_vocoder_forward    Generator.forward   models.py:113-131
  *   m2s_pipeline_forward   the no_grad section of main()   run_mri_video_inference.py:222-242
+ *   m2s_cam_*              the train-mode backbone forward of compute_gradcam (model.train(): BatchNorm
+ *                          on batch statistics)   scripts/mri_gradcam_formant.py:153-160,221-225
+ *   m2s_bilstm_train_*     BiLSTMSumMerge forward + autograd backward   mri_acoustic_model.py:50-72,
+ *                          scripts/mri_gradcam_formant.py:162-164,247-248
+ *   m2s_linear_*           nn.Linear head forward + backward   mri_acoustic_model.py:103,135,
+ *                          scripts/mri_gradcam_formant.py:165
+ *   m2s_gap_*              GlobalAvgPool / feats.mean((2,3)) forward + backward
+ *                          mri_acoustic_model.py:15-18, scripts/mri_gradcam_formant.py:162
  */
 #ifndef M2S_H_
 #define M2S_H_
@@ -31,7 +39,7 @@
 extern "C" {
 #endif
 
-#define M2S_ABI_VERSION 3
+#define M2S_ABI_VERSION 4
 
 enum m2s_status { M2S_OK = 0, M2S_E_ARG = 1, M2S_E_HIP = 2, M2S_E_STATE = 3, M2S_E_NODEV = 4, M2S_E_INTERNAL = 5 };
 /* compute dtype of the convolution stacks (BiLSTM, head and glue always run in fp32):
@@ -141,6 +149,45 @@ size_t m2s_pipeline_workspace_bytes(const m2s_acoustic* m, const m2s_vocoder* v,
 int m2s_pipeline_forward(m2s_acoustic* m, m2s_vocoder* v, const float* frames, int B, int T, int H, int W,
                          const float* mean, const float* std, float* mel_norm, float* mel_db, float* mel_log,
                          float* wav, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------- Grad-CAM (autograd) path ---- */
+/* compute_gradcam (scripts/mri_gradcam_formant.py:203-279) runs the model in train() and back-
+ * propagates a mel-band power to the last feature map.  These entry points are that path, exact
+ * fp32; every pointer is a device pointer on the current HIP device unless stated otherwise. */
+typedef struct m2s_cam m2s_cam;
+/* Packs the backbone part of an acoustic state dict (cnn.backbone.*) with unfolded BatchNorms:
+ * raw conv weights, BN gamma / beta.  Synchronous. */
+int m2s_cam_create(const m2s_tensor* sd, int n, int device, m2s_cam** out);
+void m2s_cam_destroy(m2s_cam* c);
+/* BatchNorm layers in state-dict order (conv_stem's bn1, then bn1 / bn2 / bn3 of every block) and
+ * their channel counts: m2s_cam_backbone writes [mean C | biased var C] per layer, in that order. */
+int m2s_cam_bn_layers(const m2s_cam* c);
+int m2s_cam_bn_channels(const m2s_cam* c, int layer);
+size_t m2s_cam_workspace_bytes(const m2s_cam* c, int N, int H, int W);
+/* frames (N,H,W) fp32 -> the five timm feature maps with train-mode BatchNorm (statistics of the N
+ * frames), taps[i] (N,C_i,OH_i,OW_i) fp32 (C = 16, 32, 56, 120, 208 at strides 2..32; a NULL entry
+ * is skipped), and every BN layer's batch statistics into bn_stats. */
+int m2s_cam_backbone(m2s_cam* c, const float* frames, int N, int H, int W, float* const* taps, float* bn_stats,
+                     void* ws, size_t ws_bytes, void* stream);
+/* nn.LSTM(C, H, bidirectional, batch_first) + sum merge with saved activations.  w[8] = w_ih, w_hh,
+ * b_ih, b_hh of the forward direction, then of the reverse one (nn.LSTM layouts).  x (B,T,C) ->
+ * y (B,T,H); gates (2,B,T,4H) post-activation i,f,g,o, cells / hid (2,B,T,H) kept for the backward. */
+size_t m2s_bilstm_train_workspace_bytes(int B, int T, int C, int H);
+int m2s_bilstm_train_forward(const float* x, int B, int T, int C, int H, const float* const* w, float* y,
+                             float* gates, float* cells, float* hid, void* ws, size_t ws_bytes, void* stream);
+/* Backward through time: dy (B,T,H) -> dx (B,T,C) and grads[6] = d w_ih, d w_hh, d bias (= d b_ih =
+ * d b_hh) of the forward direction, then of the reverse one; any output may be NULL. */
+int m2s_bilstm_train_backward(const float* x, const float* dy, int B, int T, int C, int H, const float* const* w,
+                              const float* gates, const float* cells, const float* hid, float* dx, float* const* grads,
+                              void* ws, size_t ws_bytes, void* stream);
+/* y (rows,out) = x (rows,in) w^T + b (b may be NULL); backward dx = dy w, dw = dy^T x, db = sum dy. */
+int m2s_linear_forward(const float* x, int rows, int in, int out, const float* w, const float* b, float* y,
+                       void* stream);
+int m2s_linear_backward(const float* dy, const float* x, int rows, int in, int out, const float* w, float* dx,
+                        float* dw, float* db, void* stream);
+/* mean over the last P elements of nc rows (NCHW maps: nc = N*C, P = H*W) and its backward. */
+int m2s_gap_forward(const float* x, int64_t nc, int p, float* y, void* stream);
+int m2s_gap_backward(const float* dy, int64_t nc, int p, float* dx, void* stream);
 
 /* -------------------------------------------------------------------- profiling ---- */
 /* While enabled, every kernel launch is bracketed by HIP events on its own stream. */

@@ -4,6 +4,7 @@
 #include <string>
 
 #include "../../include/m2s.h"
+#include "cam.hpp"
 #include "model.hpp"
 
 struct m2s_acoustic {
@@ -11,6 +12,9 @@ struct m2s_acoustic {
 };
 struct m2s_vocoder {
   m2s::Vocoder impl;
+};
+struct m2s_cam {
+  m2s::CamBackbone impl;
 };
 
 extern "C" int m2s_prof_enable_impl(int on);
@@ -245,6 +249,103 @@ int m2s_pipeline_forward(m2s_acoustic* m, m2s_vocoder* v, const float* frames, i
     if (mel_norm) M2S_HIP(hipMemcpyAsync(mel_norm, mn, rows * nm * sizeof(float), hipMemcpyDeviceToDevice, S(stream)));
     m2s::Workspace vw(rest, rest_bytes);
     v->impl.forward_from_norm(mn, mean, std, B, T, mel_db, mel_log, ln_t, wav, vw, S(stream));
+  });
+}
+
+int m2s_cam_create(const m2s_tensor* sd, int n, int device, m2s_cam** out) {
+  return guarded([&] {
+    M2S_CHECK(out && (sd || n == 0), "null argument");
+    check_device(device);
+    DeviceGuard g(device);
+    *out = new m2s_cam{m2s::CamBackbone(m2s::make_state_dict(sd, n), device)};
+  });
+}
+
+void m2s_cam_destroy(m2s_cam* c) { delete c; }
+
+int m2s_cam_bn_layers(const m2s_cam* c) { return c ? c->impl.bn_layers() : 0; }
+
+int m2s_cam_bn_channels(const m2s_cam* c, int layer) {
+  return c && layer >= 0 && layer < c->impl.bn_layers() ? c->impl.bn_channels(layer) : 0;
+}
+
+size_t m2s_cam_workspace_bytes(const m2s_cam* c, int N, int H, int W) {
+  size_t r = 0;
+  guarded([&] { r = c->impl.workspace_bytes(N, H, W); });
+  return r;
+}
+
+int m2s_cam_backbone(m2s_cam* c, const float* frames, int N, int H, int W, float* const* taps, float* bn_stats,
+                     void* ws, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    M2S_CHECK(c && frames && taps && bn_stats && ws, "null argument");
+    DeviceGuard g(c->impl.device());
+    c->impl.forward(frames, N, H, W, taps, bn_stats, ws, ws_bytes, S(stream));
+  });
+}
+
+size_t m2s_bilstm_train_workspace_bytes(int B, int T, int C, int H) {
+  size_t r = 0;
+  guarded([&] { r = m2s::bilstm_train_workspace_bytes(B, T, C, H); });
+  return r;
+}
+
+int m2s_bilstm_train_forward(const float* x, int B, int T, int C, int H, const float* const* w, float* y,
+                             float* gates, float* cells, float* hid, void* ws, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    M2S_CHECK(x && w && y && gates && cells && hid && ws, "null argument");
+    for (int i = 0; i < 8; ++i) M2S_CHECK(w[i], "null LSTM weight");
+    const float* wih[2] = {w[0], w[4]};
+    const float* whh[2] = {w[1], w[5]};
+    const float* bih[2] = {w[2], w[6]};
+    const float* bhh[2] = {w[3], w[7]};
+    m2s::bilstm_train_forward(x, B, T, C, H, wih, whh, bih, bhh, y, gates, cells, hid, ws, ws_bytes, S(stream));
+  });
+}
+
+int m2s_bilstm_train_backward(const float* x, const float* dy, int B, int T, int C, int H, const float* const* w,
+                              const float* gates, const float* cells, const float* hid, float* dx, float* const* grads,
+                              void* ws, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    M2S_CHECK(x && dy && w && gates && cells && hid && ws, "null argument");
+    const float* wih[2] = {w[0], w[4]};
+    const float* whh[2] = {w[1], w[5]};
+    M2S_CHECK(wih[0] && wih[1] && whh[0] && whh[1], "null LSTM weight");
+    float* dwih[2] = {grads ? grads[0] : nullptr, grads ? grads[3] : nullptr};
+    float* dwhh[2] = {grads ? grads[1] : nullptr, grads ? grads[4] : nullptr};
+    float* db[2] = {grads ? grads[2] : nullptr, grads ? grads[5] : nullptr};
+    m2s::bilstm_train_backward(x, dy, B, T, C, H, wih, whh, gates, cells, hid, dx, dwih, dwhh, db, ws, ws_bytes,
+                               S(stream));
+  });
+}
+
+int m2s_linear_forward(const float* x, int rows, int in, int out, const float* w, const float* b, float* y,
+                       void* stream) {
+  return guarded([&] {
+    M2S_CHECK(x && w && y && rows >= 0 && in > 0 && out > 0, "bad argument");
+    m2s::linear_forward(x, rows, in, out, w, b, y, S(stream));
+  });
+}
+
+int m2s_linear_backward(const float* dy, const float* x, int rows, int in, int out, const float* w, float* dx,
+                        float* dw, float* db, void* stream) {
+  return guarded([&] {
+    M2S_CHECK(dy && x && w && rows >= 0 && in > 0 && out > 0, "bad argument");
+    m2s::linear_backward(dy, x, rows, in, out, w, dx, dw, db, S(stream));
+  });
+}
+
+int m2s_gap_forward(const float* x, int64_t nc, int p, float* y, void* stream) {
+  return guarded([&] {
+    M2S_CHECK(x && y && nc >= 0 && p > 0, "bad argument");
+    m2s::launch_gap_nchw(x, nc, p, y, S(stream));
+  });
+}
+
+int m2s_gap_backward(const float* dy, int64_t nc, int p, float* dx, void* stream) {
+  return guarded([&] {
+    M2S_CHECK(dy && dx && nc >= 0 && p > 0, "bad argument");
+    m2s::launch_gap_nchw_bwd(dy, nc, p, dx, S(stream));
   });
 }
 

@@ -15,12 +15,17 @@
 //   hifigan_forward    Generator.forward                               models.py:113-131
 //   pipeline_forward   the no_grad section of main()                   run_mri_video_inference.py:222-242
 //   preprocess_frames  _preprocess_frame after the host decode         run_mri_video_inference.py:34-54
+//   cam_backbone       backbone(x) in train() (batch-statistics BN)    mri_gradcam_formant.py:153-160,221-225
+//   bilstm_train_*     model.rnn(seq) forward / autograd backward      mri_gradcam_formant.py:162-164,247-248
+//   linear_*           model.head(...) forward / autograd backward     mri_gradcam_formant.py:165
+//   gap_*              feats.mean(dim=(2,3)) forward / backward        mri_gradcam_formant.py:162
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
 #include <tuple>
+#include <vector>
 
 #include "../../include/m2s.h"
 
@@ -173,6 +178,153 @@ at::Tensor preprocess_frames(const at::Tensor& frames) {
   return out;
 }
 
+m2s_cam* Cm(int64_t h) {
+  TORCH_CHECK(h != 0, "null cam handle");
+  return reinterpret_cast<m2s_cam*>(h);
+}
+
+std::vector<const float*> f32_ptrs(const std::vector<at::Tensor>& ts, size_t n, const char* what) {
+  TORCH_CHECK(ts.size() == n, what, ": expected ", n, " tensors");
+  std::vector<const float*> p;
+  for (const auto& t : ts) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), what, ": contiguous fp32 HIP tensors");
+    p.push_back(t.data_ptr<float>());
+  }
+  return p;
+}
+
+// frames (N,H,W) -> five train-mode feature maps (N,C,OH,OW) + BN batch statistics (flat)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> cam_backbone(int64_t h,
+                                                                                                const at::Tensor& frames) {
+  TORCH_CHECK(frames.dim() == 3, "cam_backbone: frames must be (N,H,W)");
+  const Guard g(frames.device());
+  const at::Tensor x = f32_on_device(frames, "frames");
+  const int N = x.size(0), H = x.size(1), W = x.size(2);
+  TORCH_CHECK(N > 0, "cam_backbone: empty batch");
+  static const int ch[5] = {16, 32, 56, 120, 208}, red[5] = {2, 4, 8, 16, 32};
+  std::vector<at::Tensor> taps;
+  std::vector<float*> tp;
+  for (int i = 0; i < 5; ++i) {
+    int oh = H, ow = W;
+    for (int r = 1; r < red[i]; r *= 2) oh = (oh + 1) / 2, ow = (ow + 1) / 2;
+    taps.push_back(at::empty({N, ch[i], oh, ow}, x.options()));
+    tp.push_back(taps.back().data_ptr<float>());
+  }
+  int64_t nst = 0;
+  for (int l = 0; l < m2s_cam_bn_layers(Cm(h)); ++l) nst += 2 * m2s_cam_bn_channels(Cm(h), l);
+  at::Tensor stats = at::empty({nst}, x.options());
+  at::Tensor ws = workspace(m2s_cam_workspace_bytes(Cm(h), N, H, W), x);
+  ok(m2s_cam_backbone(Cm(h), x.data_ptr<float>(), N, H, W, tp.data(), stats.data_ptr<float>(), ws.data_ptr(),
+                      ws.numel(), S()),
+     "cam_backbone");
+  return {taps[0], taps[1], taps[2], taps[3], taps[4], stats};
+}
+
+// x (B,T,C), w = [w_ih, w_hh, b_ih, b_hh] x (fwd, reverse) -> y (B,T,H), gates (2,B,T,4H), cells, hid (2,B,T,H)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bilstm_train_forward(const at::Tensor& x_,
+                                                                                const std::vector<at::Tensor>& w) {
+  TORCH_CHECK(x_.dim() == 3, "bilstm_train_forward: x must be (B,T,C)");
+  const Guard g(x_.device());
+  const at::Tensor x = f32_on_device(x_, "x");
+  std::vector<at::Tensor> wc;
+  for (const auto& t : w) wc.push_back(f32_on_device(t, "lstm weight"));
+  const auto p = f32_ptrs(wc, 8, "bilstm_train_forward");
+  const int B = x.size(0), T = x.size(1), C = x.size(2), Hd = wc[1].size(1);
+  TORCH_CHECK(wc[0].size(0) == 4 * Hd && wc[0].size(1) == C && wc[1].size(0) == 4 * Hd, "bilstm_train_forward: weight shapes");
+  at::Tensor y = at::empty({B, T, Hd}, x.options());
+  at::Tensor gates = at::empty({2, B, T, 4 * Hd}, x.options());
+  at::Tensor cells = at::empty({2, B, T, Hd}, x.options()), hid = at::empty({2, B, T, Hd}, x.options());
+  if (B * T == 0) return {y, gates, cells, hid};
+  at::Tensor ws = workspace(m2s_bilstm_train_workspace_bytes(B, T, C, Hd), x);
+  ok(m2s_bilstm_train_forward(x.data_ptr<float>(), B, T, C, Hd, p.data(), y.data_ptr<float>(), gates.data_ptr<float>(),
+                              cells.data_ptr<float>(), hid.data_ptr<float>(), ws.data_ptr(), ws.numel(), S()),
+     "bilstm_train_forward");
+  return {y, gates, cells, hid};
+}
+
+// -> dx (B,T,C), [d w_ih, d w_hh, d bias] x (fwd, reverse)
+std::tuple<at::Tensor, std::vector<at::Tensor>> bilstm_train_backward(const at::Tensor& dy_, const at::Tensor& x_,
+                                                                      const std::vector<at::Tensor>& w,
+                                                                      const at::Tensor& gates, const at::Tensor& cells,
+                                                                      const at::Tensor& hid) {
+  const Guard g(x_.device());
+  const at::Tensor x = f32_on_device(x_, "x"), dy = f32_on_device(dy_, "dy");
+  std::vector<at::Tensor> wc;
+  for (const auto& t : w) wc.push_back(f32_on_device(t, "lstm weight"));
+  const auto p = f32_ptrs(wc, 8, "bilstm_train_backward");
+  const int B = x.size(0), T = x.size(1), C = x.size(2), Hd = wc[1].size(1);
+  TORCH_CHECK(dy.sizes() == at::IntArrayRef({B, T, Hd}), "bilstm_train_backward: dy shape");
+  const at::Tensor gs = f32_on_device(gates, "gates"), cs = f32_on_device(cells, "cells"), hs = f32_on_device(hid, "hid");
+  at::Tensor dx = at::zeros_like(x);
+  std::vector<at::Tensor> grads;
+  for (int d = 0; d < 2; ++d) {
+    grads.push_back(at::zeros_like(wc[4 * d]));
+    grads.push_back(at::zeros_like(wc[4 * d + 1]));
+    grads.push_back(at::zeros_like(wc[4 * d + 2]));
+  }
+  if (B * T == 0) return {dx, grads};
+  std::vector<float*> gp;
+  for (auto& t : grads) gp.push_back(t.data_ptr<float>());
+  at::Tensor ws = workspace(m2s_bilstm_train_workspace_bytes(B, T, C, Hd), x);
+  ok(m2s_bilstm_train_backward(x.data_ptr<float>(), dy.data_ptr<float>(), B, T, C, Hd, p.data(), gs.data_ptr<float>(),
+                               cs.data_ptr<float>(), hs.data_ptr<float>(), dx.data_ptr<float>(), gp.data(),
+                               ws.data_ptr(), ws.numel(), S()),
+     "bilstm_train_backward");
+  return {dx, grads};
+}
+
+// x (..., in), w (out, in), b (out) -> y (..., out)
+at::Tensor linear_forward(const at::Tensor& x_, const at::Tensor& w_, const c10::optional<at::Tensor>& b_) {
+  const Guard g(x_.device());
+  const at::Tensor x = f32_on_device(x_, "x"), w = f32_on_device(w_, "weight");
+  TORCH_CHECK(w.dim() == 2 && x.size(-1) == w.size(1), "linear_forward: shapes");
+  at::Tensor b;
+  if (b_.has_value()) b = f32_on_device(*b_, "bias");
+  const int in = w.size(1), out = w.size(0), rows = x.numel() / in;
+  auto shape = x.sizes().vec();
+  shape.back() = out;
+  at::Tensor y = at::empty(shape, x.options());
+  if (rows == 0) return y;
+  ok(m2s_linear_forward(x.data_ptr<float>(), rows, in, out, w.data_ptr<float>(), b.defined() ? b.data_ptr<float>() : nullptr,
+                        y.data_ptr<float>(), S()),
+     "linear_forward");
+  return y;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> linear_backward(const at::Tensor& dy_, const at::Tensor& x_,
+                                                               const at::Tensor& w_) {
+  const Guard g(x_.device());
+  const at::Tensor x = f32_on_device(x_, "x"), w = f32_on_device(w_, "weight"), dy = f32_on_device(dy_, "dy");
+  const int in = w.size(1), out = w.size(0), rows = x.numel() / in;
+  TORCH_CHECK(dy.numel() == (int64_t)rows * out, "linear_backward: dy shape");
+  at::Tensor dx = at::empty_like(x), dw = at::zeros_like(w), db = at::zeros({out}, w.options());
+  if (rows == 0) return {dx, dw, db};
+  ok(m2s_linear_backward(dy.data_ptr<float>(), x.data_ptr<float>(), rows, in, out, w.data_ptr<float>(),
+                         dx.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(), S()),
+     "linear_backward");
+  return {dx, dw, db};
+}
+
+// (N,C,H,W) -> (N,C) mean over H,W ; backward (N,C) -> (N,C,H,W)
+at::Tensor gap_forward(const at::Tensor& x_) {
+  TORCH_CHECK(x_.dim() == 4, "gap_forward: (N,C,H,W)");
+  const Guard g(x_.device());
+  const at::Tensor x = f32_on_device(x_, "x");
+  at::Tensor y = at::empty({x.size(0), x.size(1)}, x.options());
+  ok(m2s_gap_forward(x.data_ptr<float>(), x.size(0) * x.size(1), (int)(x.size(2) * x.size(3)), y.data_ptr<float>(), S()),
+     "gap_forward");
+  return y;
+}
+
+at::Tensor gap_backward(const at::Tensor& dy_, int64_t h, int64_t w) {
+  TORCH_CHECK(dy_.dim() == 2, "gap_backward: dy (N,C)");
+  const Guard g(dy_.device());
+  const at::Tensor dy = f32_on_device(dy_, "dy");
+  at::Tensor dx = at::empty({dy.size(0), dy.size(1), h, w}, dy.options());
+  ok(m2s_gap_backward(dy.data_ptr<float>(), dy.numel(), (int)(h * w), dx.data_ptr<float>(), S()), "gap_backward");
+  return dx;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(m2s, m) {
@@ -185,6 +337,14 @@ TORCH_LIBRARY(m2s, m) {
   m.def("pipeline_forward(int acoustic, int vocoder, Tensor frames, Tensor mean, Tensor std, int n_mels, int hop)"
         " -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("preprocess_frames(Tensor frames) -> Tensor");
+  m.def("cam_backbone(int handle, Tensor frames) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("bilstm_train_forward(Tensor x, Tensor[] weights) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("bilstm_train_backward(Tensor dy, Tensor x, Tensor[] weights, Tensor gates, Tensor cells, Tensor hid)"
+        " -> (Tensor, Tensor[])");
+  m.def("linear_forward(Tensor x, Tensor weight, Tensor? bias) -> Tensor");
+  m.def("linear_backward(Tensor dy, Tensor x, Tensor weight) -> (Tensor, Tensor, Tensor)");
+  m.def("gap_forward(Tensor x) -> Tensor");
+  m.def("gap_backward(Tensor dy, int h, int w) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(m2s, CUDA, m) {  // CUDA = the HIP device key of PyTorch-ROCm
@@ -196,4 +356,11 @@ TORCH_LIBRARY_IMPL(m2s, CUDA, m) {  // CUDA = the HIP device key of PyTorch-ROCm
   m.impl("hifigan_forward", &hifigan_forward);
   m.impl("pipeline_forward", &pipeline_forward);
   m.impl("preprocess_frames", &preprocess_frames);
+  m.impl("cam_backbone", &cam_backbone);
+  m.impl("bilstm_train_forward", &bilstm_train_forward);
+  m.impl("bilstm_train_backward", &bilstm_train_backward);
+  m.impl("linear_forward", &linear_forward);
+  m.impl("linear_backward", &linear_backward);
+  m.impl("gap_forward", &gap_forward);
+  m.impl("gap_backward", &gap_backward);
 }

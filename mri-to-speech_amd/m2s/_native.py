@@ -20,6 +20,7 @@ F32, BF16, BF16X3, FP8 = 0, 1, 2, 3
 DTYPES = {"fp32": F32, "float32": F32, "f32": F32, "bf16": BF16, "bfloat16": BF16, "bf16x3": BF16X3,
           "fp8": FP8, "e4m3": FP8}
 ELEM_F32, ELEM_I64 = 0, 1
+ABI_VERSION = 4  # include/m2s.h M2S_ABI_VERSION
 
 
 class M2SError(RuntimeError):
@@ -78,6 +79,19 @@ def lib():
         "m2s_vocoder_forward": (i, [vp, fp, i, i, i, fp, vp, sz, vp]),
         "m2s_pipeline_workspace_bytes": (sz, [vp, vp, i, i, i, i]),
         "m2s_pipeline_forward": (i, [vp, vp, fp, i, i, i, i, fp, fp, fp, fp, fp, fp, vp, sz, vp]),
+        "m2s_cam_create": (i, [C.POINTER(Tensor), i, i, C.POINTER(vp)]),
+        "m2s_cam_destroy": (None, [vp]),
+        "m2s_cam_bn_layers": (i, [vp]),
+        "m2s_cam_bn_channels": (i, [vp, i]),
+        "m2s_cam_workspace_bytes": (sz, [vp, i, i, i]),
+        "m2s_cam_backbone": (i, [vp, fp, i, i, i, vp, fp, vp, sz, vp]),
+        "m2s_bilstm_train_workspace_bytes": (sz, [i, i, i, i]),
+        "m2s_bilstm_train_forward": (i, [fp, i, i, i, i, vp, fp, fp, fp, fp, vp, sz, vp]),
+        "m2s_bilstm_train_backward": (i, [fp, fp, i, i, i, i, vp, fp, fp, fp, fp, vp, vp, sz, vp]),
+        "m2s_linear_forward": (i, [fp, i, i, i, fp, fp, fp, vp]),
+        "m2s_linear_backward": (i, [fp, fp, i, i, i, fp, fp, fp, fp, vp]),
+        "m2s_gap_forward": (i, [fp, C.c_int64, i, fp, vp]),
+        "m2s_gap_backward": (i, [fp, C.c_int64, i, fp, vp]),
         "m2s_prof_enable": (i, [i]),
         "m2s_prof_collect": (i, [C.POINTER(ProfStat), i, C.POINTER(i)]),
     }
@@ -85,7 +99,7 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.m2s_abi_version() != 3:
+    if L.m2s_abi_version() != ABI_VERSION:
         raise M2SError("libm2s ABI version mismatch")
     _lib = L
     return L
@@ -104,7 +118,11 @@ def exported_symbols() -> List[str]:
                         "m2s_acoustic_forward", "m2s_effnet_forward", "m2s_effnet_probe", "m2s_bilstm_summerge",
                         "m2s_mel_glue", "m2s_preprocess_frames", "m2s_vocoder_create", "m2s_vocoder_destroy",
                         "m2s_vocoder_workspace_bytes", "m2s_vocoder_forward", "m2s_pipeline_workspace_bytes",
-                        "m2s_pipeline_forward", "m2s_prof_enable", "m2s_prof_collect")]
+                        "m2s_pipeline_forward", "m2s_cam_create", "m2s_cam_destroy", "m2s_cam_bn_layers",
+                        "m2s_cam_bn_channels", "m2s_cam_workspace_bytes", "m2s_cam_backbone",
+                        "m2s_bilstm_train_workspace_bytes", "m2s_bilstm_train_forward", "m2s_bilstm_train_backward",
+                        "m2s_linear_forward", "m2s_linear_backward", "m2s_gap_forward", "m2s_gap_backward",
+                        "m2s_prof_enable", "m2s_prof_collect")]
 
 
 def tensor_array(state: Dict[str, "np.ndarray"]) -> Tuple[C.Array, list]:

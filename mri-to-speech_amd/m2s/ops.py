@@ -19,12 +19,32 @@ from ._native import M2SError
 
 TORCH_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libm2s_torch.so")
 OPS = ("acoustic_forward", "effnet_forward", "effnet_features", "bilstm_summerge", "mel_glue", "hifigan_forward",
-       "pipeline_forward", "preprocess_frames")
+       "pipeline_forward", "preprocess_frames", "cam_backbone", "bilstm_train_forward", "bilstm_train_backward",
+       "linear_forward", "linear_backward", "gap_forward", "gap_backward")
 
 # timm tf_efficientnetv2_b2 (features_only): stride and output channels of the stem (index 0) and of
 # the 29 blocks that follow (effnet_features' n_blocks = how many of them ran)
 _FEAT_STRIDE = [2] + [1, 1] + [2, 1, 1] + [2, 1, 1] + [2, 1, 1, 1] + [1] * 6 + [2] + [1] * 9
 _FEAT_CH = [32] + [16] * 2 + [32] * 3 + [56] * 3 + [104] * 4 + [120] * 6 + [208] * 10
+
+def cam_bn_layers():
+    """(state-dict prefix, channels, input reduction) of every BatchNorm in cam_backbone's statistics
+    order: conv_stem's bn1, then per block bn1 / bn2 / bn3 (timm key names).  The reduction is the
+    layer's spatial stride w.r.t. the frame (its map is ceil-halved that many times)."""
+    from .config import EFFNET_STEM, effnet_blocks
+    out = [("cnn.backbone.bn1", EFFNET_STEM, 2)]
+    red = 2
+    for b in effnet_blocks():
+        q = f"cnn.backbone.blocks.{b['stage']}.{b['idx']}."
+        r_in, red = red, red * b["stride"]
+        layers = {"cn": [(b["cout"], red)], "er": [(b["mid"], red), (b["cout"], red)],
+                  "ir": [(b["mid"], r_in), (b["mid"], red), (b["cout"], red)]}[b["type"]]
+        out += [(f"{q}bn{i + 1}", c, r) for i, (c, r) in enumerate(layers)]
+    return out
+
+
+# floats of cam_backbone's BatchNorm statistics: [mean C | var C] per layer
+CAM_BN_STATS = 2 * sum(c for _, c, _ in cam_bn_layers())
 
 _loaded = False
 
@@ -91,3 +111,35 @@ def _register_fakes():
     @f("m2s::preprocess_frames")
     def _pre(frames):
         return frames.new_empty(tuple(frames.shape[:3]), dtype=torch.float32)
+
+    @f("m2s::cam_backbone")
+    def _cam(handle, frames):
+        n, h, w = frames.shape
+        maps = [frames.new_empty(feature_shape(n, h, w, k), dtype=torch.float32) for k in (2, 5, 8, 18, 28)]
+        return (*maps, frames.new_empty((CAM_BN_STATS,), dtype=torch.float32))
+
+    @f("m2s::bilstm_train_forward")
+    def _lstm_fwd(x, weights):
+        b, t, hd = x.shape[0], x.shape[1], weights[1].shape[1]
+        return (x.new_empty((b, t, hd)), x.new_empty((2, b, t, 4 * hd)), x.new_empty((2, b, t, hd)),
+                x.new_empty((2, b, t, hd)))
+
+    @f("m2s::bilstm_train_backward")
+    def _lstm_bwd(dy, x, weights, gates, cells, hid):
+        return torch.empty_like(x), [torch.empty_like(weights[i]) for i in (0, 1, 2, 4, 5, 6)]
+
+    @f("m2s::linear_forward")
+    def _lin(x, weight, bias):
+        return x.new_empty((*x.shape[:-1], weight.shape[0]))
+
+    @f("m2s::linear_backward")
+    def _lin_bwd(dy, x, weight):
+        return torch.empty_like(x), torch.empty_like(weight), weight.new_empty((weight.shape[0],))
+
+    @f("m2s::gap_forward")
+    def _gap(x):
+        return x.new_empty((x.shape[0], x.shape[1]))
+
+    @f("m2s::gap_backward")
+    def _gap_bwd(dy, h, w):
+        return dy.new_empty((dy.shape[0], dy.shape[1], h, w))

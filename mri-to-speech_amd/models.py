@@ -14,7 +14,8 @@ The torch sub-modules only hold parameters.  Discriminators and losses (training
 of this path.  ``forward`` dispatches to ``torch.ops.m2s.hifigan_forward``.  Compute dtype:
 ``M2S_DTYPE`` / ``generator.m2s_dtype``: "bf16x3" (default; split fp32 within the fp32 tolerances),
 "fp32" (exact f32 MFMA), "bf16".  The packed engine is rebuilt after ``load_state_dict`` / ``.to()`` /
-a dtype change; ``generator.m2s_refresh()`` after in-place parameter edits.  Weight-norm removal
+a dtype change or a versioned in-place parameter edit; ``generator.m2s_refresh()`` after
+``p.data.copy_()`` edits.  Weight-norm removal
 does not change the folded weights, so it needs no repack.
 """
 from __future__ import annotations
@@ -141,7 +142,10 @@ class Generator(nn.Module):
             raise NotImplementedError("m2s implements generator inference only; call .eval()")
         if device.type != "cuda":
             raise RuntimeError("m2s runs on MI355X (HIP) tensors only; move the generator and mel to 'cuda'")
-        key = (str(device), self.m2s_dtype, self._gen)
+        # in-place edits that bump a tensor's version or move its storage repack too (see the plug-in's
+        # OTNLikeCNNBiLSTM._signature); `p.data.copy_()` edits still need m2s_refresh()
+        key = (str(device), self.m2s_dtype, self._gen, tuple((t.data_ptr(), t._version) for t in self.parameters()),
+               tuple((t.data_ptr(), t._version) for t in self.buffers()))
         if self._eng is None or self._eng_key != key:
             from m2s.runtime import VocoderEngine
             host = {k: v.detach().to("cpu") for k, v in self.state_dict().items()}

@@ -7,15 +7,25 @@ use_reentrant)``.  The returned module has the reference's tree (``cnn.backbone`
 ``rnn.lstm``, ``rnn.dropout``, ``head``) and state-dict keys (timm ``EfficientNetFeatures`` names for
 the backbone), so ``load_state_dict(checkpoint['model_state_dict'], strict=False)`` behaves the same.
 
-``forward`` (eval, HIP tensors) runs the whole CNN -> BiLSTM -> head graph in libm2s through
-``torch.ops.m2s.acoustic_forward``; the torch sub-modules are parameter containers only.
-``model.cnn.backbone(x)`` returns timm's five feature maps (strides 2..32: 16/32/56/120/208 channels) in
-eval, as mri_gradcam_formant.py:155-158 reads them (``torch.ops.m2s.effnet_features``).
-Compute dtype: ``M2S_DTYPE`` env var or ``model.m2s_dtype``: "bf16x3" (default; split fp32, meets the
-fp32 tolerances of the parity tests), "fp32" (exact f32 MFMA products), "bf16" (fast, lower precision).
-The packed engine is rebuilt after ``load_state_dict`` / ``.to()`` or a dtype / chunk change; call
-``model.m2s_refresh()`` after editing parameters in place.
-No CPU fallback: CPU tensors, training mode and autograd raise.
+Inference (eval, HIP tensors): ``forward`` runs the whole CNN -> BiLSTM -> head graph in libm2s
+through ``torch.ops.m2s.acoustic_forward``; ``model.cnn.backbone(x)`` returns timm's five feature maps
+(strides 2..32: 16/32/56/120/208 channels, ``torch.ops.m2s.effnet_features``).
+
+Grad-CAM (scripts/mri_gradcam_formant.py:203-279, m2s/autograd.py): after ``model.train()`` the
+backbone normalises with the batch statistics of the frames it is given and updates the BatchNorm
+running statistics (timm / torch train-mode semantics, ``torch.ops.m2s.cam_backbone``); ``model.rnn``,
+``model.head`` and ``model.cnn.gap`` are autograd functions over HIP kernels (BiLSTM backward through
+time with the weight gradients nn.LSTM would produce, Linear, GAP), so ``feats.grad`` of a
+leaf feature map is filled by ``backward()``.  The backbone itself has no backward: a train-mode
+``model(x)`` with gradients enabled (training the CNN) raises.
+
+Compute dtype of the inference engine: ``M2S_DTYPE`` env var or ``model.m2s_dtype``: "bf16x3"
+(default; split fp32, meets the fp32 tolerances of the parity tests), "fp32" (exact f32 MFMA
+products), "bf16" (fast, lower precision), "fp8".  The Grad-CAM path is exact fp32.
+The packed engines are rebuilt after ``load_state_dict`` / ``.to()``, a dtype / chunk change, or an
+in-place parameter edit that bumps the tensor version (``p.copy_()``, ``p.mul_()``, ``p.data = t``);
+call ``model.m2s_refresh()`` after edits through ``p.data.copy_()``, which torch does not version.
+No CPU fallback: CPU tensors raise.
 """
 from __future__ import annotations
 
@@ -109,13 +119,25 @@ class _EffNetV2B2Features(nn.Module):
             if not (torch.equal(x[:, 0], x[:, 1]) and torch.equal(x[:, 0], x[:, 2])):
                 raise ValueError("m2s folds the grey->RGB repeat into conv_stem; the 3 channels must be equal")
         g = x[:, 0]
-        eng = self._root()._engine(x.device)
+        root = self._root()
+        if root.training:  # timm train mode: BatchNorm on this batch's statistics (Grad-CAM, :223)
+            cam = root._cam_engine(x.device)
+            maps, stats = cam.backbone(g)
+            bns = {n: m for n, m in self.named_modules() if isinstance(m, nn.BatchNorm2d)}
+            bufs = {f"cnn.backbone.{n}.{b}": t for n, m in bns.items() for b, t in m.named_buffers()}
+            momenta = {f"cnn.backbone.{n}": m.momentum for n, m in bns.items() if m.track_running_stats}
+            if momenta:
+                cam.update_running_stats(bufs, stats, g.shape[0], g.shape[1], g.shape[2], momenta)
+            return maps
+        eng = root._engine(x.device)
         return [eng.probe(g, n) for n in _FEATURE_TAPS]
 
 
 class GlobalAvgPool(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return torch.mean(x, dim=(2, 3))
+        """(N,C,H,W) -> (N,C) mean over (H, W) (mri_acoustic_model.py:15-18), HIP forward + backward."""
+        from m2s import autograd
+        return autograd.gap(x)
 
 
 class EffNetV2B2Backbone(nn.Module):
@@ -133,6 +155,8 @@ class EffNetV2B2Backbone(nn.Module):
             if x.size(1) != 1:
                 raise ValueError("m2s expects grey (1-channel) frames")
             x = x[:, 0]
+        if self._root().training:  # batch-statistics BatchNorm, then GAP (autograd from the pooled map on)
+            return self.gap(self.backbone(x[:, None])[-1])
         return self._root()._engine(x.device).effnet(x)
 
 
@@ -144,8 +168,26 @@ class BiLSTMSumMerge(nn.Module):
         self.dropout = nn.Dropout(dropout)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        """(B,T,C) -> (B,T,H) forward + backward hidden states (mri_acoustic_model.py:67-72)."""
-        return self._root()._engine(x.device).bilstm(x)[0]
+        """(B,T,C) -> (B,T,H) forward + backward hidden states, then dropout (mri_acoustic_model.py:67-72).
+
+        With autograd live (training, or gradients enabled for x or the LSTM weights) it runs the
+        saved-activation kernels and their backward through time; otherwise the inference engine."""
+        root = self._root()
+        grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.lstm.parameters()))
+        if root.training or grad:
+            from m2s import autograd
+            y = autograd.bilstm(x, self.lstm)
+        else:
+            y = root._engine(x.device).bilstm(x)[0]
+        return self.dropout(y)
+
+
+class _Head(nn.Linear):
+    """nn.Linear(rnn_hidden, n_mels) (mri_acoustic_model.py:103) on HIP kernels, forward and backward."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from m2s import autograd
+        return autograd.linear(x, self.weight, self.bias)
 
 
 class OTNLikeCNNBiLSTM(nn.Module):
@@ -159,7 +201,7 @@ class OTNLikeCNNBiLSTM(nn.Module):
         self.use_reentrant = use_reentrant
         self.cnn = EffNetV2B2Backbone(pretrained=cnn_pretrained)
         self.rnn = BiLSTMSumMerge(in_dim=self.cnn.out_channels, hidden_size=rnn_hidden, dropout=dropout)
-        self.head = nn.Linear(rnn_hidden, n_mels)
+        self.head = _Head(rnn_hidden, n_mels)
         self.m2s_dtype = os.environ.get("M2S_DTYPE", "bf16x3")
         self.m2s_chunk = int(os.environ.get("M2S_CHUNK", "256"))
         root = lambda: self  # noqa: E731  (children reach the engine without registering a cycle)
@@ -167,6 +209,8 @@ class OTNLikeCNNBiLSTM(nn.Module):
             object.__setattr__(m, "_root", root)
         object.__setattr__(self, "_eng", None)
         object.__setattr__(self, "_eng_key", None)
+        object.__setattr__(self, "_cam", None)
+        object.__setattr__(self, "_cam_key", None)
         object.__setattr__(self, "_gen", 0)
         self.register_load_state_dict_post_hook(lambda mod, keys: mod.m2s_refresh())
 
@@ -180,12 +224,18 @@ class OTNLikeCNNBiLSTM(nn.Module):
         return r
 
     def _signature(self, device):
-        return (str(device), self.m2s_dtype, self.m2s_chunk, self._gen)
+        # (data_ptr, _version) of every parameter and buffer: in-place edits (p.copy_() under no_grad,
+        # EMA updates, vector_to_parameters) bump _version and `p.data = ...` moves data_ptr, so the
+        # packed engine is rebuilt without an explicit m2s_refresh(); edits through `p.data.copy_()`
+        # bypass the version counter and still need m2s_refresh().
+        params = tuple((t.data_ptr(), t._version) for t in self.parameters())
+        bufs = tuple((t.data_ptr(), t._version) for t in self.buffers())
+        return (str(device), self.m2s_dtype, self.m2s_chunk, self._gen, params, bufs)
 
     def _engine(self, device: torch.device):
         if self.training:
-            raise NotImplementedError("m2s implements inference only; call .eval() (training / Grad-CAM "
-                                      "autograd is outside the accelerated path)")
+            raise NotImplementedError("the fused m2s inference engine runs in eval(); in train() the Grad-CAM "
+                                      "path (cnn.backbone / rnn / head) is available, CNN training is not")
         if device.type != "cuda":
             raise RuntimeError("m2s runs on MI355X (HIP) tensors only; move the model and frames to 'cuda'")
         key = self._signature(device)
@@ -199,13 +249,39 @@ class OTNLikeCNNBiLSTM(nn.Module):
             object.__setattr__(self, "_eng_key", key)
         return self._eng
 
+    def _cam_engine(self, device: torch.device):
+        """Train-mode backbone weights (conv weights + BN gamma / beta; running statistics are not
+        packed, so their updates do not repack it)."""
+        if device.type != "cuda":
+            raise RuntimeError("m2s runs on MI355X (HIP) tensors only; move the model and frames to 'cuda'")
+        key = (str(device), self._gen, tuple((p.data_ptr(), p._version) for p in self.cnn.backbone.parameters()))
+        if self._cam is None or self._cam_key != key:
+            from m2s.autograd import CamEngine
+            sd = {k: v.detach().to("cpu") for k, v in self.state_dict().items() if k.startswith("cnn.backbone.")}
+            object.__setattr__(self, "_cam", CamEngine(sd, device))
+            object.__setattr__(self, "_cam_key", key)
+        return self._cam
+
     def _check_grad(self, x):
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
             if x.requires_grad:
                 raise NotImplementedError("m2s forward has no autograd; run under torch.no_grad()")
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        """(B,T,1,H,W) or (B,T,H,W) -> (B,T,n_mels)  (mri_acoustic_model.py:116-136, eval)."""
+        """(B,T,1,H,W) or (B,T,H,W) -> (B,T,n_mels)  (mri_acoustic_model.py:116-136).
+
+        eval: one fused libm2s call.  train (no_grad only): the train-mode backbone (batch-statistics
+        BatchNorm) -> GAP -> BiLSTM -> head, as the reference's training branch computes it (:118-130)."""
+        if self.training:
+            if torch.is_grad_enabled():
+                raise NotImplementedError("m2s has no backward through the CNN backbone: train-mode forward runs "
+                                          "under torch.no_grad() only (Grad-CAM uses cnn.backbone / rnn / head)")
+            if x.device.type != "cuda":
+                raise RuntimeError("m2s runs on MI355X (HIP) tensors only; move the model and frames to 'cuda'")
+            B, T = x.shape[0], x.shape[1]
+            g = x.reshape(B * T, 1, *x.shape[-2:])
+            feats = self.cnn.gap(self.cnn.backbone(g)[-1]).view(B, T, -1)
+            return self.head(self.rnn(feats))
         self._check_grad(x)
         return self._engine(x.device).forward(x)
 

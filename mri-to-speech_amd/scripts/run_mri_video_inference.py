@@ -31,7 +31,6 @@ import json
 import queue
 import sys
 import threading
-import wave
 from pathlib import Path
 
 import numpy as np
@@ -43,16 +42,12 @@ if str(PROJECT_ROOT) not in sys.path:
 
 from env import AttrDict  # noqa: E402
 from models import Generator  # noqa: E402
-from m2s import runtime  # noqa: E402
+from m2s import drivers, runtime  # noqa: E402
 
 try:  # host-side decoders the reference uses; absent from this image
     import cv2
 except ImportError:  # pragma: no cover
     cv2 = None
-try:
-    import soundfile
-except ImportError:  # pragma: no cover
-    soundfile = None
 
 TARGET = (256, 256)
 
@@ -165,82 +160,47 @@ def load_scaler(stats_path: Path):
 
 # ------------------------------------------------------------------------------------------------
 # models
-def _checkpoint(path):
-    return torch.load(path, map_location="cpu", weights_only=True)
-
-
 def build_mri_model(args, device: torch.device):
     """The acoustic model through the plug-in surface: --mri-code-dir (default <ckpt>/../../mri2speech_code)."""
     code_dir = Path(args.mri_code_dir) if getattr(args, "mri_code_dir", None) else \
         Path(args.mri_checkpoint).resolve().parent.parent / "mri2speech_code"
-    if code_dir.exists():
-        sys.path.insert(0, str(code_dir))
-    try:
-        from mri_acoustic_model import build_acoustic_model
-    except ImportError as e:
-        raise ImportError("cannot import mri_acoustic_model; point --mri-code-dir at the directory holding it") from e
-    model = build_acoustic_model(n_mels=args.n_mels, cnn_pretrained=False, rnn_hidden=args.rnn_hidden,
-                                 dropout=args.dropout, use_checkpoint=False, ckpt_segments=2,
-                                 use_reentrant=False).to(device)
-    ck = _checkpoint(args.mri_checkpoint)
-    missing, unexpected = model.load_state_dict(ck.get("model_state_dict", ck), strict=False)
-    for kind, keys in (("missing", missing), ("unexpected", unexpected)):
-        if keys:
-            print(f"[WARN] {len(keys)} {kind} key(s) in the MRI checkpoint: {list(keys)}")
-    model.eval()
-    if getattr(args, "dtype", None):
-        model.m2s_dtype = args.dtype
-    return model
+    return drivers.build_acoustic(args.mri_checkpoint, device, code_dir=code_dir, n_mels=args.n_mels,
+                                  rnn_hidden=args.rnn_hidden, dropout=args.dropout,
+                                  dtype=getattr(args, "dtype", None))
 
 
 def load_hifigan(config_path: Path, checkpoint_path: Path, device: torch.device, dtype=None):
     h = AttrDict(json.loads(Path(config_path).read_text(encoding="utf-8")))
-    gen = Generator(h).to(device)
-    ck = _checkpoint(checkpoint_path)
-    if "generator" not in ck:
-        raise KeyError("HiFi-GAN checkpoint has no 'generator' entry")
-    gen.load_state_dict(ck["generator"])
-    gen.eval()
-    from torch.nn.utils import remove_weight_norm
-    removable = [(remove_weight_norm, m) for m in list(gen.ups) + [gen.conv_post]]
-    removable += [(lambda r: r.remove_weight_norm(), r) for r in gen.resblocks]
-    for fn, mod in removable:  # best effort: layers without weight norm are left as they are
-        try:
-            fn(mod)
-        except (ValueError, AttributeError):
-            pass
-    if dtype:
-        gen.m2s_dtype = dtype
+    gen, _ = drivers.build_generator(h, checkpoint_path, device, dtype)
     return gen, h
 
 
 # ------------------------------------------------------------------------------------------------
 # run
 def run(model, gen, frames: torch.Tensor, mean: np.ndarray, std: np.ndarray):
-    """(T,H,W) device frames -> dict mel_db (T,n_mels), mel_log (T,n_mels), audio (T*hop,) on the host."""
+    """(T,H,W) device frames -> dict mel_db (T,n_mels), mel_log (T,n_mels), audio (T*hop,) on the host.
+
+    On the m2s path the acoustic engine's asynchronous failure report (a BiLSTM barrier timeout
+    poisons the outputs with NaN, include/m2s.h m2s_acoustic_status) is read after the results reach
+    the host, and raises instead of letting NaN outputs be written."""
     dev = frames.device
     if hasattr(model, "_engine") and hasattr(gen, "_engine"):  # both are m2s plug-ins: one device call
-        pipe = runtime.Pipeline(model._engine(dev), gen._engine(dev), mean, std)
+        eng = model._engine(dev)
+        pipe = runtime.Pipeline(eng, gen._engine(dev), mean, std)
         out = pipe.forward(frames[None])
-        db, ln, wav = out["mel_db"][0], out["mel_log"][0], out["wav"][0]
-    else:  # a foreign plug-in: its forward, then the device glue and the generator
-        with torch.no_grad():
-            mn = model(frames_to_tensor(frames))[0]
-            db, ln = runtime.mel_glue(mn, torch.from_numpy(mean), torch.from_numpy(std))
-            wav = gen(ln.t()[None]).reshape(-1)
+        res = {"mel_db": out["mel_db"][0], "mel_log": out["mel_log"][0], "audio": out["wav"][0]}
+        res = {k: v.float().cpu().numpy() for k, v in res.items()}
+        eng.check()
+        return res
+    with torch.no_grad():  # a foreign plug-in: its forward, then the device glue and the generator
+        mn = model(frames_to_tensor(frames))[0]
+        db, ln = runtime.mel_glue(mn, torch.from_numpy(mean), torch.from_numpy(std))
+        wav = gen(ln.t()[None]).reshape(-1)
     return {"mel_db": db.float().cpu().numpy(), "mel_log": ln.float().cpu().numpy(), "audio": wav.float().cpu().numpy()}
 
 
 def write_wav(path: Path, audio: np.ndarray, sr: int):
-    if soundfile is not None:
-        soundfile.write(str(path), audio, sr)  # WAV default subtype PCM_16
-        return
-    pcm = np.clip(np.rint(np.asarray(audio, np.float64) * 32767.0), -32768, 32767).astype("<i2")
-    with wave.open(str(path), "wb") as w:
-        w.setnchannels(1)
-        w.setsampwidth(2)
-        w.setframerate(int(sr))
-        w.writeframes(pcm.tobytes())
+    drivers.write_wav_pcm16(path, audio, sr)
 
 
 def write_outputs(res, out_dir: Path, stem: str, sr: int):

@@ -89,24 +89,31 @@ def _conv(x, w, k, s, groups=1):
     return F.conv2d(_same_pad(x, k, s), w, None, s, 0, 1, groups)
 
 
-def _bn(x, sd, p, act):
+BN_MOMENTUM = 0.1  # torch.nn.BatchNorm2d default, kept by timm's BatchNormAct2d
+
+
+def _bn(x, sd, p, act, train=False):
+    """timm BatchNormAct2d.  eval: running statistics.  train (model.train(), as the reference's
+    Grad-CAM runs it, scripts/mri_gradcam_formant.py:223): the batch's statistics, and the running
+    statistics in ``sd`` updated in place the way torch does (momentum 0.1, unbiased variance)."""
     y = F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"],
-                     sd[p + ".bias"], False, 0.0, BN_EPS)
+                     sd[p + ".bias"], train, BN_MOMENTUM if train else 0.0, BN_EPS)
     return F.silu(y) if act else y
 
 
 def effnet_features(sd: Dict[str, torch.Tensor], x: torch.Tensor, prefix: str = "cnn.backbone.",
-                    taps: list | None = None) -> torch.Tensor:
+                    taps: list | None = None, train: bool = False) -> torch.Tensor:
     """(N,1,H,W) or (N,H,W) or (N,3,H,W) fp32 -> last feature map (N,208,H/32,W/32).
 
-    ``taps``, if given, receives the output of the stem and of every block (29 tensors)."""
+    ``taps``, if given, receives the output of the stem and of every block (29 tensors).
+    ``train``: BatchNorm in training mode (see ``_bn``); ``sd``'s running statistics are updated."""
     if x.dim() == 3:
         x = x.unsqueeze(1)
     if x.size(1) == 1:  # mri_acoustic_model.py:43-44
         x = x.repeat(1, 3, 1, 1)
     p = prefix
     x = _conv(x, sd[p + "conv_stem.weight"], 3, 2)
-    x = _bn(x, sd, p + "bn1", True)
+    x = _bn(x, sd, p + "bn1", True, train)
     if taps is not None:
         taps.append(x)
     for b in block_table():
@@ -114,24 +121,24 @@ def effnet_features(sd: Dict[str, torch.Tensor], x: torch.Tensor, prefix: str = 
         sc = x
         if b["type"] == "cn":
             x = _conv(x, sd[q + "conv.weight"], b["k"], b["stride"])
-            x = _bn(x, sd, q + "bn1", True)
+            x = _bn(x, sd, q + "bn1", True, train)
         elif b["type"] == "er":
             x = _conv(x, sd[q + "conv_exp.weight"], b["k"], b["stride"])
-            x = _bn(x, sd, q + "bn1", True)
+            x = _bn(x, sd, q + "bn1", True, train)
             x = _conv(x, sd[q + "conv_pwl.weight"], 1, 1)
-            x = _bn(x, sd, q + "bn2", False)
+            x = _bn(x, sd, q + "bn2", False, train)
         else:
             x = _conv(x, sd[q + "conv_pw.weight"], 1, 1)
-            x = _bn(x, sd, q + "bn1", True)
+            x = _bn(x, sd, q + "bn1", True, train)
             x = _conv(x, sd[q + "conv_dw.weight"], b["k"], b["stride"], groups=b["mid"])
-            x = _bn(x, sd, q + "bn2", True)
+            x = _bn(x, sd, q + "bn2", True, train)
             s = x.mean((2, 3), keepdim=True)
             s = F.conv2d(s, sd[q + "se.conv_reduce.weight"], sd[q + "se.conv_reduce.bias"])
             s = F.silu(s)
             s = F.conv2d(s, sd[q + "se.conv_expand.weight"], sd[q + "se.conv_expand.bias"])
             x = x * torch.sigmoid(s)
             x = _conv(x, sd[q + "conv_pwl.weight"], 1, 1)
-            x = _bn(x, sd, q + "bn3", False)
+            x = _bn(x, sd, q + "bn3", False, train)
         if b["skip"]:
             x = x + sc
         if taps is not None:

@@ -158,7 +158,8 @@ def test_export_predicted_mels(tmp_path):
 
 
 def test_vocoder_only_callers(tmp_path):
-    """inference_e2e.py and mel_to_audio_synthesis.py drop-ins: (64, T) ln-mel files -> wav."""
+    """inference_e2e.py and mel_to_audio_synthesis.py drop-ins: (64, T) ln-mel files -> wav, files of
+    equal length batched into one generator call, malformed files reported and skipped."""
     from scipy.io import wavfile
     gen_sd = synth.synth_generator_state(8)
     ckdir = tmp_path / "cp"
@@ -168,22 +169,38 @@ def test_vocoder_only_callers(tmp_path):
     (ckdir / "config.json").write_text(json.dumps(cfg))
     mels = tmp_path / "mels"
     mels.mkdir()
-    mel = synth.synth_mel_log(1, 64, 11, seed=2)[0]
-    np.save(mels / "utt_mel.npy", mel)
-    ref = hifigan.generator(_t(gen_sd), HIFIGAN_H, torch.from_numpy(mel)[None])[0, 0].numpy()
+    inputs = {"utt_mel": synth.synth_mel_log(1, 64, 11, seed=2)[0], "b": synth.synth_mel_log(1, 64, 11, seed=4)[0],
+              "c": synth.synth_mel_log(1, 64, 7, seed=5)[0]}
+    for k, v in inputs.items():
+        np.save(mels / f"{k}.npy", v)
+    np.save(mels / "bad.npy", synth.synth_mel_log(2, 64, 5, seed=6))  # a batch of two: e2e refuses, synthesis takes row 0
+    ref = {k: hifigan.generator(_t(gen_sd), HIFIGAN_H, torch.from_numpy(v)[None])[0, 0].numpy() for k, v in inputs.items()}
+    ref["bad"] = hifigan.generator(_t(gen_sd), HIFIGAN_H, torch.from_numpy(synth.synth_mel_log(2, 64, 5, seed=6)[:1]))[0, 0].numpy()
 
     e2e = _load("inference_e2e.py", "m2s_inference_e2e")
     out = e2e.main(["--input_mels_dir", str(mels), "--output_dir", str(tmp_path / "e2e"),
                     "--checkpoint_file", str(ckdir / "g_00000010")])
-    sr, pcm = wavfile.read(out[0])
-    assert sr == 11413 and pcm.dtype == np.int16 and pcm.shape == (11 * 420,)
-    np.testing.assert_allclose(pcm.astype(np.float64), (ref * 32768.0).astype(np.int16), atol=8)
+    assert sorted(os.path.basename(p) for p in out) == ["b_generated_e2e.wav", "c_generated_e2e.wav",
+                                                         "utt_mel_generated_e2e.wav"]
+    for k in inputs:
+        sr, pcm = wavfile.read(tmp_path / "e2e" / f"{k}_generated_e2e.wav")
+        assert sr == 11413 and pcm.dtype == np.int16 and pcm.shape == (inputs[k].shape[1] * 420,)
+        np.testing.assert_allclose(pcm.astype(np.float64), (ref[k] * 32768.0).astype(np.int16), atol=8)
 
     syn = _load("mel_to_audio_synthesis.py", "m2s_mel_to_audio")
     done = syn.main(["--input", str(mels), "--checkpoint_file", str(ckdir / "g_00000010"),
                      "--config", str(ckdir / "config.json"), "--output_dir", str(tmp_path / "syn")])
-    assert done == ["utt"]
+    assert done == ["b", "bad", "c", "utt"]
     stats = json.loads((tmp_path / "syn" / "utt_synthesis_stats.json").read_text())
-    assert stats["audio_shape"] == [11 * 420] and stats["sampling_rate"] == 11413
-    for f in ("utt_from_mel.wav", "mel_synthesis_results.html", "overall_synthesis_stats.json"):
+    assert stats["audio_shape"] == [11 * 420] and stats["sampling_rate"] == 11413 and stats["mel_shape"] == [1, 64, 11]
+    for f in ("utt_from_mel.wav", "utt_input_mel.png", "mel_synthesis_results.html", "overall_synthesis_stats.json"):
         assert (tmp_path / "syn" / f).exists(), f
+    overall = json.loads((tmp_path / "syn" / "overall_synthesis_stats.json").read_text())
+    assert overall["total_files"] == 4 and overall["successful_syntheses"] == 4
+    for k in ("b", "bad", "c"):
+        with open(tmp_path / "syn" / f"{k}_from_mel.wav", "rb") as fh:
+            import wave
+            with wave.open(fh) as w:
+                pcm = np.frombuffer(w.readframes(w.getnframes()), dtype="<i2")
+        want = np.clip(np.rint(ref[k].astype(np.float64) * 32767.0), -32768, 32767)
+        np.testing.assert_allclose(pcm.astype(np.float64), want, atol=8)
