@@ -179,6 +179,7 @@ def test_train_mode_forward_no_grad_and_cnn_backward_refused():
     reference's training-mode graph, mri_acoustic_model.py:116-130); with gradients enabled it refuses
     (no backbone backward) instead of returning gradient-less outputs."""
     m = _model(4).train()
+    m.rnn.dropout.train(False)  # Dropout(0.5) is live in train(): compare the deterministic graph
     fr = synth.synth_frames(1, 4, seed=8)
     x = torch.from_numpy(fr)[:, :, None]
     with torch.no_grad():
