@@ -61,10 +61,15 @@ class CamEngine:
             destroy(h)
             self._h = None
 
+    @property
+    def handle(self) -> int:
+        """The m2s_cam* as the int torch.ops.m2s.cam_backbone takes."""
+        return int(self._h.value)
+
     def backbone(self, frames: torch.Tensor) -> Tuple[List[torch.Tensor], torch.Tensor]:
         """frames (N,H,W) -> ([5 feature maps (N,C,OH,OW)], BN batch stats [mean C | var C] per layer)."""
         _need_hip(frames, "cam backbone")
-        out = self.ops.cam_backbone(int(self._h.value), frames.to(torch.float32).contiguous())
+        out = self.ops.cam_backbone(self.handle, frames.to(torch.float32).contiguous())
         return list(out[:5]), out[5]
 
     def update_running_stats(self, buffers: Dict[str, torch.Tensor], stats: torch.Tensor, n: int, h: int, w: int,

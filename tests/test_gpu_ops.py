@@ -26,6 +26,11 @@ def _frames(b, t, hw=(96, 80)):
 def test_opcheck_every_op(engines):
     ac, voc = engines
     o = ops.load()
+    from m2s.autograd import CamEngine
+    cam = CamEngine({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synth_acoustic_state(2).items()}, DEV)
+    g = torch.Generator().manual_seed(0)
+    lw = [(torch.rand(*s, generator=g) * 0.1 - 0.05).to(DEV)
+          for s in [(2560, 208), (2560, 640), (2560,), (2560,)] * 2]
     mean, std = (torch.from_numpy(a).to(DEV) for a in synth.synth_scaler())
     cases = {
         "acoustic_forward": (ac.handle, _frames(2, 3), 64),
@@ -36,6 +41,16 @@ def test_opcheck_every_op(engines):
         "hifigan_forward": (voc.handle, torch.from_numpy(synth.synth_mel_log(2, 64, 7)).to(DEV), 0, voc.hop),
         "pipeline_forward": (ac.handle, voc.handle, _frames(2, 4), mean, std, 64, voc.hop),
         "preprocess_frames": (torch.randint(0, 256, (3, 40, 36), dtype=torch.uint8, device=DEV),),
+        "cam_backbone": (cam.handle, _frames(1, 3, hw=(64, 48))[0]),
+        "bilstm_train_forward": (torch.randn(2, 3, 208, device=DEV), lw),
+        "bilstm_train_backward": (torch.randn(2, 3, 640, device=DEV), torch.randn(2, 3, 208, device=DEV), lw,
+                                  *o.bilstm_train_forward(torch.randn(2, 3, 208, device=DEV), lw)[1:]),
+        "linear_forward": (torch.randn(2, 3, 640, device=DEV), torch.randn(64, 640, device=DEV),
+                           torch.randn(64, device=DEV)),
+        "linear_backward": (torch.randn(2, 3, 64, device=DEV), torch.randn(2, 3, 640, device=DEV),
+                            torch.randn(64, 640, device=DEV)),
+        "gap_forward": (torch.randn(2, 208, 8, 8, device=DEV),),
+        "gap_backward": (torch.randn(2, 208, device=DEV), 8, 8),
     }
     assert set(cases) == set(ops.OPS)
     for name, args in cases.items():
