@@ -451,12 +451,7 @@ void launch_lstm_train_step(const float* pre, const float* whh, float* gates, fl
                             int H, int step, hipStream_t s) {
   M2S_CHECK(H % 8 == 0 && (32 * H + 32) * sizeof(float) <= 160 * 1024, "lstm_train: hidden size");
   const size_t lds = (32 * (size_t)H + 32) * sizeof(float);
-  static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_train_step_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    return true;
-  }();
-  (void)attr;
+  allow_lds(reinterpret_cast<const void*>(&lstm_train_step_kernel));
   hipLaunchKernelGGL(lstm_train_step_kernel, dim3(H / 8, 2), dim3(256), lds, s, pre, whh, gates, cells, hid, B, T, H,
                      step);
   M2S_HIP(hipGetLastError());
@@ -466,12 +461,7 @@ void launch_lstm_bptt_step(const float* whh_t, const float* dy, const float* gat
                            float* dg, int B, int T, int H, int step, hipStream_t s) {
   M2S_CHECK(H % 8 == 0 && (32 * (size_t)H + 8) * sizeof(float) <= 160 * 1024, "lstm_bptt: hidden size");
   const size_t lds = (32 * (size_t)H + 8) * sizeof(float);
-  static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_bptt_step_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    return true;
-  }();
-  (void)attr;
+  allow_lds(reinterpret_cast<const void*>(&lstm_bptt_step_kernel));
   hipLaunchKernelGGL(lstm_bptt_step_kernel, dim3(H / 8, 2), dim3(256), lds, s, whh_t, dy, gates, cells, dc, dg, B, T, H,
                      step);
   M2S_HIP(hipGetLastError());

@@ -229,12 +229,7 @@ __global__ void __launch_bounds__(64 * h1_waves<C>(), 2) conv1d_halo_sp_kernel(c
 
 template <int C>
 void launch_c(const ConvBatch& b, int n, int B, int L, hipStream_t s, double flops, double bytes) {
-  static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1d_halo_sp_kernel<C>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    return true;
-  }();
-  (void)attr;
+  allow_lds(reinterpret_cast<const void*>(&conv1d_halo_sp_kernel<C>));
   const int tiles = ceil_div(L, H1_BM);
   char name[48];
   snprintf(name, sizeof(name), "conv1d_halo_sp_kernel<%d>", C);
@@ -263,6 +258,8 @@ void launch_conv1d_halo_sp(const ConvArgs* as, int n, hipStream_t s, double flop
                   c.L_out == a.L_out && c.in_xform == IN_NONE && c.pad_left == (c.ntaps - 1) * c.dil &&
                   conv1d_halo_sp_supported(a.cs_in, c.cs_in, c.ntaps, c.dil),
               "conv1d_halo: causal 1-D convs of one shape, C = 64, (k - 1) d <= 64");
+    M2S_CHECK(c.x && c.w && c.bias && c.y && c.y != c.x && c.y != c.res, "conv1d_halo: operand pointers");
+    for (int j = 0; j < i; ++j) M2S_CHECK(as[j].y != c.y, "conv1d_halo: two convs write one output");
     b.a[i] = c;
   }
   const int L = a.L_out, B = a.M / L;

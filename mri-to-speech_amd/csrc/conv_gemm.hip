@@ -600,12 +600,7 @@ void launch_tile(const ConvBatch& b, hipStream_t s, int phases, double flops, do
   // split operands double the slot, so they run two stages
   constexpr int S = SP == 1 ? (BM == 128 && BN == 64 && XF != IN_SE_SCALE ? 3 : 2) : (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
   constexpr int R = SP == 1 ? 2 : 1;
-  static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF, SP>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    return true;
-  }();
-  (void)attr;
+  allow_lds(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF, SP>));
   const int m_tiles = ceil_div(a.M, BM), n_tiles = ceil_div(a.cs_out, BN);
   int se_imgs = 0;
   if (a.in_xform == IN_SE_SCALE) {
@@ -703,6 +698,10 @@ void launch_conv_gemm_batch(const ConvArgs* as, int n, hipStream_t s, double flo
                   c.in_xform == a.in_xform && c.L_in == a.L_in && c.L_out == a.L_out,
               "conv_gemm batch: convs of one shape");
     M2S_CHECK(c.kp % 32 == 0 && c.kp >= c.ntaps * c.cs_in && c.ntaps <= 31, "conv_gemm batch: kp / taps");
+    // every conv of the batch reads its own operands and writes its own output (grid.z = i below):
+    // no null pointer, and no output aliasing an input or another conv's output
+    M2S_CHECK(c.x && c.w && c.bias && c.y && c.y != c.x && c.y != c.res, "conv_gemm batch: operand pointers");
+    for (int j = 0; j < i; ++j) M2S_CHECK(as[j].y != c.y, "conv_gemm batch: two convs write one output");
     M2S_CHECK((double)(c.M / c.L_out) * c.L_in * c.cs_in * 2 < 2147483647.0, "conv_gemm batch: 32-bit offsets");
     b.a[i] = c;
   }

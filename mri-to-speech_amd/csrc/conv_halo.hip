@@ -214,12 +214,7 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(const HaloArgs a) {
 }
 
 int num_cus() {
-  static const int n = [] {
-    int dev = 0, v = 0;
-    M2S_HIP(hipGetDevice(&dev));
-    M2S_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev));
-    return v > 0 ? v : 256;
-  }();
+  const int n = device_cus();
   return n;
 }
 
@@ -250,12 +245,7 @@ bool launch_cfg(const ConvArgs& c, hipStream_t s, double flops, double bytes) {
   const int hblocks = ceil_div(hrows, 16);
   const size_t lds = (size_t)(a.kp / 32) * BN * ROWB + 2 * (size_t)hblocks * 16 * ROWB;
   if (lds > 160 * 1024) return false;
-  static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_halo_kernel<MTW, NTW, WM, WN, KC>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    return true;
-  }();
-  (void)attr;
+  allow_lds(reinterpret_cast<const void*>(&conv_halo_kernel<MTW, NTW, WM, WN, KC>));
   const int per_cu = std::max(1, (int)((160 * 1024) / lds));
   int wgs = std::min(a.m_tiles * a.n_tiles, num_cus() * std::min(per_cu, 4));
   wgs = std::max(a.n_tiles, wgs / a.n_tiles * a.n_tiles);

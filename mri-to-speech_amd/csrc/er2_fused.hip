@@ -240,18 +240,8 @@ void launch_er2_fused(const bf16_t* x, int N, int H, int W, const bf16_t* wst, c
   a.tiles_x = W / E2_TW;
   a.tiles_y = H / E2_TW;
   const size_t lds = E2_SLOTS * E2_STAGE + 2 * E2_BUF + E2_MID * sizeof(float);
-  static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&er2_fused_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024));
-    return true;
-  }();
-  (void)attr;
-  static const int cus = [] {
-    int dev = 0, v = 0;
-    M2S_HIP(hipGetDevice(&dev));
-    M2S_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev));
-    return v > 0 ? v : 256;
-  }();
+  allow_lds(reinterpret_cast<const void*>(&er2_fused_kernel));
+  const int cus = device_cus();
   const int grid = std::min(N * a.tiles_x * a.tiles_y, cus);
   ProfScope ps("er2_fused_kernel", flops, bytes, s);
   hipLaunchKernelGGL(er2_fused_kernel, dim3(grid), dim3(512), lds, s, a);

@@ -196,18 +196,8 @@ void launch_er_fused(const bf16_t* x, int N, int H, int W, const bf16_t* wexp, c
   a.tiles_x = W / ER_TW;
   a.tiles_y = H / ER_TW;
   const size_t lds = ER_WEXP + 2 * ER_BUF;
-  static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&er_fused_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024));
-    return true;
-  }();
-  (void)attr;
-  static const int cus = [] {
-    int dev = 0, v = 0;
-    M2S_HIP(hipGetDevice(&dev));
-    M2S_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev));
-    return v > 0 ? v : 256;
-  }();
+  allow_lds(reinterpret_cast<const void*>(&er_fused_kernel));
+  const int cus = device_cus();
   const int grid = std::min(N * a.tiles_x * a.tiles_y, cus);
   ProfScope ps("er_fused_kernel", flops, bytes, s);
   hipLaunchKernelGGL(er_fused_kernel, dim3(grid), dim3(512), lds, s, a);

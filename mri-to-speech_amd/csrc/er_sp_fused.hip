@@ -281,18 +281,8 @@ void launch_t(const ErSpArgs& a, const char* name, double flops, double bytes, h
   constexpr int HW = 18, HPB = ((TH + 2) * HW + 63) / 64, CH = CSI / 8, PPW = (NT + NW - 1) / NW;
   const size_t lds = 3 * (size_t)PPW * NW * 1024 + 2 * (size_t)(2 * CH * HPB * 1024) + NT * 16 * sizeof(float);
   M2S_CHECK(lds <= (NW == 4 ? 80 : 160) * 1024, "er_sp: LDS budget");
-  static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&er_sp_kernel<TH, CSI, NT, ON, NW>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    return true;
-  }();
-  (void)attr;
-  static const int cus = [] {
-    int dev = 0, v = 0;
-    M2S_HIP(hipGetDevice(&dev));
-    M2S_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev));
-    return v > 0 ? v : 256;
-  }();
+  allow_lds(reinterpret_cast<const void*>(&er_sp_kernel<TH, CSI, NT, ON, NW>));
+  const int cus = device_cus();
   const int grid = std::min(a.N * a.tiles_x * a.tiles_y, (NW == 4 ? 2 : 1) * cus);
   ProfScope ps(name, flops, bytes, s);
   hipLaunchKernelGGL((er_sp_kernel<TH, CSI, NT, ON, NW>), dim3(grid), dim3(64 * NW), lds, s, a);

@@ -293,19 +293,9 @@ template <int CIN, int MID, int CO>
 void launch_cfg_sp(const Es2Args& a, double flops, double bytes, hipStream_t s) {
   constexpr int KS = (9 * CIN + 31) / 32;
   const size_t lds = (size_t)2 * KS * (MID / 16) * 1024 + 2 * (size_t)2 * (CIN / 8) * 2 * ES_PLANE;
-  static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ers2_sp_kernel<CIN, MID, CO>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    return true;
-  }();
-  (void)attr;
+  allow_lds(reinterpret_cast<const void*>(&ers2_sp_kernel<CIN, MID, CO>));
   M2S_CHECK(lds <= 160 * 1024, "ers2_sp: LDS budget");
-  static const int cus = [] {
-    int dev = 0, v = 0;
-    M2S_HIP(hipGetDevice(&dev));
-    M2S_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev));
-    return v > 0 ? v : 256;
-  }();
+  const int cus = device_cus();
   const int grid = std::min(a.N * a.tiles_x * a.tiles_y, cus);
   char name[64];
   snprintf(name, sizeof(name), "ers2_sp_kernel<%d, %d, %d>", CIN, MID, CO);
@@ -318,19 +308,9 @@ template <int CIN, int MID, int CO>
 void launch_cfg(const Es2Args& a, double flops, double bytes, hipStream_t s) {
   constexpr int KS = (9 * CIN + 31) / 32;
   const size_t lds = (size_t)KS * (MID / 16) * 1024 + 2 * (size_t)(CIN / 8) * 2 * ES_PLANE;
-  static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ers2_fused_kernel<CIN, MID, CO>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    return true;
-  }();
-  (void)attr;
+  allow_lds(reinterpret_cast<const void*>(&ers2_fused_kernel<CIN, MID, CO>));
   M2S_CHECK(lds <= 160 * 1024, "ers2_fused: LDS budget");
-  static const int cus = [] {
-    int dev = 0, v = 0;
-    M2S_HIP(hipGetDevice(&dev));
-    M2S_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev));
-    return v > 0 ? v : 256;
-  }();
+  const int cus = device_cus();
   // CIN 16: 60 KB of LDS and < 128 VGPRs, so two workgroups per CU
   const int grid = std::min(a.N * a.tiles_x * a.tiles_y, (CIN == 16 ? 2 : 1) * cus);
   char name[64];

@@ -387,12 +387,7 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
                   hipStream_t s) {
   M2S_CHECK(ir_ws_supported(H, W, cs_in, kp, cs_mid) && N > 0, "ir_ws: unsupported shape");
   const WsLayout L = ws_layout(H, W, cs_in, cs_mid);
-  static int n_cu = [] {
-    int dev = 0, n = 0;
-    M2S_HIP(hipGetDevice(&dev));
-    M2S_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
-    return n > 0 ? n : 256;
-  }();
+  const int n_cu = device_cus();
   const dim3 grid(std::min(N, n_cu));
 #ifdef IRWS_TRACE
   static unsigned long long* tr = [] {
@@ -412,12 +407,7 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
   bf16_t* mb = static_cast<bf16_t*>(se_mean);
 #define M2S_IRWS(W_, KS_)                                                                               \
   if (W == W_ && kp == KS_ * 32) {                                                                      \
-    static bool attr = [] {                                                                             \
-      M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ir_ws_kernel<W_, KS_>),                \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));             \
-      return true;                                                                                      \
-    }();                                                                                                \
-    (void)attr;                                                                                         \
+    allow_lds(reinterpret_cast<const void*>(&ir_ws_kernel<W_, KS_>));                                 \
     ProfScope ps("ir_ws_kernel<" #W_ ", " #KS_ ">", flops, bytes, s);                                   \
     hipLaunchKernelGGL((ir_ws_kernel<W_, KS_>), grid, dim3(64 * (WS_NP + WS_NC)), L.total, s, xb, N, H, cs_mid, wb, \
                        bpw, wdw, bdw, yb, mb, tr);                                                      \

@@ -311,13 +311,7 @@ void launch_lstm_small(const float* pre, const float* whh, float* hs, int B, int
                        unsigned* err_host, hipStream_t s) {
   M2S_CHECK(lstm_small_supported(B, H) && T > 0, "lstm_small: unsupported shape");
   const int grid = 2 * (H / LP_U);
-  static const int resident = [] {
-    int dev = 0, cus = 0, per_cu = 0;
-    M2S_HIP(hipGetDevice(&dev));
-    M2S_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    M2S_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&lstm_small_kernel), 256, 0));
-    return cus * per_cu;
-  }();
+  const int resident = device_resident(reinterpret_cast<const void*>(&lstm_small_kernel), 256, 0);
   M2S_CHECK(grid <= resident, "lstm_small: grid not co-resident on this device");
   // [256 B: error word][granules 2 dir x 2 parity x LS_BMAX x H]: every tag restarts at 0 each call
   M2S_HIP(hipMemsetAsync(sync, 0, lstm_small_sync_bytes(), s));
@@ -337,14 +331,7 @@ void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B
   // workgroups at one per CU; check it against the occupancy query once.  (A plain launch has the
   // same residency as a cooperative one, which only adds this check - and crashes rocprofv3 7.x's
   // kernel tracer at process exit.)
-  static const int resident = [] {
-    int dev = 0, cus = 0, per_cu = 0;
-    M2S_HIP(hipGetDevice(&dev));
-    M2S_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    M2S_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&lstm_persistent_kernel),
-                                                          256, 0));
-    return cus * per_cu;
-  }();
+  const int resident = device_resident(reinterpret_cast<const void*>(&lstm_persistent_kernel), 256, 0);
   M2S_CHECK(grid <= resident, "lstm_persistent: grid not co-resident on this device");
   LstmSync* sp = static_cast<LstmSync*>(sync);
   for (int b0 = 0; b0 < B; b0 += LP_BMAX) {  // c lives in LDS: at most LP_BMAX sequences per launch

@@ -201,6 +201,14 @@ __device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rc
 __device__ __forceinline__ float silu_exact(float x) { return x / (1.0f + expf(-x)); }
 __device__ __forceinline__ float sigmoid_exact(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Per-device launch attributes (device_attr.cpp), cached per (device[, kernel]) so engines on
+// different devices in one process each get their own: the current device's CU count, the 160 KB
+// dynamic-LDS opt-in of `kernel` on the current device, and how many workgroups of `kernel` (block
+// threads, dynamic LDS) the current device holds at once.
+int device_cus();
+void allow_lds(const void* kernel);
+int device_resident(const void* kernel, int block, size_t lds);
+
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 inline int round_up(int a, int b) { return ceil_div(a, b) * b; }
 

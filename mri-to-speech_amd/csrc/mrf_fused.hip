@@ -320,12 +320,7 @@ void launch_cfg(const RbArgs& a, int B, hipStream_t s, double flops, double byte
   constexpr int NPL = C / 8, HR = SP ? 2 : 1;
   const size_t lds = RB_SLOTS * RB_STAGE + 2 * RB_MAXP * C * 4 + 2 * (size_t)HR * NPL * (a.H + TOUT + 16) * 16;
   M2S_CHECK(lds <= 160 * 1024, "rb1_fused: LDS budget");
-  static bool attr = [] {
-    M2S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&rb1_fused_kernel<C, K, TOUT, SP>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    return true;
-  }();
-  (void)attr;
+  allow_lds(reinterpret_cast<const void*>(&rb1_fused_kernel<C, K, TOUT, SP>));
   char name[64];
   snprintf(name, sizeof(name), "rb1_fused_kernel<%d, %d, %d, %d>", C, K, TOUT, SP);
   ProfScope ps(name, flops, bytes, s);

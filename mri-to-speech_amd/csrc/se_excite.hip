@@ -172,12 +172,7 @@ void launch_se_excite(const void* mean, int N, int mid, int cs_mid, const void* 
   // expand tiles split over ES workgroups per 16 images (each recomputes the reduce) while the grid
   // stays within one workgroup per CU: 1920 images were 120 workgroups (0.67 ms per step); ES = 2
   // gives 0.50, and ES = 3 / 4 / 8 (past one per CU) 0.64 / 0.61 / 0.87
-  static const int cus = [] {
-    int dev = 0, v = 0;
-    M2S_HIP(hipGetDevice(&dev));
-    M2S_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev));
-    return v;
-  }();
+  const int cus = device_cus();
   const int nwg = ceil_div(N, SE_IMG), ES = std::max(1, std::min(std::min(cus / nwg, cs_mid / 64), 8));
   hipLaunchKernelGGL(k, dim3(nwg, ES), dim3(256), 0, s, static_cast<const bf16_t*>(mean), N, mid, cs_mid,
                      static_cast<const bf16_t*>(w1), kp1, b1, rd, static_cast<const bf16_t*>(w2), kp2, b2,

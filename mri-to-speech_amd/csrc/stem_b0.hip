@@ -342,12 +342,7 @@ void launch_stem_b0(const float* frames, int N, int H, int W, int OH, int OW, in
   M2S_CHECK((double)N * a.tiles_x * a.tiles_y < 2147483647.0, "stem_b0: grid");
   // persistent grid: the resident workgroups of the device (two per CU split, three bf16), a multiple
   // of 8 (one equal share per XCD); small inputs take fewer
-  static const int cus = [] {
-    int dev = 0, v = 0;
-    M2S_HIP(hipGetDevice(&dev));
-    M2S_HIP(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev));
-    return v;
-  }();
+  const int cus = device_cus();
   const int total = N * a.tiles_x * a.tiles_y;
   a.per_xcd = ceil_div(total, 8);
   const int per_cu = split ? 2 : 3;
