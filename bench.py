@@ -70,18 +70,39 @@ def kernel_arith(name: str, dtype: str) -> str:
     return dtype
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest profiles/*pmc_traffic.json (rocprofv3
-    FETCH_SIZE x2 + WRITE_SIZE passes over the same workload, tools/gpu_pmc.sh + tools/pmc_traffic.py)."""
+def source_sha() -> str:
+    """sha256 (16 hex digits) of the HIP / C++ sources and the C ABI header: the identity of the
+    kernels a measurement was taken on (the GPU box gets the tree without .git)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as fh:
-        k = json.load(fh)["kernels"].get(kernel)
-    if not k:
-        return None, None
-    return round(k["hbm_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(REPO, "mri-to-speech_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(REPO, "mri-to-speech_amd", "csrc", "*.cpp")) +
+                   glob.glob(os.path.join(REPO, "mri-to-speech_amd", "csrc", "*.hpp")) +
+                   [os.path.join(REPO, "include", "m2s.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the profiles/*pmc_traffic.json record measured on THIS
+    tree (its meta.src_sha equals source_sha(); rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes,
+    tools/gpu_evidence.sh + tools/evidence.py).  No record of this tree: no traffic figure."""
+    import glob
+    sha = source_sha()
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic.json")), reverse=True):
+        with open(f) as fh:
+            rec = json.load(fh)
+        if rec.get("meta", {}).get("src_sha") != sha:
+            continue
+        k = rec["kernels"].get(kernel)
+        if not k:
+            return None, os.path.relpath(f, REPO), sha
+        return round(k["hbm_bytes_per_launch"]), os.path.relpath(f, REPO), sha
+    return None, None, sha
 
 
 def parse(argv=None):
@@ -226,7 +247,7 @@ def roofline(stats, dtype, steps, fps, frames_per_step):
     mm = [s for s in stats if s["name"].startswith(MFMA_KERNELS)]
     mm_ms, mm_fl = sum(s["ms"] for s in mm), sum(s["flops"] for s in mm)
     flop_per_frame = sum(s["flops"] for s in stats) / (steps * frames_per_step)
-    traffic, tsrc = pmc_traffic(dom["name"])
+    traffic, tsrc, sha = pmc_traffic(dom["name"])
     r = {
         "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 2), "unit": unit,
         "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -240,8 +261,8 @@ def roofline(stats, dtype, steps, fps, frames_per_step):
         "e2e_tflops": round(flop_per_frame * fps / 1e12, 2),
         "e2e_frac_of_peak": round(flop_per_frame * fps / 1e12 / PEAK_TFLOPS[dtype], 4),
     }
-    if tsrc:
-        r["traffic_source"] = tsrc
+    r["traffic_source"] = tsrc or f"no PMC record of source {sha} in profiles/ (tools/gpu_evidence.sh)"
+    r["src_sha"] = sha
     return r
 
 
