@@ -146,6 +146,12 @@ size_t lstm_small_sync_bytes();
 void launch_lstm_small(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,
                        unsigned* err_host, hipStream_t s);
 constexpr unsigned LSTM_SPIN_MAX = 1u << 24;
+// 4 < B <= 64: the same granule exchange with 512-thread workgroups, sequences in chunks of 16 whose
+// sweep overlaps the previous chunk's dot products (lstm_persistent.hip).  `sync` = lstm_mid_sync_bytes().
+bool lstm_mid_supported(int B, int H);
+size_t lstm_mid_sync_bytes();
+void launch_lstm_mid(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,
+                     unsigned* err_host, hipStream_t s);
 void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync,
                             unsigned spin_max, unsigned* err_host, hipStream_t s);
 

@@ -299,7 +299,189 @@ __global__ void __launch_bounds__(256, 1) lstm_small_kernel(const float* __restr
   }
 }
 
+// ---- medium batches (LS_BMAX < B <= LM_BMAX: configs[4]'s 8 x 1000 frames, the bench's 64 clips) -------
+// The granule exchange of lstm_small_kernel, scaled to B sequences:
+// * 512 threads (two waves per SIMD: one wave alone issues v_fma_f32 every 4 cycles, two every 2);
+//   lane (wave w, k half kk, gate row l32) keeps 40 W_hh values (k = 80 w + 40 kk ..) in VGPRs;
+// * sequences in chunks of LM_CH: the chunk's h_{t-1} granules (LM_CH x 640 x 8 B) are swept into a
+//   double-buffered LDS image, and the sweep of chunk c + 1 is ISSUED (LM_G independent sc1 loads per
+//   thread, tags checked afterwards) before the dot products of chunk c, so the exchange latency runs
+//   under the arithmetic;
+// * per chunk the 16 K-slice partials of every (gate row, sequence) are summed in LDS in a fixed order and
+//   128 threads apply the cell update and publish h_t (tag = step + 1), as lstm_small_kernel does.
+// Double buffering by step parity stays safe per chunk: a workgroup can publish chunk c of h_{t+1} only
+// after every workgroup published chunk c of h_t, i.e. after each of them finished reading chunk c of
+// h_{t-1}.  Exact fp32 products; the partial-sum order is fixed.
+constexpr int LM_BMAX = 64, LM_CH = 8, LM_THREADS = 512;
+constexpr int LM_KL = LP_H / 16;                    // k per lane (16 slices of 40)
+constexpr int LM_G = LM_CH * LP_H / LM_THREADS;     // granules per thread per chunk (20)
+
+__global__ void __launch_bounds__(LM_THREADS, 1) lstm_mid_kernel(const float* __restrict__ pre,
+                                                                 const float* __restrict__ whh, float* hs, int B,
+                                                                 int T, unsigned long long* gran, unsigned* err,
+                                                                 unsigned spin_max, unsigned* err_host) {
+  __shared__ __attribute__((aligned(16))) float hsh[2][LM_CH][LP_H];   // h_{t-1} of two chunks
+  __shared__ __attribute__((aligned(16))) float red[16][32][LM_CH];    // [K slice][gate row][sequence]
+  __shared__ float cst[LP_U][LM_BMAX];
+  __shared__ int abort_flag;
+  const int H = LP_H;
+  const int dir = blockIdx.x / (H / LP_U), ug = blockIdx.x - dir * (H / LP_U);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kk = lane >> 5, l32 = lane & 31;
+  const int slice = wave * 2 + kk, kbase = slice * LM_KL;
+  float* hsd = hs + (size_t)dir * B * T * H;
+  unsigned long long* gd = gran + (size_t)dir * 2 * LM_BMAX * H;
+  const int nch = (B + LM_CH - 1) / LM_CH;
+
+  float wa[LM_KL];
+  {
+    const int r = l32, g = r / LP_U, u = ug * LP_U + (r % LP_U);
+    const float* wr = whh + ((size_t)dir * 4 * H + (size_t)g * H + u) * H + kbase;
+#pragma unroll
+    for (int s = 0; s < LM_KL; s += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(wr + s);
+      wa[s] = v.x;
+      wa[s + 1] = v.y;
+      wa[s + 2] = v.z;
+      wa[s + 3] = v.w;
+    }
+  }
+  for (int i = tid; i < LP_U * LM_BMAX; i += LM_THREADS) (&cst[0][0])[i] = 0.f;
+  if (tid == 0) abort_flag = 0;
+  __syncthreads();
+
+  unsigned long long g[LM_G];
+  // issue the sweep loads of chunk c of h_{step-1} (relaxed agent loads: sc1, served by L2)
+  auto issue = [&](int step, int c) {
+    const unsigned long long* src = gd + (size_t)((step - 1) & 1) * LM_BMAX * H + (size_t)c * LM_CH * H;
+    const int n = min(LM_CH, B - c * LM_CH) * H;
+#pragma unroll
+    for (int j = 0; j < LM_G; ++j) {
+      const int i = tid + j * LM_THREADS;
+      g[j] = i < n ? __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    }
+  };
+  // tags checked, late granules re-polled (bounded), values -> LDS buffer `buf`; false on timeout
+  auto land = [&](int step, int c, int buf) -> bool {
+    const unsigned long long* src = gd + (size_t)((step - 1) & 1) * LM_BMAX * H + (size_t)c * LM_CH * H;
+    const int n = min(LM_CH, B - c * LM_CH) * H;
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < LM_G; ++j) {
+      const int i = tid + j * LM_THREADS;
+      if (i >= n) continue;
+      unsigned long long x = g[j];
+      unsigned spins = 0;
+      while (ok && (unsigned)(x >> 32) != (unsigned)step) {
+        __builtin_amdgcn_s_sleep(1);
+        x = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (++spins > spin_max || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          abort_flag = 1;
+          ok = false;
+        }
+      }
+      hsh[buf][i / H][i % H] = __uint_as_float((unsigned)x);
+    }
+    return ok;
+  };
+
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? step : T - 1 - step;
+    if (step > 0) {
+      issue(step, 0);
+      land(step, 0, 0);
+    }
+    for (int c = 0; c < nch; ++c) {
+      const int nb = min(LM_CH, B - c * LM_CH);
+      // cell-update threads fetch their gate pre-activations early (tid = u + 8 b)
+      float pr4[4] = {0.f, 0.f, 0.f, 0.f};
+      const int cu = tid % LP_U, cb = tid / LP_U;
+      if (tid < LP_U * nb) {
+        const float* pr = pre + ((size_t)(c * LM_CH + cb) * T + t) * 8 * H + (size_t)dir * 4 * H + ug * LP_U + cu;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pr4[q] = pr[q * H];
+      }
+      __syncthreads();  // chunk c's image complete (and red free)
+      if (abort_flag) {  // a peer stopped publishing: flag the host, poison the remaining outputs, leave
+        if (tid == 0 && err_host) __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int st = step; st < T; ++st) {
+          const int tt = dir == 0 ? st : T - 1 - st;
+          for (int q = tid; q < LP_U * B; q += LM_THREADS)
+            hsd[((size_t)(q / LP_U) * T + tt) * H + ug * LP_U + q % LP_U] = __builtin_nanf("");
+        }
+        return;
+      }
+      if (step > 0 && c + 1 < nch) issue(step, c + 1);  // next chunk's exchange under this chunk's math
+      // this lane's 40-term dot products for its gate row, one sequence at a time (four interleaved
+      // accumulators, summed in a fixed order), straight into the partial-sum image
+      const int buf = c & 1;
+#pragma unroll 2
+      for (int b = 0; b < nb; ++b) {
+        float a4[4] = {0.f, 0.f, 0.f, 0.f};
+        if (step > 0) {
+          const float* hb = &hsh[buf][b][kbase];
+#pragma unroll
+          for (int s = 0; s < LM_KL; s += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(hb + s);
+            a4[0] = fmaf(wa[s], v.x, a4[0]);
+            a4[1] = fmaf(wa[s + 1], v.y, a4[1]);
+            a4[2] = fmaf(wa[s + 2], v.z, a4[2]);
+            a4[3] = fmaf(wa[s + 3], v.w, a4[3]);
+          }
+        }
+        red[slice][l32][b] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+      }
+      if (step > 0 && c + 1 < nch) land(step, c + 1, (c + 1) & 1);
+      __syncthreads();
+      if (tid < LP_U * nb) {
+        const int unit = ug * LP_U + cu, b = c * LM_CH + cb;
+        float gs[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = q * LP_U + cu;
+          float s = 0.f;
+#pragma unroll
+          for (int sl = 0; sl < 16; sl += 4)
+            s += (red[sl][r][cb] + red[sl + 1][r][cb]) + (red[sl + 2][r][cb] + red[sl + 3][r][cb]);
+          gs[q] = s;
+        }
+        const float gi = sigmoid_exact(pr4[0] + gs[0]);
+        const float gf = sigmoid_exact(pr4[1] + gs[1]);
+        const float gg = tanhf(pr4[2] + gs[2]);
+        const float go = sigmoid_exact(pr4[3] + gs[3]);
+        const float cc = step > 0 ? gf * cst[cu][b] + gi * gg : gi * gg;
+        cst[cu][b] = cc;
+        const float h = go * tanhf(cc);
+        hsd[((size_t)b * T + t) * H + unit] = h;
+        if (step + 1 < T)
+          __hip_atomic_store(gd + (size_t)(step & 1) * LM_BMAX * H + (size_t)b * H + unit,
+                             ((unsigned long long)(step + 1) << 32) | __float_as_uint(h), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
 }  // namespace
+
+bool lstm_mid_supported(int B, int H) { return H == LP_H && B > LS_BMAX && B <= LM_BMAX; }
+
+size_t lstm_mid_sync_bytes() { return 256 + (size_t)2 * 2 * LM_BMAX * LP_H * sizeof(unsigned long long); }
+
+void launch_lstm_mid(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,
+                     unsigned* err_host, hipStream_t s) {
+  M2S_CHECK(lstm_mid_supported(B, H) && T > 0, "lstm_mid: unsupported shape");
+  const int grid = 2 * (H / LP_U);
+  const int resident = device_resident(reinterpret_cast<const void*>(&lstm_mid_kernel), LM_THREADS, 0);
+  M2S_CHECK(grid <= resident, "lstm_mid: grid not co-resident on this device");
+  M2S_HIP(hipMemsetAsync(sync, 0, lstm_mid_sync_bytes(), s));
+  unsigned* err = static_cast<unsigned*>(sync);
+  unsigned long long* gran = reinterpret_cast<unsigned long long*>(static_cast<char*>(sync) + 256);
+  hipLaunchKernelGGL(lstm_mid_kernel, dim3(grid), dim3(LM_THREADS), 0, s, pre, whh, hs, B, T, gran, err, spin_max,
+                     err_host);
+  M2S_HIP(hipGetLastError());
+}
 
 bool lstm_persistent_supported(int H) { return H == LP_H; }
 
