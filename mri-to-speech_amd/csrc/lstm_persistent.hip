@@ -19,6 +19,7 @@
 // too, and the C ABI reports it (m2s_acoustic_status; the next forward fails with M2S_E_INTERNAL).
 // Products are exact fp32 (MFMA f32); only the summation order differs from torch.
 #include <algorithm>
+#include <cstdlib>
 
 #include "kernels.hpp"
 
@@ -186,8 +187,10 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
 // most one step ahead of any other: publishing h_{t+1} needs every h_t).  The recurrence products
 // run on VALU: lane (wave, k half, row) holds the same 80 W_hh values as above and forms B fp32 dot
 // products of 80 terms; the 8 K-slice partials of each gate row are summed in LDS in a fixed order.
-constexpr int LS_BMAX = 4;
+constexpr int LS_BMAX = 4;   // default small-batch limit
+constexpr int LS_BCAP = 8;   // largest instantiation (M2S_LSTM_SMALL_B = 8 selects it for B <= 8)
 
+template <int LS_BMAX>
 __global__ void __launch_bounds__(256, 1) lstm_small_kernel(const float* __restrict__ pre, const float* __restrict__ whh,
                                                             float* hs, int B, int T, unsigned long long* gran,
                                                             unsigned* err, unsigned spin_max, unsigned* err_host) {
@@ -222,7 +225,9 @@ __global__ void __launch_bounds__(256, 1) lstm_small_kernel(const float* __restr
 
   for (int step = 0; step < T; ++step) {
     const int t = dir == 0 ? step : T - 1 - step;
-    float p[LS_BMAX] = {0.f, 0.f, 0.f, 0.f};
+    float p[LS_BMAX];
+#pragma unroll
+    for (int b = 0; b < LS_BMAX; ++b) p[b] = 0.f;
     if (step > 0) {
       // ---- h_{t-1}: sweep the direction's granules (tag == step) into LDS -----------------------
       const unsigned long long* src = gd + (size_t)((step - 1) & 1) * LS_BMAX * H;
@@ -253,8 +258,7 @@ __global__ void __launch_bounds__(256, 1) lstm_small_kernel(const float* __restr
       }
       // ---- this lane's 80-term K-slice dot products for gate row l32 -----------------------------
 #pragma unroll
-      for (int b = 0; b < LS_BMAX; ++b) {
-        if (b >= B) break;
+      for (int b = 0; b < LS_BMAX; ++b) {  // rows past B are stale and never read back
         const float* hb = &hsh[b][kbase];
         float a = 0.f;
 #pragma unroll
@@ -312,10 +316,10 @@ __global__ void __launch_bounds__(256, 1) lstm_small_kernel(const float* __restr
 // Double buffering by step parity stays safe per chunk: a workgroup can publish chunk c of h_{t+1} only
 // after every workgroup published chunk c of h_t, i.e. after each of them finished reading chunk c of
 // h_{t-1}.  Exact fp32 products; the partial-sum order is fixed.
-constexpr int LM_BMAX = 64, LM_CH = 8, LM_THREADS = 512;
+constexpr int LM_BMAX = 64, LM_THREADS = 512;
 constexpr int LM_KL = LP_H / 16;                    // k per lane (16 slices of 40)
-constexpr int LM_G = LM_CH * LP_H / LM_THREADS;     // granules per thread per chunk (20)
 
+template <int LM_CH>
 __global__ void __launch_bounds__(LM_THREADS, 1) lstm_mid_kernel(const float* __restrict__ pre,
                                                                  const float* __restrict__ whh, float* hs, int B,
                                                                  int T, unsigned long long* gran, unsigned* err,
@@ -332,6 +336,7 @@ __global__ void __launch_bounds__(LM_THREADS, 1) lstm_mid_kernel(const float* __
   float* hsd = hs + (size_t)dir * B * T * H;
   unsigned long long* gd = gran + (size_t)dir * 2 * LM_BMAX * H;
   const int nch = (B + LM_CH - 1) / LM_CH;
+  constexpr int LM_G = LM_CH * LP_H / LM_THREADS;  // granules per thread per chunk
 
   float wa[LM_KL];
   {
@@ -465,7 +470,15 @@ __global__ void __launch_bounds__(LM_THREADS, 1) lstm_mid_kernel(const float* __
 
 }  // namespace
 
-bool lstm_mid_supported(int B, int H) { return H == LP_H && B > LS_BMAX && B <= LM_BMAX; }
+static int small_cap() {
+  static const int cap = [] {
+    const char* e = std::getenv("M2S_LSTM_SMALL_B");
+    return e && std::atoi(e) == 8 ? 8 : LS_BMAX;
+  }();
+  return cap;
+}
+
+bool lstm_mid_supported(int B, int H) { return H == LP_H && B > small_cap() && B <= LM_BMAX; }
 
 size_t lstm_mid_sync_bytes() { return 256 + (size_t)2 * 2 * LM_BMAX * LP_H * sizeof(unsigned long long); }
 
@@ -473,33 +486,57 @@ void launch_lstm_mid(const float* pre, const float* whh, float* hs, int B, int T
                      unsigned* err_host, hipStream_t s) {
   M2S_CHECK(lstm_mid_supported(B, H) && T > 0, "lstm_mid: unsupported shape");
   const int grid = 2 * (H / LP_U);
-  const int resident = device_resident(reinterpret_cast<const void*>(&lstm_mid_kernel), LM_THREADS, 0);
+  // sequences per chunk (env M2S_LSTM_MID_CH: 4 / 8 / 16 for A/B runs)
+  static const int ch = [] {
+    const char* e = std::getenv("M2S_LSTM_MID_CH");
+    const int v = e ? std::atoi(e) : 8;
+    return v == 4 || v == 16 ? v : 8;
+  }();
+  const void* fn = ch == 4 ? reinterpret_cast<const void*>(&lstm_mid_kernel<4>)
+                   : ch == 16 ? reinterpret_cast<const void*>(&lstm_mid_kernel<16>)
+                              : reinterpret_cast<const void*>(&lstm_mid_kernel<8>);
+  const int resident = device_resident(fn, LM_THREADS, 0);
   M2S_CHECK(grid <= resident, "lstm_mid: grid not co-resident on this device");
   M2S_HIP(hipMemsetAsync(sync, 0, lstm_mid_sync_bytes(), s));
   unsigned* err = static_cast<unsigned*>(sync);
   unsigned long long* gran = reinterpret_cast<unsigned long long*>(static_cast<char*>(sync) + 256);
-  hipLaunchKernelGGL(lstm_mid_kernel, dim3(grid), dim3(LM_THREADS), 0, s, pre, whh, hs, B, T, gran, err, spin_max,
-                     err_host);
+  if (ch == 4)
+    hipLaunchKernelGGL(lstm_mid_kernel<4>, dim3(grid), dim3(LM_THREADS), 0, s, pre, whh, hs, B, T, gran, err,
+                       spin_max, err_host);
+  else if (ch == 16)
+    hipLaunchKernelGGL(lstm_mid_kernel<16>, dim3(grid), dim3(LM_THREADS), 0, s, pre, whh, hs, B, T, gran, err,
+                       spin_max, err_host);
+  else
+    hipLaunchKernelGGL(lstm_mid_kernel<8>, dim3(grid), dim3(LM_THREADS), 0, s, pre, whh, hs, B, T, gran, err,
+                       spin_max, err_host);
   M2S_HIP(hipGetLastError());
 }
 
 bool lstm_persistent_supported(int H) { return H == LP_H; }
 
-bool lstm_small_supported(int B, int H) { return H == LP_H && B >= 1 && B <= LS_BMAX; }
+bool lstm_small_supported(int B, int H) { return H == LP_H && B >= 1 && B <= small_cap(); }
 
-size_t lstm_small_sync_bytes() { return 256 + (size_t)2 * 2 * LS_BMAX * LP_H * sizeof(unsigned long long); }
+size_t lstm_small_sync_bytes() { return 256 + (size_t)2 * 2 * LS_BCAP * LP_H * sizeof(unsigned long long); }
 
 void launch_lstm_small(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,
                        unsigned* err_host, hipStream_t s) {
   M2S_CHECK(lstm_small_supported(B, H) && T > 0, "lstm_small: unsupported shape");
   const int grid = 2 * (H / LP_U);
-  const int resident = device_resident(reinterpret_cast<const void*>(&lstm_small_kernel), 256, 0);
+  const bool b8 = B > LS_BMAX;  // the 8-sequence instantiation (M2S_LSTM_SMALL_B = 8)
+  const void* fn = b8 ? reinterpret_cast<const void*>(&lstm_small_kernel<LS_BCAP>)
+                      : reinterpret_cast<const void*>(&lstm_small_kernel<LS_BMAX>);
+  const int resident = device_resident(fn, 256, 0);
   M2S_CHECK(grid <= resident, "lstm_small: grid not co-resident on this device");
   // [256 B: error word][granules 2 dir x 2 parity x LS_BMAX x H]: every tag restarts at 0 each call
   M2S_HIP(hipMemsetAsync(sync, 0, lstm_small_sync_bytes(), s));
   unsigned* err = static_cast<unsigned*>(sync);
   unsigned long long* gran = reinterpret_cast<unsigned long long*>(static_cast<char*>(sync) + 256);
-  hipLaunchKernelGGL(lstm_small_kernel, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, T, gran, err, spin_max, err_host);
+  if (b8)
+    hipLaunchKernelGGL(lstm_small_kernel<LS_BCAP>, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, T, gran, err, spin_max,
+                       err_host);
+  else
+    hipLaunchKernelGGL(lstm_small_kernel<LS_BMAX>, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, T, gran, err, spin_max,
+                       err_host);
   M2S_HIP(hipGetLastError());
 }
 
