@@ -258,7 +258,8 @@ __global__ void __launch_bounds__(256, 1) lstm_small_kernel(const float* __restr
       }
       // ---- this lane's 80-term K-slice dot products for gate row l32 -----------------------------
 #pragma unroll
-      for (int b = 0; b < LS_BMAX; ++b) {  // rows past B are stale and never read back
+      for (int b = 0; b < LS_BMAX; ++b) {
+        if (LS_BMAX <= 4 && b >= B) break;  // (the 8-wide instantiation computes all rows: stale ones unused)
         const float* hb = &hsh[b][kbase];
         float a = 0.f;
 #pragma unroll
@@ -478,7 +479,10 @@ static int small_cap() {
   return cap;
 }
 
-bool lstm_mid_supported(int B, int H) { return H == LP_H && B > small_cap() && B <= LM_BMAX; }
+// 4 < B <= 16: above 16 sequences every workgroup's sweep of B x 640 granules per step (sc1 loads, the
+// exchange volume grows with B) costs more than the counter barrier's plain loads of h (tools/lstm_bench.py,
+// profiles/r03f_lstm_ab.txt: B = 32 20.2 vs 18.3 us, B = 64 40.9 vs 24.7 us per step)
+bool lstm_mid_supported(int B, int H) { return H == LP_H && B > small_cap() && B <= 16; }
 
 size_t lstm_mid_sync_bytes() { return 256 + (size_t)2 * 2 * LM_BMAX * LP_H * sizeof(unsigned long long); }
 
@@ -486,12 +490,14 @@ void launch_lstm_mid(const float* pre, const float* whh, float* hs, int B, int T
                      unsigned* err_host, hipStream_t s) {
   M2S_CHECK(lstm_mid_supported(B, H) && T > 0, "lstm_mid: unsupported shape");
   const int grid = 2 * (H / LP_U);
-  // sequences per chunk (env M2S_LSTM_MID_CH: 4 / 8 / 16 for A/B runs)
-  static const int ch = [] {
+  // sequences per chunk: 4 up to B = 8 (two chunks at B = 8: the second one's sweep overlaps the first's
+  // dot products; 6.5 us per step vs 8.6 at one chunk of 8), 8 above; env M2S_LSTM_MID_CH for A/B runs
+  static const int ch_env = [] {
     const char* e = std::getenv("M2S_LSTM_MID_CH");
-    const int v = e ? std::atoi(e) : 8;
-    return v == 4 || v == 16 ? v : 8;
+    const int v = e ? std::atoi(e) : 0;
+    return v == 4 || v == 8 || v == 16 ? v : 0;
   }();
+  const int ch = ch_env ? ch_env : (B <= 8 ? 4 : 8);
   const void* fn = ch == 4 ? reinterpret_cast<const void*>(&lstm_mid_kernel<4>)
                    : ch == 16 ? reinterpret_cast<const void*>(&lstm_mid_kernel<16>)
                               : reinterpret_cast<const void*>(&lstm_mid_kernel<8>);
