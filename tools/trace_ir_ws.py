@@ -7,6 +7,7 @@ import os, sys
 import numpy as np
 import torch
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "mri-to-speech_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "diag"))  # tools/build_diag.sh
 from m2s import runtime as rt, synth
 DEV = torch.device("cuda", 0)
 st = synth.synth_acoustic_state(1)
