@@ -71,3 +71,22 @@ def test_vocoder_fp8_wav_cosine_1x1000(rt):
     snr = 10 * np.log10((ref ** 2).sum() / max(((wav.reshape(ref.shape) - ref) ** 2).sum(), 1e-30))
     print(f"\nfp8 vocoder 1x1000 frames: wav cos {c:.5f}, SNR {snr:.1f} dB")
     assert c >= COS_MIN
+
+
+def test_pipeline_fp8_end_to_end_1x1000(rt, clip1000):
+    """configs[4] end to end at its clip length: frames -> mel -> wav in ONE fp8 pipeline_forward call
+    (e4m3 backbone and MRF convs), mel_norm and wav cosine vs the fp32 oracle of the same clip."""
+    st, fr, _, mn_ref = clip1000
+    gen_sd = synth.synth_generator_state(5, HIFIGAN_H)
+    mean, std = synth.synth_scaler()
+    pipe = rt.Pipeline(rt.AcousticEngine(st, dtype="fp8", device=DEV),
+                       rt.VocoderEngine(gen_sd, HIFIGAN_H, dtype="fp8", device=DEV), mean, std)
+    out = pipe.forward(torch.from_numpy(fr).to(DEV))
+    pipe.ac.check()
+    ln_ref = acoustic.mel_db_to_log(acoustic.denormalize_mel(torch.from_numpy(mn_ref), mean, std))
+    wav_ref = hifigan.generator({k: torch.from_numpy(v) for k, v in gen_sd.items()}, HIFIGAN_H,
+                                ln_ref.transpose(1, 2))[:, 0].numpy()
+    c_mel, c_wav = _cos(out["mel_norm"].cpu().numpy(), mn_ref), _cos(out["wav"].cpu().numpy(), wav_ref)
+    print(f"\nfp8 pipeline 1x1000: mel_norm cos {c_mel:.5f}, wav cos {c_wav:.5f}")
+    assert out["wav"].shape == (1, 1000 * 420)
+    assert c_mel >= COS_MIN and c_wav >= COS_MIN
