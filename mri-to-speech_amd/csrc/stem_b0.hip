@@ -27,6 +27,8 @@
 // one XCD work on neighbouring tiles of the same frames at any time (shared halos stay in its L2).
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 #include "kernels.hpp"
 #include "prof.hpp"
@@ -54,6 +56,7 @@ struct StemB0Args {
   bf16_t* y;            // (N, OH, OW, 16) (SP: (N, OH, OW, [hi 16 | lo 16]))
   int N, H, W, OH, OW, pad_t, pad_l, kp0, kp1, tiles_x, tiles_y;
   int per_xcd;  // tiles per XCD range (gridDim.x is a multiple of 8)
+  unsigned long long* trace;  // diagnostic build (-DIRWS_TRACE): per-phase s_memtime stamps, else null
 };
 
 __device__ __forceinline__ bf16x8 frag(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
@@ -146,9 +149,18 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
   const float4 bb1 = *reinterpret_cast<const float4*>(a.b1 + 4 * g);
   __syncthreads();
 
-  for (; t < t_end; t += gx) {
+  int it = 0;  // tile iteration (diagnostic stamps)
+  auto TR = [&](int k) {
+#ifdef IRWS_TRACE
+    if (a.trace && blockIdx.x == 0 && lane == 0 && it < 32) a.trace[(it * 4 + wave) * 8 + k] = __builtin_amdgcn_s_memtime();
+#else
+    (void)k;
+#endif
+  };
+  for (; t < t_end; t += gx, ++it) {
     int n, ty0, tx0;
     tile_of(t, n, ty0, tx0);
+    TR(0);
     // ---- phase 1: stem (fp32 VALU) -> S -----------------------------------------------------
     // (S is free: every wave passed this tile's predecessor's phase-2/3 barrier before reaching here.)
     if (p1) {
@@ -206,7 +218,9 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
       // the next tile's frame pixels, in flight through phases 2 and 3
       if (t + gx < t_end) load_in(t + gx);
     }
+    TR(1);
     __syncthreads();
+    TR(2);
 
     // ---- phase 2: blocks.0.0 (32 -> 16) on MFMA -> A ------------------------------------------
     {
@@ -255,7 +269,9 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
         if constexpr (SP) *reinterpret_cast<uint2*>(sA + ALO + (g >> 1) * APLANE + pa * 16 + (g & 1) * 8) = ul;
       }
     }
+    TR(3);
     __syncthreads();
+    TR(4);
 
     // ---- phase 3: blocks.0.1 (16 -> 16) + skip on MFMA -> y -----------------------------------
     {
@@ -309,6 +325,7 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
         }
       }
     }
+    TR(5);
   }
 }
 
@@ -337,6 +354,15 @@ void launch_stem_b0(const float* frames, int N, int H, int W, int OH, int OW, in
   a.pad_l = pad_l;
   a.kp0 = kp0;
   a.kp1 = kp1;
+  a.trace = nullptr;
+#ifdef IRWS_TRACE
+  static unsigned long long* tr = [] {
+    unsigned long long* p = nullptr;
+    if (getenv("M2S_IR_WS_TRACE")) M2S_HIP(hipMalloc(&p, 32 * 4 * 8 * 8));
+    return p;
+  }();
+  a.trace = tr;
+#endif
   a.tiles_x = ceil_div(OW, SB_TW);
   a.tiles_y = ceil_div(OH, TH);
   M2S_CHECK((double)N * a.tiles_x * a.tiles_y < 2147483647.0, "stem_b0: grid");
@@ -350,6 +376,25 @@ void launch_stem_b0(const float* frames, int N, int H, int W, int OH, int OW, in
   if (split) {
     ProfScope ps("stem_b0_kernel<16, 1>", flops, bytes, s);
     hipLaunchKernelGGL((stem_b0_kernel<TH, 1>), dim3(grid), dim3(256), 0, s, a);
+#ifdef IRWS_TRACE
+    if (tr) {  // per-phase cycles of workgroup 0's four waves, first tiles: p1 bar1 p2 bar2 p3
+      static int calls = 0;
+      if (++calls <= 4) {
+        std::vector<unsigned long long> h(32 * 4 * 8);
+        M2S_HIP(hipStreamSynchronize(s));
+        M2S_HIP(hipMemcpy(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost));
+        fprintf(stderr, "STEMTRACE");
+        for (int i = 2; i < 12; ++i)
+          for (int w = 0; w < 4; w += 3) {
+            const unsigned long long* q = &h[(i * 4 + w) * 8];
+            fprintf(stderr, " [t%d w%d p1 %lld bar1 %lld p2 %lld bar2 %lld p3 %lld next %lld]", i, w, (long long)(q[1] - q[0]),
+                    (long long)(q[2] - q[1]), (long long)(q[3] - q[2]), (long long)(q[4] - q[3]), (long long)(q[5] - q[4]),
+                    (long long)(h[((i + 1) * 4 + w) * 8] - q[5]));
+          }
+        fprintf(stderr, "\n");
+      }
+    }
+#endif
   } else {
     ProfScope ps("stem_b0_kernel<16, 0>", flops, bytes, s);
     hipLaunchKernelGGL((stem_b0_kernel<TH, 0>), dim3(grid), dim3(256), 0, s, a);
