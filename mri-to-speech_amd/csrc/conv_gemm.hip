@@ -107,8 +107,13 @@ __device__ __forceinline__ void scale_split(bf16x8& h, bf16x8& l, const float* s
   resplit_frag(v, h, l);
 }
 
-// 8 bf16 -> 8 OCP e4m3fn (gfx950 v_cvt_pk_fp8_f32, round to nearest even), clamped to +-448 (the
-// largest finite e4m3: the conversion has no saturating mode)
+// finite values clamped to +-448 (the largest finite e4m3: the conversion has no saturating mode);
+// a NaN stays NaN (fmaxf would turn it into -448) so an upstream fault is not hidden as finite data
+__device__ __forceinline__ float sat_e4m3(float x) {
+  return x != x ? x : fminf(fmaxf(x, -448.f), 448.f);
+}
+
+// 8 bf16 -> 8 OCP e4m3fn (gfx950 v_cvt_pk_fp8_f32, round to nearest even), saturated by sat_e4m3
 __device__ __forceinline__ long fp8x8(bf16x8 v) {
   const uint4 u = __builtin_bit_cast(uint4, v);
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
@@ -118,8 +123,8 @@ __device__ __forceinline__ long fp8x8(bf16x8 v) {
     float f[4];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      f[2 * j] = fminf(fmaxf(__uint_as_float(w[2 * h + j] << 16), -448.f), 448.f);
-      f[2 * j + 1] = fminf(fmaxf(__uint_as_float(w[2 * h + j] & 0xffff0000u), -448.f), 448.f);
+      f[2 * j] = sat_e4m3(__uint_as_float(w[2 * h + j] << 16));
+      f[2 * j + 1] = sat_e4m3(__uint_as_float(w[2 * h + j] & 0xffff0000u));
     }
     int r = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
     q[h] = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], r, true);
@@ -726,6 +731,7 @@ void launch_conv_gemm(const ConvArgs& a, bool split, hipStream_t s, double flops
   if (a.M <= 0) return;
   M2S_CHECK(!(split && a.wscale), "conv_gemm: e4m3 operands take bf16 storage");
   if (split) {
+    if (a.kind == KIND_GEMM && a.in_xform == IN_SE_SCALE && se_gemm_supported(a)) return launch_se_gemm(a, s, flops, bytes);
     switch (a.kind) {
       case KIND_CONV2D: launch_kind<KIND_CONV2D, 1>(a, s, 1, flops, bytes); break;
       case KIND_CONV1D: launch_kind<KIND_CONV1D, 1>(a, s, 1, flops, bytes); break;

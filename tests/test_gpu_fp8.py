@@ -51,6 +51,18 @@ def test_effnet_fp8_features_cosine(rt, clip1000):
     assert c >= COS_MIN
 
 
+def test_effnet_fp8_propagates_nan(rt):
+    """A NaN pixel must reach the features as NaN (the e4m3 operand saturation keeps NaN), not be
+    clamped to -448 and come out as finite data; the clean frames of the same batch stay finite."""
+    st = synth.synth_acoustic_state(3)
+    eng = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    fr = torch.from_numpy(synth.synth_frames(1, 4, seed=2)[0]).to(DEV)
+    fr[1, 100, 100] = float("nan")
+    f = eng.effnet(fr).cpu()
+    assert torch.isnan(f[1]).any()
+    assert torch.isfinite(f[[0, 2, 3]]).all()
+
+
 def test_acoustic_fp8_mel_cosine_1x1000(rt, clip1000):
     st, fr, _, mn_ref = clip1000
     eng = rt.AcousticEngine(st, dtype="fp8", device=DEV)
