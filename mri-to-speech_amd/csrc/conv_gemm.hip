@@ -731,7 +731,6 @@ void launch_conv_gemm(const ConvArgs& a, bool split, hipStream_t s, double flops
   if (a.M <= 0) return;
   M2S_CHECK(!(split && a.wscale), "conv_gemm: e4m3 operands take bf16 storage");
   if (split) {
-    if (a.kind == KIND_GEMM && a.in_xform == IN_SE_SCALE && se_gemm_supported(a)) return launch_se_gemm(a, s, flops, bytes);
     switch (a.kind) {
       case KIND_CONV2D: launch_kind<KIND_CONV2D, 1>(a, s, 1, flops, bytes); break;
       case KIND_CONV1D: launch_kind<KIND_CONV1D, 1>(a, s, 1, flops, bytes); break;
