@@ -88,7 +88,8 @@ int m2s_acoustic_set_chunk(m2s_acoustic* m, int frames);
  * launch has happened: call it after synchronising the stream.  The next forward / bilstm /
  * pipeline call on the engine fails the same way.  Synchronous, host only. */
 int m2s_acoustic_status(m2s_acoustic* m);
-/* Fault injection for tests: polls per BiLSTM barrier wait before it times out (default 2^24). */
+/* Fault injection for tests: polls per BiLSTM barrier wait before it times out (default 2^24); 0 makes
+ * the first wait time out unconditionally. */
 int m2s_acoustic_set_lstm_spin_limit(m2s_acoustic* m, unsigned polls);
 size_t m2s_acoustic_workspace_bytes(const m2s_acoustic* m, int B, int T, int H, int W);
 /* frames (B,T,H,W) fp32 in [0,1] -> mel_norm (B,T,n_mels) fp32. */

@@ -114,7 +114,7 @@ int m2s_acoustic_status(m2s_acoustic* m) {
 
 int m2s_acoustic_set_lstm_spin_limit(m2s_acoustic* m, unsigned polls) {
   return guarded([&] {
-    M2S_CHECK(m && polls > 0, "bad argument");
+    M2S_CHECK(m, "bad argument");
     m->impl.lstm_spin_max_ = polls;
   });
 }

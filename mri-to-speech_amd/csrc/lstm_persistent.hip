@@ -14,6 +14,8 @@
 // (the layer output) and is published to the direction's other workgroups by a release/acquire
 // counter barrier (cdna_hip_programming.md Guideline 16): plain stores -> vmcnt(0) -> barrier ->
 // agent release fence -> atomic add; consumers poll relaxed, then one agent acquire fence.
+// (spin_max == 0 is fault injection: the first wait times out whatever the tags say, so a test of
+// the report does not depend on how late a peer happens to publish.)
 // Spins are bounded: on timeout the workgroup sets the error word, poisons its remaining outputs
 // with NaN and leaves, so the grid always drains; the engine's pinned host flag (`err_host`) is set
 // too, and the C ABI reports it (m2s_acoustic_status; the next forward fails with M2S_E_INTERNAL).
@@ -85,7 +87,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
       if (tid == 0) {
         const unsigned target = (unsigned)step * nwg;
         unsigned spins = 0;
-        while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target || spin_max == 0) {
           __builtin_amdgcn_s_sleep(1);
           if (++spins > spin_max ||
               __hip_atomic_load(&sync->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
@@ -235,7 +237,8 @@ __global__ void __launch_bounds__(256, 1) lstm_small_kernel(const float* __restr
       for (int i = tid; i < B * H && ok; i += 256) {
         unsigned spins = 0;
         unsigned long long x;
-        while (((x = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != (unsigned)step) {
+        while (((x = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != (unsigned)step ||
+               spin_max == 0) {
           __builtin_amdgcn_s_sleep(1);
           if (++spins > spin_max || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
             __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -378,7 +381,7 @@ __global__ void __launch_bounds__(LM_THREADS, 1) lstm_mid_kernel(const float* __
       if (i >= n) continue;
       unsigned long long x = g[j];
       unsigned spins = 0;
-      while (ok && (unsigned)(x >> 32) != (unsigned)step) {
+      while (ok && ((unsigned)(x >> 32) != (unsigned)step || spin_max == 0)) {
         __builtin_amdgcn_s_sleep(1);
         x = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (++spins > spin_max || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {

@@ -323,13 +323,13 @@ def test_preprocess_vs_oracle_shapes_and_bgr(rt, shape):
 # ------------------------------------------------------------------------------ asynchronous failure report
 @pytest.mark.parametrize("B", [1, 8, 70])
 def test_bilstm_barrier_timeout_is_reported(rt, ac_state, B):
-    """A BiLSTM hand-off wait that times out (forced: one poll allowed) poisons the outputs and is
+    """A BiLSTM hand-off wait that times out (forced: spin limit 0 = the first wait fails) poisons the outputs and is
     reported: m2s_acoustic_status -> M2SError, and the next forward on the engine fails too.  B = 1:
     lstm_small_kernel, 8: lstm_mid_kernel (granule sweeps), 70: the counter barrier."""
     import ctypes
     from m2s import _native
     eng = rt.AcousticEngine(ac_state[1], dtype="fp32", device=DEV)
-    _native.check(_native.lib().m2s_acoustic_set_lstm_spin_limit(ctypes.c_void_p(eng.handle), 1))
+    _native.check(_native.lib().m2s_acoustic_set_lstm_spin_limit(ctypes.c_void_p(eng.handle), 0))
     x = torch.randn(B, 30, 208, device=DEV)
     y, _ = eng.bilstm(x)
     with pytest.raises(_native.M2SError, match="timed out"):
