@@ -107,13 +107,8 @@ __device__ __forceinline__ void scale_split(bf16x8& h, bf16x8& l, const float* s
   resplit_frag(v, h, l);
 }
 
-// finite values clamped to +-448 (the largest finite e4m3: the conversion has no saturating mode);
-// a NaN stays NaN (fmaxf would turn it into -448) so an upstream fault is not hidden as finite data
-__device__ __forceinline__ float sat_e4m3(float x) {
-  return x != x ? x : fminf(fmaxf(x, -448.f), 448.f);
-}
-
 // 8 bf16 -> 8 OCP e4m3fn (gfx950 v_cvt_pk_fp8_f32, round to nearest even), saturated by sat_e4m3
+// (m2s_common.hpp: finite values clamped to +-448, a NaN stays NaN so an upstream fault is not hidden)
 __device__ __forceinline__ long fp8x8(bf16x8 v) {
   const uint4 u = __builtin_bit_cast(uint4, v);
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};

@@ -53,7 +53,7 @@ __device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float acc) {
 // SOH x SOW map, TF-SAME with top / left pads pad_t / pad_l (the stride-2 blocks.5.0 at 16x16).
 // SP = 1: x, wpw (rows [hi kp | lo kp]), y and se_mean are split fp32; wdw2 is then the fp32
 // tap-major [9][cs_mid] depthwise weight.
-template <int MT, int G, int S, int SP>
+template <int MT, int G, int S, int SPM>
 __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int cs_in, int kp,
                                                          const bf16_t* __restrict__ wpw, const float* __restrict__ bpw,
                                                          const uint32_t* __restrict__ wdw2,
@@ -61,6 +61,8 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
                                                          int cs_mid, bf16_t* __restrict__ y,
                                                          bf16_t* __restrict__ se_mean, int SOH, int SOW, int pad_t,
                                                          int pad_l) {
+  constexpr bool SP = SPM == 1;  // split fp32
+  constexpr bool F8 = SPM == 2;  // bf16 compute, e4m3 depthwise output (fp8 engines: the e4m3 SE GEMM's operand)
   // the haloed tile: dynamic LDS sized for this launch's G images (ir_tile_bytes)
   extern __shared__ __attribute__((aligned(16))) char tile_raw[];
   bf16_t* tile = reinterpret_cast<bf16_t*>(tile_raw);
@@ -318,15 +320,20 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
         }
         uint4 o;
         uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+        float v[8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float v0 = silu(a[2 * j]);
-          const float v1 = silu(a[2 * j + 1]);
-          s[2 * j] += v0;
-          s[2 * j + 1] += v1;
-          ow[j] = pack_bf16x2(v0, v1);
+          v[2 * j] = silu(a[2 * j]);
+          v[2 * j + 1] = silu(a[2 * j + 1]);
+          s[2 * j] += v[2 * j];  // the squeeze sums the unrounded values
+          s[2 * j + 1] += v[2 * j + 1];
+          ow[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
         }
-        *reinterpret_cast<uint4*>(yi + (size_t)p * cs_mid) = o;
+        if constexpr (F8) {  // 8 channels -> 8 bytes at byte (n, p, c) of the e4m3 map
+          reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(y) + ((size_t)(n0 + g) * PO + p) * cs_mid + c)[0] = e4m3x8(v);
+        } else {
+          *reinterpret_cast<uint4*>(yi + (size_t)p * cs_mid) = o;
+        }
       }
     }
     // ---- squeeze: the wave's 16 pixel lanes (lane / CG) share cg = lane % CG; one image per wave
@@ -354,7 +361,7 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
 }
 
 template <int MT, int G, int SP>
-__global__ void __launch_bounds__(256, SP ? (MT >= 4 ? 3 : 4) : 4)
+__global__ void __launch_bounds__(256, SP == 1 ? (MT >= 4 ? 3 : 4) : 4)
     ir_pwdw_kernel(const bf16_t* __restrict__ x, int cs_in, int kp, const bf16_t* __restrict__ wpw,
                    const float* __restrict__ bpw, const uint32_t* __restrict__ wdw2, const float* __restrict__ bdw, int N,
                    int OH, int OW, int cs_mid, bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean) {
@@ -362,7 +369,7 @@ __global__ void __launch_bounds__(256, SP ? (MT >= 4 ? 3 : 4) : 4)
 }
 
 template <int SP>
-__global__ void __launch_bounds__(256, SP ? 3 : 4)
+__global__ void __launch_bounds__(256, SP == 1 ? 3 : 4)
     ir_pwdw_s2_kernel(const bf16_t* __restrict__ x, int cs_in, int kp, const bf16_t* __restrict__ wpw,
                       const float* __restrict__ bpw, const uint32_t* __restrict__ wdw2, const float* __restrict__ bdw,
                       int N, int IH, int IW, int cs_mid, bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, int OH,
@@ -392,8 +399,10 @@ bool ir_fused_supported(int OH, int OW, int cs_in, int cs_mid, bool split) {
 
 void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, const float* bpw, const void* wdw,
                     const float* bdw, int OH, int OW, int cs_mid, void* y, void* se_mean, bool split, double flops,
-                    double bytes, hipStream_t s) {
+                    double bytes, hipStream_t s, bool f8_out) {
   M2S_CHECK(ir_fused_supported(OH, OW, cs_in, cs_mid, split), "ir_pwdw: unsupported shape");
+  M2S_CHECK(!(split && f8_out), "ir_pwdw: e4m3 output is a bf16-path variant");
+  const int mode = split ? 1 : f8_out ? 2 : 0;
   M2S_CHECK(kp % 32 == 0 && kp >= cs_in, "ir_pwdw: kp");
   const int G = ir_group(OH, OW, split), pos = G * OH * OW;
   const dim3 grid(ceil_div(cs_mid, SL) * ceil_div(N, G));
@@ -405,7 +414,7 @@ void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, co
   // MT = 16-position subtiles per wave (pos <= 64 * MT); G = images per workgroup.  Each pair is
   // its own symbol, so rocprofv3 and the event profiler see the same kernel.
 #define M2S_IRF(MT_, G_, SP_)                                                                            \
-  if (pos <= 64 * MT_ && G == G_ && (int)split == SP_) {                                                 \
+  if (pos <= 64 * MT_ && G == G_ && mode == SP_) {                                                 \
     ProfScope ps("ir_pwdw_kernel<" #MT_ ", " #G_ ", " #SP_ ">", flops, bytes, s);                       \
     hipLaunchKernelGGL((ir_pwdw_kernel<MT_, G_, SP_>), grid, dim3(256), ir_tile_bytes(OH, OW, G, split), s, xb, cs_in, \
                        kp, wb, bpw, wd, bdw, N, OH, OW, cs_mid, yb, mb);                                 \
@@ -418,6 +427,7 @@ void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, co
   M2S_IRF(1, 1, 1) M2S_IRF(1, 2, 1) M2S_IRF(1, 4, 1)
   M2S_IRF(2, 1, 1) M2S_IRF(2, 2, 1) M2S_IRF(2, 4, 1)
   M2S_IRF(4, 1, 1) M2S_IRF(4, 2, 1) M2S_IRF(4, 4, 1)
+  M2S_IRF(4, 1, 2) M2S_IRF(4, 4, 2)
 #undef M2S_IRF
   M2S_CHECK(false, "ir_pwdw: no variant for this shape");
 }

@@ -295,11 +295,32 @@ __global__ void __launch_bounds__(256) unpad_kernel(const T* __restrict__ x, lon
 
 inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 
+// fp8 engines: y = e4m3(lrelu(x)) for 8 bf16 per thread (the operand of the first e4m3 MRF conv of a stage)
+__global__ void __launch_bounds__(256) lrelu_e4m3_kernel(const uint4* __restrict__ x, uint2* __restrict__ y, long n8,
+                                                         float slope) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const uint4 u = x[i];
+  float v[8];
+  unpack_bf16x4(make_uint2(u.x, u.y), v);
+  unpack_bf16x4(make_uint2(u.z, u.w), v + 4);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * slope;
+  y[i] = e4m3x8(v);
+}
+
 }  // namespace
 
 template <typename T>
 void launch_unpad(const T* x, long rows, int C, int cs, float* y, hipStream_t s) {
   hipLaunchKernelGGL(unpad_kernel<T>, dim3(nblk(rows * C)), dim3(256), 0, s, x, rows, C, cs, y);
+  M2S_HIP(hipGetLastError());
+}
+
+void launch_lrelu_e4m3(const bf16_t* x, uint8_t* y, long n, float slope, hipStream_t s) {
+  M2S_CHECK(n % 8 == 0, "lrelu_e4m3: n % 8");
+  hipLaunchKernelGGL(lrelu_e4m3_kernel, dim3(nblk(n / 8)), dim3(256), 0, s, reinterpret_cast<const uint4*>(x),
+                     reinterpret_cast<uint2*>(y), n / 8, slope);
   M2S_HIP(hipGetLastError());
 }
 

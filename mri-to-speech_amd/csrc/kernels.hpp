@@ -33,7 +33,18 @@ void launch_se_mean(const float* psum, int N, int npb, int cs, float inv_count, 
 bool ir_fused_supported(int OH, int OW, int cs_in, int cs_mid, bool split);
 void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, const float* bpw, const void* wdw,
                     const float* bdw, int OH, int OW, int cs_mid, void* y, void* se_mean, bool split, double flops,
-                    double bytes, hipStream_t s);
+                    double bytes, hipStream_t s, bool f8_out = false);
+// f8_out (bf16 inputs and weights): the depthwise output y is stored as OCP e4m3 bytes [N][P][cs_mid]
+// (saturated to +-448), the operand of launch_se_gemm_f8; the SE means stay bf16 (exact sums).
+
+// fp8 engines: the SE-gated conv_pwl (+ bn3 + skip) of a stride-1 IR block on v_mfma_scale_f32_16x16x128_f8f6f4:
+// y (M, cs_out) bf16 = wscale[n] * sum_k w8[n][k] e4m3(gate[m / P][k] x8[m][k]) + bias[n] (+ res (M, cs_out) bf16).
+// x8: e4m3 (M, cs_in) (launch_ir_pwdw f8_out); w8: e4m3 [n_pad][kp], kp = cs_in rounded up to 128, zero
+// padded (pack_gemm_f8); gate: bf16 (M / P, cs_in).  P % 64 == 0, cs_out <= 224.  (gemm_f8.hip)
+bool se_gemm_f8_supported(int P, int cs_in, int cs_out);
+void launch_se_gemm_f8(const void* x8, int M, int P, int cs_in, const void* w8, int kp, int n_pad, const float* wscale,
+                       const float* bias, const void* gate, const void* res, void* y, int cs_out, hipStream_t s,
+                       double flops, double bytes);
 
 // The same for a stride-2 depthwise (TF-SAME, top / left pads pad_t / pad_l) on an IH x IW <= 256-pixel
 // conv_pw map: y (N, OH*OW, cs_mid), se_mean over the OH x OW output.  (ir_fused.hip)
@@ -176,6 +187,16 @@ void launch_conv_post(const T* x, int B, int L, int C, int cs, const float* w /*
 
 // y = a + b (fp32, n elements)
 void launch_add2(const float* a, const float* b, float* y, long n, hipStream_t s);
+// fp8 engines: y (n bytes, e4m3) = lrelu(x) for bf16 x, n % 8 == 0  (kernels.hip)
+void launch_lrelu_e4m3(const bf16_t* x, uint8_t* y, long n, float slope, hipStream_t s);
+// fp8 engines, HiFi-GAN MRF conv at C in {128, 256} (models.py:11-49, causal left pad (k - 1) dil): x8 e4m3
+// (B, L, C) already LeakyReLU'd; w8 e4m3 [C][k C] tap-major (pack_gemm_f8), per-channel scales; v = conv + bias
+// (+ res bf16); y bf16 = v, or with accum 1 / 2 the MRF running sum y + v / (y + v) / accum_div; y8 (e4m3) =
+// lrelu(v, slope8).  Either output may be null.  (gemm_f8.hip)
+bool conv1d_f8_supported(int C, int k);
+void launch_conv1d_f8(const void* x8, int B, int L, int C, int k, int dil, const void* w8, const float* wscale,
+                      const float* bias, const void* res, void* y, void* y8, float slope8, int accum, float accum_div,
+                      hipStream_t s, double flops, double bytes);
 
 // (rows, cs) T -> (rows, C) fp32 dense (debug taps)
 template <typename T>

@@ -189,6 +189,19 @@ __device__ __forceinline__ void il_st8(sp_t* x, long p, int cs, int c, const flo
   *reinterpret_cast<uint4*>(u + 32) = make_uint4(l0.x, l0.y, l1.x, l1.y);
 }
 
+// OCP e4m3fn storage (fp8 engines): 8 floats -> 8 bytes (v_cvt_pk_fp8_f32, round to nearest even),
+// finite values saturated to +-448 (the conversion has no saturating mode), NaN kept
+__device__ __forceinline__ float sat_e4m3(float x) { return x != x ? x : fminf(fmaxf(x, -448.f), 448.f); }
+__device__ __forceinline__ uint2 e4m3x8(const float* v) {
+  int q[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = __builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v[4 * h]), sat_e4m3(v[4 * h + 1]), 0, false);
+    q[h] = __builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v[4 * h + 2]), sat_e4m3(v[4 * h + 3]), r, true);
+  }
+  return make_uint2((uint32_t)q[0], (uint32_t)q[1]);
+}
+
 // bf16-path activations: one v_exp_f32 + one v_rcp_f32 (1 ulp) instead of an IEEE divide and
 // __expf's denormal-range fix-up (a compare + select + multiply per value); e^-x underflowing to
 // 0 or overflowing to inf gives silu = x or -0 as the exact function does.  These run in every

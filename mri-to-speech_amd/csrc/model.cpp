@@ -98,6 +98,9 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
     stem_w_ = arena_.add_vec(w9);
     stem_b_ = arena_.add_vec(bn.b);
   }
+  // fp8 engines run the bf16 kernels (and bf16 packings) except the stride-1 IR blocks' SE-gated conv_pwl,
+  // which gets an e4m3 copy for the block-scaled MFMA (gemm_f8.hip) below
+  const int pdt = dtype == M2S_DT_FP8 ? M2S_DT_BF16 : dtype;
   int cin = EFF_STEM;
   for (int s = 0; s < 6; ++s) {
     const StageDef& sdf = kStages[s];
@@ -112,18 +115,18 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
       const int k = sdf.k;
       auto conv2d_kxk = [&](PConv& pc, const std::string& wk, int ci, int co, const BN& bn) {
         const float* w = need(sd, wk, {co, ci, k, k}).data;
-        pc = make_pconv(KIND_CONV2D, ci, co, k * k, dtype);
+        pc = make_pconv(KIND_CONV2D, ci, co, k * k, pdt);
         pc.ks = k;
         pc.stride = b.stride;
         pc.macs_per_row = (double)co * ci * k * k;
-        pack_conv(arena_, dtype, pc, [&](int, int n, int t, int c) { return w[((size_t)n * ci + c) * k * k + t] * bn.a[n]; },
+        pack_conv(arena_, pdt, pc, [&](int, int n, int t, int c) { return w[((size_t)n * ci + c) * k * k + t] * bn.a[n]; },
                   [&](int n) { return bn.b[n]; });
       };
       auto conv1x1 = [&](PConv& pc, const std::string& wk, int ci, int co, const BN& bn) {
         const float* w = need(sd, wk, {co, ci, 1, 1}).data;
-        pc = make_pconv(KIND_GEMM, ci, co, 1, dtype);
+        pc = make_pconv(KIND_GEMM, ci, co, 1, pdt);
         pc.macs_per_row = (double)co * ci;
-        pack_conv(arena_, dtype, pc, [&](int, int n, int, int c) { return w[(size_t)n * ci + c] * bn.a[n]; },
+        pack_conv(arena_, pdt, pc, [&](int, int n, int, int c) { return w[(size_t)n * ci + c] * bn.a[n]; },
                   [&](int n) { return bn.b[n]; });
       };
       if (b.type == 0) {
@@ -202,7 +205,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
           b.er_wexp = arena_.add_vec(fe);
           b.er_wpwl = arena_.add_vec(fp);
           b.ers_sp = true;
-        } else if (dtype == M2S_DT_BF16 && b.stride == 1 && b.skip && k == 3 &&
+        } else if (pdt == M2S_DT_BF16 && b.stride == 1 && b.skip && k == 3 &&
             er_fused_supported(64, 64, cin, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
           // er_fused.hip operand orders: conv_exp [tap][n16][lane][8] (lane = (k8 group, row));
           // conv_pwl [n16][k-step][lane][8] with the k-slot permutation of the kernel's header
@@ -228,7 +231,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
           b.er_wexp = arena_.add_vec(fe);
           b.er_wpwl = arena_.add_vec(fp);
           b.er_frag = true;
-        } else if (dtype == M2S_DT_BF16 && b.stride == 1 && b.skip && k == 3 &&
+        } else if (pdt == M2S_DT_BF16 && b.stride == 1 && b.skip && k == 3 &&
                    er2_fused_supported(32, 32, b.c1.cs_in, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
           // er2_fused.hip stage stream [20][16 pieces][lane][8]: stages 0..17 = conv_exp k-step s (tap
           // s / 2, input channels 32 (s % 2) ..), piece = n16; stages 18 / 19 = conv_pwl k-steps 0..3 /
@@ -255,7 +258,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
                 }
           b.er_wexp = arena_.add_vec(st);
           b.er_frag = true;
-        } else if (dtype == M2S_DT_BF16 && b.stride == 2 && k == 3 &&
+        } else if (pdt == M2S_DT_BF16 && b.stride == 2 && k == 3 &&
                    ers2_fused_supported(8, 16, b.c1.cs_in, b.mid, chan_stride(b.cout), b.c1.kp, b.c2.kp)) {
           // ers2_fused.hip: conv_exp [k-step][n16][lane][8] (CIN 16: lane groups 0-1 tap 2s, 2-3 tap
           // 2s + 1; CIN 32: tap s), conv_pwl [n16][k-step][lane][8] with the permuted K
@@ -301,7 +304,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
         }
         b.dw_w = arena_.add_vec(w9);
         b.dw_b = arena_.add_vec(bd);
-        if (dtype == M2S_DT_BF16) {  // fused kernel: bf16 weight in the half matching the channel
+        if (pdt == M2S_DT_BF16) {  // fused kernel: bf16 weight in the half matching the channel
           std::vector<uint32_t> w2(w9.size());  // (v_dot2 against a (c, c+1) activation dword)
           for (size_t i = 0; i < w9.size(); ++i) {
             const uint32_t h = f2bf_host(w9[i]);
@@ -326,6 +329,15 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
         pack_conv(arena_, se_dt, b.se2, [&](int, int n, int, int c) { return w2[(size_t)n * rd + c]; },
                   [&](int n) { return b2[n]; });
         conv1x1(b.c2, q + "conv_pwl.weight", m, b.cout, fold_bn(sd, q + "bn3", b.cout));
+        if (dtype == M2S_DT_FP8 && b.stride == 1 && chan_stride(b.cout) <= 224) {
+          const float* wq = need(sd, q + "conv_pwl.weight", {b.cout, m, 1, 1}).data;
+          const BN bn3 = fold_bn(sd, q + "bn3", b.cout);
+          b.f8_kp = round_up(cs, 128);
+          b.f8_npad = std::max(round_up(chan_stride(b.cout), 64), chan_stride(b.cout) > 128 ? 224 : 128);
+          pack_gemm_f8(arena_, m, b.cout, b.f8_npad, b.f8_kp, [&](int n, int c) { return wq[(size_t)n * m + c] * bn3.a[n]; },
+                       [&](int n) { return bn3.b[n]; }, &b.f8_w, &b.f8_s, &b.f8_b);
+          b.f8_pwl = true;
+        }
       }
       blocks_.push_back(b);
       cin = sdf.cout;
@@ -471,7 +483,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
     same_pad(W, 3, 2, &ow, &pl);
     // stem + blocks.0 (two 3x3 ConvBnAct at stride 1: 32 -> 16, 16 -> 16 + skip) in one kernel
     constexpr bool SPL = std::is_same<T, sp_t>::value;
-    const bool front = ((std::is_same<T, bf16_t>::value && dtype_ == M2S_DT_BF16) || SPL) && stem_fused_ && !(probe && stop_after >= 0 && stop_after < 2) &&
+    const bool front = ((std::is_same<T, bf16_t>::value && (dtype_ == M2S_DT_BF16 || dtype_ == M2S_DT_FP8)) || SPL) && stem_fused_ && !(probe && stop_after >= 0 && stop_after < 2) &&
                        blocks_.size() >= 2 && blocks_[0].type == 0 && blocks_[0].stride == 1 && !blocks_[0].skip &&
                        blocks_[0].cout == 16 && blocks_[0].c1.cs_in == 32 && blocks_[0].c1.kp == 288 &&
                        blocks_[1].type == 0 && blocks_[1].stride == 1 && blocks_[1].skip && blocks_[1].cout == 16 &&
@@ -576,7 +588,8 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
       } else {
         const int cs = chan_stride(b.mid);
         constexpr bool SPL = std::is_same<T, sp_t>::value;
-        const bool FUSABLE = (std::is_same<T, bf16_t>::value && dtype_ == M2S_DT_BF16) || SPL;
+        const bool FUSABLE = (std::is_same<T, bf16_t>::value && (dtype_ == M2S_DT_BF16 || dtype_ == M2S_DT_FP8)) || SPL;
+        bool f8 = false;  // fp8 engine: e4m3 depthwise output -> the e4m3 SE GEMM
         // bf16 feeds the fused kernel bf16 depthwise taps (dword halves), split fp32 the fp32 taps
         const void* wdw = arena_.ptr(SPL ? b.dw_w : b.dw_w2);
         if (SPL && b.stride == 1 && ir_fused_ && ir_ws_ && ir_ws_supported(nh, nw, b.c1.cs_in, b.c1.kp, cs)) {
@@ -586,9 +599,10 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                        4.0 * nc * P * (b.c1.cs_in + cs), s);
         } else if (FUSABLE && b.stride == 1 && ir_fused_ && ir_fused_supported(nh, nw, b.c1.cs_in, cs, SPL)) {
           const double P = (double)nh * nw, es = SPL ? 4.0 : 2.0;
+          f8 = b.f8_pwl && se_gemm_f8_supported(nh * nw, cs, chan_stride(b.cout));
           launch_ir_pwdw(cur, nc, b.c1.cs_in, b.c1.kp, b.c1.w, b.c1.b, wdw, static_cast<const float*>(arena_.ptr(b.dw_b)),
                          nh, nw, cs, M2, se_mean, SPL, 2.0 * nc * P * b.mid * (b.c1.cin + 9),
-                         es * nc * P * (b.c1.cs_in + cs), s);
+                         nc * P * (es * b.c1.cs_in + (f8 ? 1.0 : es) * cs), s, f8);
         } else if (FUSABLE && b.stride == 2 && ir_fused_ && ir_fused_s2_supported(oh, ow, b.c1.cs_in, cs, SPL) &&
                    nh * nw <= 64) {
           const double Pi = (double)oh * ow, Po = (double)nh * nw, es = SPL ? 4.0 : 2.0;
@@ -632,6 +646,14 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         r2.act = ACT_SIGMOID;
         run_conv<T>(r2, b.se2, s);
         }
+        if (f8) {
+          const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
+          launch_se_gemm_f8(M2, nc * nh * nw, nh * nw, cs, arena_.ptr(b.f8_w), b.f8_kp, b.f8_npad,
+                            static_cast<const float*>(arena_.ptr(b.f8_s)), static_cast<const float*>(arena_.ptr(b.f8_b)),
+                            scale, b.skip ? cur : nullptr, nxt, chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
+                            rows * cs + 2.0 * rows * co * (b.skip ? 2.0 : 1.0) + (double)b.f8_npad * b.f8_kp +
+                                2.0 * nc * cs);
+        } else {
         ConvArgs p = conv_args(b.c2);
         p.x = M2;
         p.y = nxt;
@@ -641,6 +663,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         p.in_scale = scale;
         p.res = b.skip ? cur : nullptr;
         run_conv<T>(p, b.c2, s);
+        }
       }
       std::swap(cur, nxt);
       oh = nh;
@@ -733,7 +756,8 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
     : h_(h), dtype_(dtype), device_(device) {
   M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16 || dtype == M2S_DT_BF16X3 || dtype == M2S_DT_FP8, "bad dtype");
   M2S_CHECK(h.resblock == 1 || h.resblock == 2, "resblock must be 1 or 2");
-  // fp8 engines: e4m3 resblock (MRF) convs; conv_pre and the upsamplers stay bf16
+  // fp8 engines: e4m3 resblock (MRF) convs at C = 128 / 256; conv_pre, the upsamplers and the fused
+  // C = 32 / 64 ResBlock1 kernels stay bf16
   const int io_dt = dtype == M2S_DT_FP8 ? M2S_DT_BF16 : dtype;
   if (const char* e = std::getenv("M2S_MRF_FUSED")) mrf_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_MRF_BATCH")) mrf_batch_ = std::strcmp(e, "0") != 0;
@@ -799,7 +823,8 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
         return c;
       };
       const bool fsplit = dtype == M2S_DT_BF16X3;
-      const bool frag = (dtype == M2S_DT_BF16 || fsplit) && h.resblock == 1 &&
+      // (fp8 engines: the fused bf16 ResBlock1 at C = 32 / 64, e4m3 convs at the wider stages)
+      const bool frag = (dtype == M2S_DT_BF16 || dtype == M2S_DT_FP8 || fsplit) && h.resblock == 1 &&
                         rb1_fused_supported(co, chan_stride(co), kk, rb.dil.data(), (int)rb.dil.size(), kk * co, fsplit);
       auto mk_frag = [&](const std::string& name) {  // fragment order of mrf_fused.hip
         std::vector<float> wv = fold_wn(sd, name, {co, co, kk});
@@ -823,6 +848,18 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
                     }
                   }
         return arena_.add_vec(f);
+      };
+      // fp8: the C = 128 / 256 resblock convs as e4m3 bytes for conv1d_f8 (K = 128 block-scaled MFMA)
+      const bool q8 = dtype == M2S_DT_FP8 && h.resblock == 1 && !frag && conv1d_f8_supported(co, kk);
+      auto mk_q8 = [&](const std::string& name) {
+        std::vector<float> wv = fold_wn(sd, name, {co, co, kk});
+        const HostTensor& bv = need(sd, name + ".bias", {co});
+        RB::F8 f;
+        pack_gemm_f8(
+            arena_, kk * co, co, co, kk * co,
+            [&](int n, int kx) { return wv[((size_t)n * co + kx % co) * kk + kx / co]; },  // K = tap-major t C + c
+            [&](int n) { return bv.data[n]; }, &f.w, &f.s, &f.b);
+        return f;
       };
       bool halo = fsplit && h.resblock == 1 && !frag;
       for (size_t d = 0; d < rb.dil.size(); ++d) halo = halo && conv1d_halo_sp_supported(co, chan_stride(co), kk, rb.dil[d]);
@@ -855,6 +892,10 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
             rb.h1_off.push_back(mk_halo(q + ".convs1." + std::to_string(d)));
             rb.h2_off.push_back(mk_halo(q + ".convs2." + std::to_string(d)));
           }
+          if (q8) {
+            rb.q1.push_back(mk_q8(q + ".convs1." + std::to_string(d)));
+            rb.q2.push_back(mk_q8(q + ".convs2." + std::to_string(d)));
+          }
         } else {
           rb.c1.push_back(mk(q + ".convs." + std::to_string(d), rb.dil[d]));
         }
@@ -882,6 +923,12 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
     for (size_t o : rb.f2_off) rb.f2.push_back(static_cast<const bf16_t*>(arena_.ptr(o)));
     for (size_t o : rb.h1_off) rb.h1.push_back(static_cast<const bf16_t*>(arena_.ptr(o)));
     for (size_t o : rb.h2_off) rb.h2.push_back(static_cast<const bf16_t*>(arena_.ptr(o)));
+    for (auto* qv : {&rb.q1, &rb.q2})
+      for (RB::F8& f : *qv) {
+        f.wp = arena_.ptr(f.w);
+        f.sp = static_cast<const float*>(arena_.ptr(f.s));
+        f.bp = static_cast<const float*>(arena_.ptr(f.b));
+      }
   }
 }
 
@@ -944,7 +991,8 @@ void Vocoder::forward_from_norm(const float* mel_norm, const float* mean, const 
     run_t<float>(ln_buf, B, T, wav, ws, s);
 }
 
-int Vocoder::act_buffers() const { return dtype_ == M2S_DT_BF16X3 ? 5 + 3 * CONV_BATCH : 5; }
+// split: + the batched stages' per-resblock buffers; fp8: + one for the e4m3 pair outputs (run_t)
+int Vocoder::act_buffers() const { return dtype_ == M2S_DT_BF16X3 ? 5 + 3 * CONV_BATCH : dtype_ == M2S_DT_FP8 ? 6 : 5; }
 
 // Split-fp32 ResBlock1 stage with the resblocks batched (conv_gemm batch launches, grid.z = resblock):
 // X holds a0 = lrelu(x) (the upsampler's epilogue applied it), so no conv re-applies LeakyReLU to its
@@ -1037,6 +1085,7 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
   T* Hb[2] = {ws.take<T>(n), ws.take<T>(n)};
   T* T1 = ws.take<T>(n);
   T* S = ws.take<T>(n);
+  T* E8 = dtype_ == M2S_DT_FP8 ? ws.take<T>(n) : nullptr;  // fp8: e4m3 outputs of the C = 128 / 256 MRF pairs
   T* Bt[CONV_BATCH][3] = {};  // split: per resblock, c1 output and the pair outputs (ping-pong)
   if (SPL)
     for (int j = 0; j < CONV_BATCH; ++j)
@@ -1094,6 +1143,44 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
       continue;
     }
     s_act = false;
+    if (std::is_same<T, bf16_t>::value && !rbs_[i * nk].q1.empty()) {
+      // fp8 stage (C = 128 / 256): e4m3 operands.  X8 = e4m3(lrelu(x)) once; per pair, c1 stores only
+      // e4m3(lrelu(xt)) (its sole consumer is c2), c2 adds the bf16 residual and stores x (bf16, the next
+      // residual) and e4m3(lrelu(x)) (the next c1's operand); the last c2 accumulates the MRF sum in S.
+      const int C = up.cout;
+      const long nel = (long)B * L * C;
+      uint8_t* X8 = reinterpret_cast<uint8_t*>(T1);  // T1 (2 bytes / element) holds X8 and T8
+      uint8_t* T8 = X8 + nel;
+      uint8_t* H8[2] = {reinterpret_cast<uint8_t*>(E8), reinterpret_cast<uint8_t*>(E8) + nel};
+      {
+        ProfScope ps("lrelu_e4m3_kernel", 0.0, 3.0 * nel, s);
+        launch_lrelu_e4m3(reinterpret_cast<const bf16_t*>(X), X8, nel, 0.1f, s);
+      }
+      const double rows = (double)B * L;
+      for (int j = 0; j < nk; ++j) {
+        const RB& rb = rbs_[i * nk + j];
+        const int np = (int)rb.dil.size();
+        const bf16_t* cur = reinterpret_cast<const bf16_t*>(X);
+        const uint8_t* cur8 = X8;
+        for (int p = 0; p < np; ++p) {
+          const double fl = 2.0 * rows * C * C * rb.k, wb = (double)C * C * rb.k;
+          launch_conv1d_f8(cur8, B, L, C, rb.k, rb.dil[p], rb.q1[p].wp, rb.q1[p].sp, rb.q1[p].bp, nullptr, nullptr, T8,
+                           0.1f, 0, 1.f, s, fl, 2.0 * nel + wb);
+          if (p == np - 1) {
+            const int accum = j == 0 ? 0 : (j == nk - 1 ? 2 : 1);
+            launch_conv1d_f8(T8, B, L, C, rb.k, 1, rb.q2[p].wp, rb.q2[p].sp, rb.q2[p].bp, cur, S, nullptr, 0.f, accum,
+                             (float)nk, s, fl, nel * (1.0 + 2.0 + 2.0 + (accum ? 2.0 : 0.0)) + wb);
+          } else {
+            bf16_t* xo = reinterpret_cast<bf16_t*>(Hb[p & 1]);
+            launch_conv1d_f8(T8, B, L, C, rb.k, 1, rb.q2[p].wp, rb.q2[p].sp, rb.q2[p].bp, cur, xo, H8[p & 1], 0.1f, 0,
+                             1.f, s, fl, nel * (1.0 + 2.0 + 2.0 + 1.0) + wb);
+            cur = xo;
+            cur8 = H8[p & 1];
+          }
+        }
+      }
+      continue;
+    }
     for (int j = 0; j < nk; ++j) {
       const RB& rb = rbs_[i * nk + j];
       const T* hcur = X;

@@ -120,6 +120,10 @@ class Acoustic {
     size_t er_sp_w = 0;  // split fp32 er stride 1: er_sp_fused.hip stage stream
     bool er_sp = false;
     bool ers_sp = false;  // split fp32 er stride 2 (blocks.1.0): er_wexp / er_wpwl in [hi/lo] fragment order
+    // fp8 engines, ir conv_pwl: e4m3 bytes [f8_npad][f8_kp] of W / scale, per-channel scales, bias
+    size_t f8_w = 0, f8_s = 0, f8_b = 0;
+    int f8_kp = 0, f8_npad = 0;
+    bool f8_pwl = false;
   };
   template <typename T>
   void effnet_t(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe, int* probe_dims,
@@ -171,6 +175,14 @@ class Vocoder {
     // split resblock "1" at C in {64, 128}: conv1d_halo.hip fragment order
     std::vector<size_t> h1_off, h2_off;
     std::vector<const bf16_t*> h1, h2;
+    // fp8 resblock "1" at C in {128, 256}: e4m3 [C][k C] weights, scales, biases (conv1d_f8)
+    struct F8 {
+      size_t w = 0, s = 0, b = 0;
+      const void* wp = nullptr;
+      const float* sp = nullptr;
+      const float* bp = nullptr;
+    };
+    std::vector<F8> q1, q2;
   };
   m2s_hifigan_h h_;
   int dtype_, device_, hop_ = 1;

@@ -69,6 +69,36 @@ inline float e4m3_host(float x) {
 }
 
 
+// OCP e4m3fn bit pattern of a value on the e4m3 grid (e4m3_host output; -0 -> +0)
+inline uint8_t e4m3_bits_host(float v) {
+  if (v == 0.f) return 0;
+  const uint8_t sgn = v < 0.f ? 0x80 : 0;
+  const float a = std::fabs(v);
+  int e;
+  std::frexp(a, &e);
+  const int E = e - 1;  // a = 1.m x 2^E
+  if (E < -6) return sgn | (uint8_t)std::nearbyint(a / std::ldexp(1.f, -9));  // subnormal: m x 2^-9
+  return sgn | (uint8_t)((E + 7) << 3) | (uint8_t)std::nearbyint((a / std::ldexp(1.f, E) - 1.f) * 8.f);
+}
+
+// A 1x1 conv as e4m3 bytes for the K = 128 block-scaled MFMA (gemm_f8.hip): rows [n_pad][kp], kp = cin
+// rounded up to 128, w[n][c] / s[n] on the e4m3 grid with s[n] = amax_n / 448; scales and bias [n_pad].
+template <class Get, class Bias>
+inline void pack_gemm_f8(Arena& ar, int cin, int cout, int n_pad, int kp, Get get, Bias bias, size_t* w_off,
+                         size_t* s_off, size_t* b_off) {
+  std::vector<uint8_t> w((size_t)n_pad * kp, 0);
+  std::vector<float> sc(n_pad, 1.f), b(n_pad, 0.f);
+  for (int n = 0; n < cout; ++n) {
+    float amax = 0.f;
+    for (int c = 0; c < cin; ++c) amax = std::max(amax, std::fabs(get(n, c)));
+    if (amax > 0.f) sc[n] = amax / 448.f;
+    for (int c = 0; c < cin; ++c) w[(size_t)n * kp + c] = e4m3_bits_host(e4m3_host(get(n, c) / sc[n]));
+    b[n] = bias(n);
+  }
+  *w_off = ar.add_vec(w);
+  *s_off = ar.add_vec(sc);
+  *b_off = ar.add_vec(b);
+}
 
 inline PConv make_pconv(int kind, int cin, int cout, int ntaps, int dtype) {
   PConv p;
