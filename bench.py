@@ -45,8 +45,8 @@ SR = 11413
 # dense MFMA peaks (MI355X_MICROARCH.md): per ALGORITHMIC flop, so bf16x3 (three bf16 MFMAs per
 # product) peaks at a third of the bf16 rate
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "bf16x3": 2500.0 / 3,
-               # non-scaled v_mfma_f32_16x16x32_fp8_fp8 runs at the bf16 rate (MI355X_MICROARCH.md)
-               "fp8": 2500.0}
+               # e4m3 on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4: 2x bf16 (MI355X_MICROARCH.md)
+               "fp8": 5000.0}
 PEAK_HBM_GBS = 8000.0
 FP32_TOL = {"mel_norm": 1e-4, "mel_log": 5e-4, "wav": 2e-4}  # tests/test_gpu_configs.py
 PRECISION = {
@@ -54,11 +54,13 @@ PRECISION = {
               "BiLSTM/head/glue exact fp32",
     "fp32": "exact f32 MFMA products (v_mfma_f32_16x16x4_f32), fp32 storage",
     "bf16": "bf16 storage and operands, fp32 accumulate; BiLSTM/head/glue fp32",
-    "fp8": "e4m3 MFMA operands (per-output-channel weight scales) for the backbone and MRF convs, bf16 "
-           "storage, SE / conv_pre / upsamplers bf16; BiLSTM/head/glue fp32",
+    "fp8": "e4m3 storage + block-scaled e4m3 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, per-output-channel "
+           "weight scales) for the IR blocks' expanded maps and SE-gated conv_pwl GEMMs and the C=128/256 "
+           "MRF convs; the other convs (stem, EdgeResidual, IR expand/depthwise, C=32/64 MRF, upsamplers) "
+           "bf16; BiLSTM/head/glue fp32",
 }
 
-MFMA_KERNELS = ("conv_gemm_kernel", "conv_halo_kernel", "conv_igemm_kernel", "ir_pwdw", "lstm_persistent_kernel",
+MFMA_KERNELS = ("conv_gemm_kernel", "f8_gemm_kernel", "conv_halo_kernel", "conv_igemm_kernel", "ir_pwdw", "lstm_persistent_kernel",
                 "rb1_fused_kernel", "stem_b0_kernel", "se_excite_kernel", "er_fused_kernel", "er2_fused_kernel",
                 "ers2_fused_kernel")
 
@@ -67,6 +69,8 @@ def kernel_arith(name: str, dtype: str) -> str:
     """Arithmetic of a kernel in a run of `dtype`: the BiLSTM and its input projection are exact f32."""
     if name.startswith("lstm_persistent") or name.startswith("lstm_step") or "<float" in name:
         return "fp32"
+    if dtype == "fp8":  # only the e4m3 kernels run fp8 MFMA; the rest of an fp8 engine is bf16
+        return "fp8" if name.startswith("f8_gemm_kernel") else "bf16"
     return dtype
 
 
