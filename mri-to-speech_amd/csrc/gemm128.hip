@@ -1,31 +1,29 @@
-// e4m3 GEMMs of the fp8 engines (configs[4]) on the block-scaled MFMA v_mfma_scale_f32_16x16x128_f8f6f4
-// (2x the bf16 MFMA rate per clock; MI355X_MICROARCH.md Matrix cores), operands stored as OCP e4m3 bytes:
+// GEMMs over 128-byte K-step rows: one LDS row of an operand row per K step, filled by LDS-DMA through a
+// 3-slot ring.  Three kinds (one kernel template, gemm128_kernel<KIND, WM, WN, NT, S>):
 //
-// KIND_F8_SE (the IR blocks' SE-gated conv_pwl):
+// KIND_F8_SE (fp8 engines, the IR blocks' SE-gated conv_pwl), on the block-scaled MFMA
+//   v_mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate per clock; MI355X_MICROARCH.md Matrix cores),
+//   K step = 128 e4m3 channels:
 //   y[m][n] = wscale[n] * sum_k W8[n][k] * e4m3(gate[img(m)][k] * X8[m][k]) + bias[n] (+ res[m][n])
-// KIND_F8_C1D (the HiFi-GAN MRF convs at C = 128 / 256, models.py:11-49: causal dilated Conv1d, the operand
-// already LeakyReLU'd by its producer):
+// KIND_F8_C1D (fp8 engines, the HiFi-GAN MRF convs at C = 128 / 256, models.py:11-49: causal dilated
+//   Conv1d, the operand already LeakyReLU'd by its producer), same MFMA:
 //   v[m][n] = wscale[n] * sum_{t,c} W8[n][t C + c] * X8[b, l + t dil - (k - 1) dil][c] + bias[n] (+ res[m][n])
 //   y (bf16) = v, or the MRF running sum (y + v) [/ nk]; y8 (e4m3) = lrelu(v) for the next conv's operand.
+// KIND_SP_SE (bf16x3 engines, the same SE-gated conv_pwl in split fp32), K step = 32 channels as
+//   [hi 32 | lo 32] bf16 (the interleaved operand ir_ws / ir_pwdw write, m2s_common.hpp il_st8), three
+//   v_mfma_f32_16x16x32_bf16 terms per product (hi*hi + hi*lo + lo*hi), gate applied in fp32 and re-split:
+//   y[m][n] = sum_k W[n][k] * (gate[img(m)][k] * X[m][k]) + bias[n] (+ res[m][n]), all split fp32.
 //
 // The InvertedResidual tail of timm's EfficientNetV2 (se.conv_expand gate x conv_pwl + bn3 + skip;
-// mri_acoustic_model.py:28-34,46): X8 is the depthwise output the bf16 IR front half stored as OCP e4m3
-// bytes (ir_fused.hip f8_out), W8 the BN-folded conv_pwl weight on the e4m3 grid with a per-output-channel
-// scale (pack_conv_f8), gate the SE excitation (bf16).  Storing the expanded map in one byte halves the
-// bytes of the IR stage's largest HBM stream (the map is written once and read once per block).
-//
-// Tiling.  BM = 64 WM positions x BN = 16 NT WN output channels, 4 waves (WM x WN); every wave owns 64
-// rows that lie in ONE image (P % 64 == 0), so its 32 gate values per K step are the same for all of its
-// row fragments.  One K step = 128 channels = one 128-byte LDS row per operand row; S stages of
-// [BN weight rows | BM activation rows] are filled by LDS-DMA (global_load_lds_dwordx4: 8 rows = 1 KB per
-// wave instruction), retired by a counted s_waitcnt vmcnt and a barrier as in conv_gemm.hip.  The gate is
-// applied to the activation fragments in registers (e4m3 -> f32 pairs, multiply, e4m3; the gate is in
-// (0, 1), so no new saturation); the weights go to the MFMA as stored.  Unit E8M0 block scales: the
-// per-channel weight scale is applied in the epilogue.
+// mri_acoustic_model.py:28-34,46).  Every wave owns 64 rows that lie in ONE image (P % 64 == 0), so its gates
+// per K step are shared by its four row fragments and the gate is applied to the activation fragments in
+// registers (the gate is in (0, 1): no new saturation in e4m3).  The per-channel fp8 weight scale is applied
+// in the epilogue; the E8M0 block scales are 1.
 #include "conv_igemm.hpp"
 #include "kernels.hpp"
 #include "prof.hpp"
 
+#include <cstdlib>
 #include <cstring>
 
 namespace m2s {
@@ -45,6 +43,9 @@ __device__ __attribute__((aligned(16))) uint4 g_zero_f8[4];  // padding lanes' D
 // lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...; MI355X_MICROARCH.md LDS table) on 16 distinct
 // 16-byte bank quads for both reads (exhaustive check over the XOR swizzles of the row's low 4 bits).
 __device__ __forceinline__ int f8_swz(int r) { return ((r >> 1) & 1) | (r & 4); }
+// SP: a fragment reads chunks g (hi) and g + 4 (lo); f(r) = r & 6 is conflict-free for that pair (same check)
+template <bool SP>
+__device__ __forceinline__ int swz128(int r) { return SP ? (r & 6) : f8_swz(r); }
 
 __device__ __forceinline__ void dma16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, lds_wave_base, 16, 0, 0);
@@ -62,16 +63,16 @@ __device__ __forceinline__ int gate4(int d, const float* s) {
   return __builtin_amdgcn_cvt_pk_fp8_f32(hi[0] * s[2], hi[1] * s[3], r, true);
 }
 
-enum { KIND_F8_SE = 0, KIND_F8_C1D = 1 };
+enum { KIND_F8_SE = 0, KIND_F8_C1D = 1, KIND_SP_SE = 2 };
 
-struct F8Args {
-  const uint8_t* x;     // e4m3 [M][cs_in]
-  const uint8_t* w;     // e4m3 [n_pad][kp], zero beyond the input channels
+struct G128Args {
+  const uint8_t* x;     // e4m3 [M][cs_in]; SP: interleaved split [M][cs_in / 32][hi 32 | lo 32] bf16
+  const uint8_t* w;     // e4m3 [n_pad][kp], zero beyond the input channels; SP: bf16 rows [hi kp | lo kp]
   const float* wscale;  // [n_pad]
   const float* bias;    // [n_pad]
-  const bf16_t* gate;   // SE: [M / P][cs_in]
-  const bf16_t* res;    // [M][cs_out] or null
-  bf16_t* y;            // [M][cs_out] bf16 or null
+  const bf16_t* gate;   // SE: [M / P][cs_in] (SP: split [M / P][hi cs_in | lo cs_in])
+  const bf16_t* res;    // [M][cs_out] or null (SP: split [M][hi cs_out | lo cs_out])
+  bf16_t* y;            // [M][cs_out] bf16 or null (SP: split)
   uint8_t* y8;          // C1D: [M][cs_out] e4m3 of lrelu(v, slope8) or null
   int M, P, cs_in, kp, cs_out, n_tiles, nimg;  // P: SE rows per image, C1D sequence length L
   int dil, pad_left, accum;                     // C1D: tap dilation, causal left pad, MRF sum mode (0 / 1 / 2)
@@ -79,8 +80,9 @@ struct F8Args {
 };
 
 template <int KIND, int WM, int WN, int NT, int S>
-__global__ void __launch_bounds__(256, 1) f8_gemm_kernel(const F8Args a) {
-  constexpr bool SE = KIND == KIND_F8_SE;
+__global__ void __launch_bounds__(256, 1) gemm128_kernel(const G128Args a) {
+  constexpr bool SP = KIND == KIND_SP_SE;  // split fp32 operands, three bf16 MFMA terms
+  constexpr bool SE = KIND == KIND_F8_SE || SP;
   constexpr int BM = 64 * WM, BN = 16 * NT * WN, MT = 4;
   constexpr int A_BLK = BN / 8, TB = A_BLK + BM / 8;  // 8-row (1 KB) DMA blocks: weights, then activations
   static_assert(WM * WN == 4 && TB % 4 == 0, "bad tile");
@@ -100,7 +102,7 @@ __global__ void __launch_bounds__(256, 1) f8_gemm_kernel(const F8Args a) {
   const int wid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + orig / 8;
   const int mt = wid / a.n_tiles, nt = wid - mt * a.n_tiles;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int nsteps = a.kp / F8_ROW;
+  const int nsteps = SP ? a.kp / 32 : a.kp / F8_ROW;
   const int img0 = m0 / a.P;
 
   // ---- SE: gate table of the tile's images (fp32, zero past cs_in) ---------------------------------
@@ -108,7 +110,8 @@ __global__ void __launch_bounds__(256, 1) f8_gemm_kernel(const F8Args a) {
     for (int i = tid; i < a.nimg * a.kp; i += 256) {
       const int im = i / a.kp, k = i - im * a.kp;
       const int img = img0 + im;
-      gtab[i] = (k < a.cs_in && img * a.P < a.M) ? bf2f(a.gate[(size_t)img * a.cs_in + k]) : 0.f;
+      const bf16_t* gp = a.gate + (size_t)img * a.cs_in * (SP ? 2 : 1) + k;
+      gtab[i] = (k < a.cs_in && img * a.P < a.M) ? (SP ? bf2f(gp[0]) + bf2f(gp[a.cs_in]) : bf2f(gp[0])) : 0.f;
     }
     __syncthreads();
   }
@@ -127,15 +130,16 @@ __global__ void __launch_bounds__(256, 1) f8_gemm_kernel(const F8Args a) {
   for (int j = 0; j < PER; ++j) {
     const int blk = wave + 4 * j;
     const int lr = blk * 8 + lrow;  // LDS row within the slot
-    const int c = pch ^ f8_swz(lr & 15);
+    const int c = pch ^ swz128<SP>(lr & 15);
     cofs[j] = c * 16;
     lpos[j] = 0;
-    if (blk < A_BLK) {
-      srow[j] = a.w + (size_t)(n0 + lr) * a.kp + c * 16;
+    if (blk < A_BLK) {  // SP: hi chunks 0-3 from the row's hi half, lo chunks 4-7 from its lo half
+      srow[j] = SP ? a.w + (size_t)(n0 + lr) * a.kp * 4 + (c < 4 ? c * 16 : a.kp * 2 + (c - 4) * 16)
+                   : a.w + (size_t)(n0 + lr) * a.kp + c * 16;
     } else {
       const int m = m0 + lr - BN;
       if constexpr (SE) {
-        srow[j] = m < a.M ? a.x + (size_t)m * a.cs_in + c * 16 : nullptr;
+        srow[j] = m < a.M ? a.x + (size_t)m * a.cs_in * (SP ? 4 : 1) + c * 16 : nullptr;
       } else {
         const int l = m - (m / a.P) * a.P;
         lpos[j] = l - a.pad_left;
@@ -151,7 +155,9 @@ __global__ void __launch_bounds__(256, 1) f8_gemm_kernel(const F8Args a) {
       const int blk = wave + 4 * j;
       const void* src;
       if (blk < A_BLK) {
-        src = srow[j] + st * F8_ROW;
+        src = srow[j] + st * (SP ? 64 : F8_ROW);
+      } else if constexpr (SP) {
+        src = srow[j] ? static_cast<const void*>(srow[j] + st * F8_ROW) : static_cast<const void*>(zp);
       } else if constexpr (SE) {
         src = srow[j] && st * F8_ROW + cofs[j] < a.cs_in ? static_cast<const void*>(srow[j] + st * F8_ROW) : zp;
       } else {
@@ -170,9 +176,10 @@ __global__ void __launch_bounds__(256, 1) f8_gemm_kernel(const F8Args a) {
     for (int mi = 0; mi < MT; ++mi) acc[ni][mi] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int wimg = SE ? (min(m0 + wm * 64, a.M - 1)) / a.P - img0 : 0;  // this wave's image within the table
-  const uint32_t gaddr0 = (uint32_t)(uintptr_t)(gtab + wimg * a.kp + g * 32);
-  const int sw = f8_swz(r16);
-  const int ch0 = ((2 * g) ^ sw) << 4, ch1 = ((2 * g + 1) ^ sw) << 4;
+  const uint32_t gaddr0 = (uint32_t)(uintptr_t)(gtab + wimg * a.kp + g * (SP ? 8 : 32));
+  const int sw = swz128<SP>(r16);
+  // a lane's two 16-byte chunks of a fragment row: e4m3 2g, 2g + 1 (32 consecutive k); SP hi g, lo g + 4
+  const int ch0 = ((SP ? g : 2 * g) ^ sw) << 4, ch1 = ((SP ? g + 4 : 2 * g + 1) ^ sw) << 4;
 
   // LDS reads through inline asm: a plain ds_read after an LDS-DMA makes hipcc wait for every DMA in
   // flight (vmcnt(0)) before it, which would drain the pipeline each K step; the data dependence on the
@@ -183,6 +190,58 @@ __global__ void __launch_bounds__(256, 1) f8_gemm_kernel(const F8Args a) {
   const uint32_t b_lds0 = sm0 + (uint32_t)((BN + wm * 64 + r16) * F8_ROW);
   auto compute = [&](int st, int slot) {
     const uint32_t so = (uint32_t)(slot * SLOT);
+    if constexpr (SP) {
+      // 8 gates (k = 32 st + 8 g + j) and the MT activation fragments (hi chunk g, lo chunk g + 4 of a row)
+      f32x4 q0, q1;
+      u32x4 bh[MT], bl[MT];
+      const uint32_t ga = gaddr0 + st * 32 * 4, ba0 = b_lds0 + so + ch0, ba1 = b_lds0 + so + ch1;
+      asm volatile(
+          "ds_read_b128 %0, %10\n\tds_read_b128 %1, %10 offset:16\n\t"
+          "ds_read_b128 %2, %11\n\tds_read_b128 %3, %12\n\tds_read_b128 %4, %11 offset:2048\n\t"
+          "ds_read_b128 %5, %12 offset:2048\n\tds_read_b128 %6, %11 offset:4096\n\tds_read_b128 %7, %12 offset:4096\n\t"
+          "ds_read_b128 %8, %11 offset:6144\n\tds_read_b128 %9, %12 offset:6144\n\ts_waitcnt lgkmcnt(0)"
+          : "=&v"(q0), "=&v"(q1), "=&v"(bh[0]), "=&v"(bl[0]), "=&v"(bh[1]), "=&v"(bl[1]), "=&v"(bh[2]), "=&v"(bl[2]),
+            "=&v"(bh[3]), "=&v"(bl[3])
+          : "v"(ga), "v"(ba0), "v"(ba1)
+          : "memory");
+      static_assert(MT == 4, "the read statement above covers four 16-row fragments");
+      u32x4 ah[NT], al[NT];
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) {
+        const uint32_t aa = a_lds0 + so + ni * 16 * F8_ROW;
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3" : "=&v"(ah[ni]), "=&v"(al[ni]) : "v"(aa + ch0), "v"(aa + ch1) : "memory");
+      }
+      // gate in fp32 on hi + lo, re-split (17 significant bits kept)
+      const float gsc[8] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3]};
+      bf16x8 xh[MT], xl[MT];
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) {
+        float v[8], w[8];
+        unpack_bf16x4(make_uint2(bh[mi][0], bh[mi][1]), v);
+        unpack_bf16x4(make_uint2(bh[mi][2], bh[mi][3]), v + 4);
+        unpack_bf16x4(make_uint2(bl[mi][0], bl[mi][1]), w);
+        unpack_bf16x4(make_uint2(bl[mi][2], bl[mi][3]), w + 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (v[j] + w[j]) * gsc[j];
+        uint2 h0, l0, h1, l1;
+        split4(v, h0, l0);
+        split4(v + 4, h1, l1);
+        xh[mi] = __builtin_bit_cast(bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+        xl[mi] = __builtin_bit_cast(bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+      }
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) {
+        asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(ah[ni]), "+v"(al[ni]) : "n"(2 * (NT - 1 - ni)));
+        const bf16x8 wh = __builtin_bit_cast(bf16x8, ah[ni]), wl = __builtin_bit_cast(bf16x8, al[ni]);
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi) {
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xh[mi], acc[ni][mi], 0, 0, 0);
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xl[mi], acc[ni][mi], 0, 0, 0);
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xh[mi], acc[ni][mi], 0, 0, 0);
+        }
+      }
+      return;
+    }
     // the wave's 32 gates of this K step (k = 128 st + 32 g + j) and its MT activation fragments
     f32x4 q[8];
     u32x4 b0[MT], b1[MT];
@@ -276,14 +335,18 @@ __global__ void __launch_bounds__(256, 1) f8_gemm_kernel(const F8Args a) {
   // the skip operand is fetched for the whole tile first (one wait), not load -> wait -> store per piece
   const bf16_t* __restrict__ R = a.res;
   bf16_t* __restrict__ Y = a.y;
-  uint2 rv[MT][NT];
+  constexpr int RP = SP ? 2 : 1;  // planes of the residual / output rows
+  uint2 rv[MT][NT][RP];
 #pragma unroll
   for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NT; ++ni) {
       const int m = m0 + wm * 64 + mi * 16 + r16, n4 = n0 + wn * NT * 16 + ni * 16 + 4 * g;
-      rv[mi][ni] = (R && m < a.M && n4 < a.cs_out) ? *reinterpret_cast<const uint2*>(R + (size_t)m * a.cs_out + n4)
-                                                   : make_uint2(0u, 0u);
+#pragma unroll
+      for (int h = 0; h < RP; ++h)
+        rv[mi][ni][h] = (R && m < a.M && n4 < a.cs_out)
+                            ? *reinterpret_cast<const uint2*>(R + (size_t)m * a.cs_out * RP + h * a.cs_out + n4)
+                            : make_uint2(0u, 0u);
     }
 #pragma unroll
   for (int mi = 0; mi < MT; ++mi) {
@@ -293,10 +356,22 @@ __global__ void __launch_bounds__(256, 1) f8_gemm_kernel(const F8Args a) {
     for (int ni = 0; ni < NT; ++ni) {
       const int n4 = n0 + wn * NT * 16 + ni * 16 + 4 * g;
       if (n4 >= a.cs_out) continue;
-      const float4 ws = *reinterpret_cast<const float4*>(a.wscale + n4);
       const float4 bb = *reinterpret_cast<const float4*>(a.bias + n4);
       float r[4];
-      unpack_bf16x4(rv[mi][ni], r);
+      unpack_bf16x4(rv[mi][ni][0], r);
+      if constexpr (SP) {
+        float rl[4];
+        unpack_bf16x4(rv[mi][ni][RP - 1], rl);
+        const float v[4] = {acc[ni][mi][0] + bb.x + (r[0] + rl[0]), acc[ni][mi][1] + bb.y + (r[1] + rl[1]),
+                            acc[ni][mi][2] + bb.z + (r[2] + rl[2]), acc[ni][mi][3] + bb.w + (r[3] + rl[3])};
+        uint2 hi, lo;
+        split4(v, hi, lo);
+        bf16_t* yo = Y + (size_t)m * a.cs_out * 2 + n4;
+        *reinterpret_cast<uint2*>(yo) = hi;
+        *reinterpret_cast<uint2*>(yo + a.cs_out) = lo;
+        continue;
+      }
+      const float4 ws = *reinterpret_cast<const float4*>(a.wscale + n4);
       float v[4] = {fmaf(acc[ni][mi][0], ws.x, bb.x) + r[0], fmaf(acc[ni][mi][1], ws.y, bb.y) + r[1],
                     fmaf(acc[ni][mi][2], ws.z, bb.z) + r[2], fmaf(acc[ni][mi][3], ws.w, bb.w) + r[3]};
       const size_t o = (size_t)m * a.cs_out + n4;
@@ -319,25 +394,26 @@ __global__ void __launch_bounds__(256, 1) f8_gemm_kernel(const F8Args a) {
 }
 
 template <int KIND, int WM, int WN, int NT>
-void launch_tile(F8Args& a, hipStream_t s, double flops, double bytes) {
+void launch_tile(G128Args& a, hipStream_t s, double flops, double bytes) {
   constexpr int S = 3, BM = 64 * WM, BN = 16 * NT * WN;
-  const void* fn = reinterpret_cast<const void*>(&f8_gemm_kernel<KIND, WM, WN, NT, S>);
+  const void* fn = reinterpret_cast<const void*>(&gemm128_kernel<KIND, WM, WN, NT, S>);
   allow_lds(fn);
   a.n_tiles = ceil_div(a.cs_out, BN);
-  a.nimg = KIND != KIND_F8_SE ? 0 : BM % a.P == 0 ? BM / a.P : 1;  // SE: P % BM == 0 otherwise (checked)
+  const bool se = KIND != KIND_F8_C1D;
+  a.nimg = !se ? 0 : BM % a.P == 0 ? BM / a.P : 1;  // SE: P % BM == 0 otherwise (checked)
   const size_t lds = (size_t)S * (BN + BM) * F8_ROW + (size_t)a.nimg * a.kp * sizeof(float);
-  M2S_CHECK(lds <= 160 * 1024, "f8_gemm: LDS budget");
-  M2S_CHECK(KIND != KIND_F8_SE || BM % a.P == 0 || a.P % BM == 0, "se_gemm_f8: tile rows vs image size");
+  M2S_CHECK(lds <= 160 * 1024, "gemm128: LDS budget");
+  M2S_CHECK(!se || BM % a.P == 0 || a.P % BM == 0, "gemm128 SE: tile rows vs image size");
   const dim3 grid(ceil_div(a.M, BM) * a.n_tiles);
   char name[64];
-  snprintf(name, sizeof(name), "f8_gemm_kernel<%d, %d, %d, %d, %d>", KIND, WM, WN, NT, S);
+  snprintf(name, sizeof(name), "gemm128_kernel<%d, %d, %d, %d, %d>", KIND, WM, WN, NT, S);  // rocprof's symbol
   ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((f8_gemm_kernel<KIND, WM, WN, NT, S>), grid, dim3(256), lds, s, a);
+  hipLaunchKernelGGL((gemm128_kernel<KIND, WM, WN, NT, S>), grid, dim3(256), lds, s, a);
   M2S_HIP(hipGetLastError());
 }
 
-F8Args f8_args() {
-  F8Args a;
+G128Args g128_args() {
+  G128Args a;
   std::memset(&a, 0, sizeof(a));
   a.accum_div = 1.f;
   return a;
@@ -357,7 +433,7 @@ void launch_se_gemm_f8(const void* x8, int M, int P, int cs_in, const void* w8, 
   M2S_CHECK(x8 && w8 && wscale && bias && gate && y && y != res && y != x8, "se_gemm_f8: operand pointers");
   M2S_CHECK((double)M * cs_in < 4294967295.0, "se_gemm_f8: input too large");
   if (M <= 0) return;
-  F8Args a = f8_args();
+  G128Args a = g128_args();
   a.x = static_cast<const uint8_t*>(x8);
   a.w = static_cast<const uint8_t*>(w8);
   a.wscale = wscale;
@@ -389,7 +465,7 @@ void launch_conv1d_f8(const void* x8, int B, int L, int C, int k, int dil, const
             "conv1d_f8: operand pointers");
   M2S_CHECK(!accum || y, "conv1d_f8: the MRF sum needs y");
   M2S_CHECK((double)B * L * C < 2147483647.0, "conv1d_f8: input too large");
-  F8Args a = f8_args();
+  G128Args a = g128_args();
   a.x = static_cast<const uint8_t*>(x8);
   a.w = static_cast<const uint8_t*>(w8);
   a.wscale = wscale;
@@ -410,6 +486,37 @@ void launch_conv1d_f8(const void* x8, int B, int L, int C, int k, int dil, const
     launch_tile<KIND_F8_C1D, 4, 1, 8>(a, s, flops, bytes);  // 256 positions x 128 channels
   else
     launch_tile<KIND_F8_C1D, 2, 2, 8>(a, s, flops, bytes);  // 128 positions x 256 channels
+}
+
+bool se_gemm_sp_supported(int P, int cs_in, int cs_out) {
+  return P % 64 == 0 && cs_in % 32 == 0 && cs_out % 4 == 0 && cs_out <= 224 && (P % 256 == 0 || 256 % P == 0 || cs_out > 128);
+}
+
+void launch_se_gemm_sp(const void* x, int M, int P, int cs_in, const void* w, int n_pad, const float* bias,
+                       const void* gate, const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes) {
+  M2S_CHECK(se_gemm_sp_supported(P, cs_in, cs_out) && M % P == 0, "se_gemm_sp: unsupported shape");
+  M2S_CHECK(x && w && bias && gate && y && y != res && y != x, "se_gemm_sp: operand pointers");
+  M2S_CHECK((double)M * cs_in * 4 < 4294967295.0 * 4, "se_gemm_sp: input too large");
+  if (M <= 0) return;
+  G128Args a = g128_args();
+  a.x = static_cast<const uint8_t*>(x);
+  a.w = static_cast<const uint8_t*>(w);
+  a.bias = bias;
+  a.gate = static_cast<const bf16_t*>(gate);
+  a.res = static_cast<const bf16_t*>(res);
+  a.y = static_cast<bf16_t*>(y);
+  a.M = M;
+  a.P = P;
+  a.cs_in = cs_in;
+  a.kp = cs_in;  // weight rows [hi kp | lo kp] with kp = cs_in (conv_gemm's split packing)
+  a.cs_out = cs_out;
+  if (cs_out <= 128) {
+    M2S_CHECK(n_pad >= 128, "se_gemm_sp: weight rows");
+    launch_tile<KIND_SP_SE, 4, 1, 8>(a, s, flops, bytes);  // 256 x 128: 16x16 maps (one image per tile)
+  } else {
+    M2S_CHECK(n_pad >= 224, "se_gemm_sp: weight rows");
+    launch_tile<KIND_SP_SE, 2, 2, 7>(a, s, flops, bytes);  // 128 x 224: 8x8 maps (two images per tile)
+  }
 }
 
 }  // namespace m2s

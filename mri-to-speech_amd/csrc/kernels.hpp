@@ -40,11 +40,18 @@ void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, co
 // fp8 engines: the SE-gated conv_pwl (+ bn3 + skip) of a stride-1 IR block on v_mfma_scale_f32_16x16x128_f8f6f4:
 // y (M, cs_out) bf16 = wscale[n] * sum_k w8[n][k] e4m3(gate[m / P][k] x8[m][k]) + bias[n] (+ res (M, cs_out) bf16).
 // x8: e4m3 (M, cs_in) (launch_ir_pwdw f8_out); w8: e4m3 [n_pad][kp], kp = cs_in rounded up to 128, zero
-// padded (pack_gemm_f8); gate: bf16 (M / P, cs_in).  P % 64 == 0, cs_out <= 224.  (gemm_f8.hip)
+// padded (pack_gemm_f8); gate: bf16 (M / P, cs_in).  P % 64 == 0, cs_out <= 224.  (gemm128.hip)
 bool se_gemm_f8_supported(int P, int cs_in, int cs_out);
 void launch_se_gemm_f8(const void* x8, int M, int P, int cs_in, const void* w8, int kp, int n_pad, const float* wscale,
                        const float* bias, const void* gate, const void* res, void* y, int cs_out, hipStream_t s,
                        double flops, double bytes);
+
+// bf16x3 engines: the same SE-gated conv_pwl (+ bn3 + skip) in split fp32 on gemm128.hip: x interleaved split
+// (M, cs_in / 32, [hi 32 | lo 32]) (il_st8), w split rows [hi cs_in | lo cs_in] (conv_gemm packing, n_pad rows),
+// gate split (M / P, [hi cs_in | lo cs_in]), res / y split (M, [hi cs_out | lo cs_out]).  P % 64 == 0.
+bool se_gemm_sp_supported(int P, int cs_in, int cs_out);
+void launch_se_gemm_sp(const void* x, int M, int P, int cs_in, const void* w, int n_pad, const float* bias,
+                       const void* gate, const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes);
 
 // The same for a stride-2 depthwise (TF-SAME, top / left pads pad_t / pad_l) on an IH x IW <= 256-pixel
 // conv_pw map: y (N, OH*OW, cs_mid), se_mean over the OH x OW output.  (ir_fused.hip)
@@ -192,7 +199,7 @@ void launch_lrelu_e4m3(const bf16_t* x, uint8_t* y, long n, float slope, hipStre
 // fp8 engines, HiFi-GAN MRF conv at C in {128, 256} (models.py:11-49, causal left pad (k - 1) dil): x8 e4m3
 // (B, L, C) already LeakyReLU'd; w8 e4m3 [C][k C] tap-major (pack_gemm_f8), per-channel scales; v = conv + bias
 // (+ res bf16); y bf16 = v, or with accum 1 / 2 the MRF running sum y + v / (y + v) / accum_div; y8 (e4m3) =
-// lrelu(v, slope8).  Either output may be null.  (gemm_f8.hip)
+// lrelu(v, slope8).  Either output may be null.  (gemm128.hip)
 bool conv1d_f8_supported(int C, int k);
 void launch_conv1d_f8(const void* x8, int B, int L, int C, int k, int dil, const void* w8, const float* wscale,
                       const float* bias, const void* res, void* y, void* y8, float slope8, int accum, float accum_div,

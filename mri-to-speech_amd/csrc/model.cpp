@@ -85,6 +85,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_FUSED")) se_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER_FUSED")) er_fused_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_SE_SP")) se_sp_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_LSTM_PERSISTENT")) lstm_persistent_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_LSTM_MID")) lstm_mid_ = std::strcmp(e, "0") != 0;
   const std::string P = "cnn.backbone.";
@@ -99,7 +100,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
     stem_b_ = arena_.add_vec(bn.b);
   }
   // fp8 engines run the bf16 kernels (and bf16 packings) except the stride-1 IR blocks' SE-gated conv_pwl,
-  // which gets an e4m3 copy for the block-scaled MFMA (gemm_f8.hip) below
+  // which gets an e4m3 copy for the block-scaled MFMA (gemm128.hip) below
   const int pdt = dtype == M2S_DT_FP8 ? M2S_DT_BF16 : dtype;
   int cin = EFF_STEM;
   for (int s = 0; s < 6; ++s) {
@@ -653,6 +654,12 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                             scale, b.skip ? cur : nullptr, nxt, chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
                             rows * cs + 2.0 * rows * co * (b.skip ? 2.0 : 1.0) + (double)b.f8_npad * b.f8_kp +
                                 2.0 * nc * cs);
+        } else if (SPL && se_sp_ && se_gemm_sp_supported(nh * nw, cs, chan_stride(b.cout))) {
+          const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
+          launch_se_gemm_sp(M2, nc * nh * nw, nh * nw, cs, b.c2.w, b.c2.n_pad, b.c2.b, scale, b.skip ? cur : nullptr, nxt,
+                            chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
+                            4.0 * rows * cs + 4.0 * rows * co * (b.skip ? 2.0 : 1.0) + 4.0 * b.c2.n_pad * b.c2.kp +
+                                4.0 * nc * cs);
         } else {
         ConvArgs p = conv_args(b.c2);
         p.x = M2;

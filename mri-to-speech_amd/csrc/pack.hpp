@@ -81,7 +81,7 @@ inline uint8_t e4m3_bits_host(float v) {
   return sgn | (uint8_t)((E + 7) << 3) | (uint8_t)std::nearbyint((a / std::ldexp(1.f, E) - 1.f) * 8.f);
 }
 
-// A 1x1 conv as e4m3 bytes for the K = 128 block-scaled MFMA (gemm_f8.hip): rows [n_pad][kp], kp = cin
+// A 1x1 conv as e4m3 bytes for the K = 128 block-scaled MFMA (gemm128.hip): rows [n_pad][kp], kp = cin
 // rounded up to 128, w[n][c] / s[n] on the e4m3 grid with s[n] = amax_n / 448; scales and bias [n_pad].
 template <class Get, class Bias>
 inline void pack_gemm_f8(Arena& ar, int cin, int cout, int n_pad, int kp, Get get, Bias bias, size_t* w_off,
