@@ -24,6 +24,7 @@
 #include "prof.hpp"
 
 #include <cstdlib>
+#include <cstdlib>
 #include <cstring>
 
 namespace m2s {
@@ -80,13 +81,14 @@ struct G128Args {
 };
 
 template <int KIND, int WM, int WN, int NT, int S>
-__global__ void __launch_bounds__(256, 1) gemm128_kernel(const G128Args a) {
+__global__ void __launch_bounds__(64 * WM * WN, 1) gemm128_kernel(const G128Args a) {
+  constexpr int NW = WM * WN, NTHR = 64 * NW;  // 4 waves (one per SIMD) or 8 (two per SIMD)
   constexpr bool SP = KIND == KIND_SP_SE;  // split fp32 operands, three bf16 MFMA terms
   constexpr bool SE = KIND == KIND_F8_SE || SP;
   constexpr int BM = 64 * WM, BN = 16 * NT * WN, MT = 4;
   constexpr int A_BLK = BN / 8, TB = A_BLK + BM / 8;  // 8-row (1 KB) DMA blocks: weights, then activations
-  static_assert(WM * WN == 4 && TB % 4 == 0, "bad tile");
-  constexpr int PER = TB / 4;  // DMA instructions per wave per stage
+  static_assert((NW == 4 || NW == 8) && TB % NW == 0, "bad tile");
+  constexpr int PER = TB / NW;  // DMA instructions per wave per stage
   constexpr int SLOT = (BN + BM) * F8_ROW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* gtab = reinterpret_cast<float*>(smem + S * SLOT);  // [nimg][kp] gates of the tile's images
@@ -107,7 +109,7 @@ __global__ void __launch_bounds__(256, 1) gemm128_kernel(const G128Args a) {
 
   // ---- SE: gate table of the tile's images (fp32, zero past cs_in) ---------------------------------
   if constexpr (SE) {
-    for (int i = tid; i < a.nimg * a.kp; i += 256) {
+    for (int i = tid; i < a.nimg * a.kp; i += NTHR) {
       const int im = i / a.kp, k = i - im * a.kp;
       const int img = img0 + im;
       const bf16_t* gp = a.gate + (size_t)img * a.cs_in * (SP ? 2 : 1) + k;
@@ -128,7 +130,7 @@ __global__ void __launch_bounds__(256, 1) gemm128_kernel(const G128Args a) {
   int lpos[PER];             // C1D: position of tap 0 within the sequence (l - pad_left)
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    const int blk = wave + 4 * j;
+    const int blk = wave + NW * j;
     const int lr = blk * 8 + lrow;  // LDS row within the slot
     const int c = pch ^ swz128<SP>(lr & 15);
     cofs[j] = c * 16;
@@ -152,7 +154,7 @@ __global__ void __launch_bounds__(256, 1) gemm128_kernel(const G128Args a) {
     const int t = SE ? 0 : st / gpt, cg = SE ? st : st - t * gpt;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      const int blk = wave + 4 * j;
+      const int blk = wave + NW * j;
       const void* src;
       if (blk < A_BLK) {
         src = srow[j] + st * (SP ? 64 : F8_ROW);
@@ -408,7 +410,7 @@ void launch_tile(G128Args& a, hipStream_t s, double flops, double bytes) {
   char name[64];
   snprintf(name, sizeof(name), "gemm128_kernel<%d, %d, %d, %d, %d>", KIND, WM, WN, NT, S);  // rocprof's symbol
   ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((gemm128_kernel<KIND, WM, WN, NT, S>), grid, dim3(256), lds, s, a);
+  hipLaunchKernelGGL((gemm128_kernel<KIND, WM, WN, NT, S>), grid, dim3(64 * WM * WN), lds, s, a);
   M2S_HIP(hipGetLastError());
 }
 
@@ -510,9 +512,19 @@ void launch_se_gemm_sp(const void* x, int M, int P, int cs_in, const void* w, in
   a.cs_in = cs_in;
   a.kp = cs_in;  // weight rows [hi kp | lo kp] with kp = cs_in (conv_gemm's split packing)
   a.cs_out = cs_out;
+  static const int waves = [] {
+    const char* e = std::getenv("M2S_SE_SP_WAVES");
+    return e && std::atoi(e) == 4 ? 4 : 8;
+  }();
   if (cs_out <= 128) {
     M2S_CHECK(n_pad >= 128, "se_gemm_sp: weight rows");
-    launch_tile<KIND_SP_SE, 4, 1, 8>(a, s, flops, bytes);  // 256 x 128: 16x16 maps (one image per tile)
+    if (waves == 8)  // 256 x 128, two waves per SIMD (each gates its rows' fragments for its 64 columns)
+      launch_tile<KIND_SP_SE, 4, 2, 4>(a, s, flops, bytes);
+    else
+      launch_tile<KIND_SP_SE, 4, 1, 8>(a, s, flops, bytes);  // 256 x 128: 16x16 maps (one image per tile)
+  } else if (waves == 8) {
+    M2S_CHECK(n_pad >= 256, "se_gemm_sp: weight rows");
+    launch_tile<KIND_SP_SE, 2, 4, 4>(a, s, flops, bytes);  // 128 x 256 (224 used), two waves per SIMD
   } else {
     M2S_CHECK(n_pad >= 224, "se_gemm_sp: weight rows");
     launch_tile<KIND_SP_SE, 2, 2, 7>(a, s, flops, bytes);  // 128 x 224: 8x8 maps (two images per tile)
