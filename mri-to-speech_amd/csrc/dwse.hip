@@ -39,10 +39,19 @@ __global__ void __launch_bounds__(256) dwconv_kernel(const T* __restrict__ x, in
   __shared__ float red[DW_MAXG][DW_PL][DW_CB + 1];
   __shared__ __attribute__((aligned(16))) float wsm[10][DW_CB];  // 9 taps + bias
   const int cg = threadIdx.x % (DW_CB / 8), pl = threadIdx.x / (DW_CB / 8);
-  const int cb = blockIdx.x * DW_CB;
+  // XCD-aware work order: the hardware deals linear block ids round-robin over the 8 XCDs, so consecutive ids
+  // of one image's channel slices landed on different L2s; a slice is 32 channels = 64 B of a 128-byte line
+  // at split cs = 224, whose other half belongs to the neighbouring slice, and every L2 fetched the whole
+  // line (PMC: 2.1x the input bytes).  Here the slices (and pixel blocks) of one image share an XCD.
+  const int nwg = gridDim.x * gridDim.y * gridDim.z;
+  const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int xq = nwg / 8, xr = nwg % 8, xcd = lin % 8;
+  const int wid = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + lin / 8;
+  const int bx = wid % gridDim.x, byz = wid / gridDim.x, by = byz % gridDim.y, bz = byz / gridDim.y;
+  const int cb = bx * DW_CB;
   const int c0 = cb + cg * 8;
   const int P = OH * OW;
-  const int n0 = blockIdx.y * G, pb = blockIdx.z;
+  const int n0 = by * G, pb = bz;
   for (int i = threadIdx.x; i < 10 * DW_CB; i += 256) {
     const int t = i / DW_CB, c = cb + (i % DW_CB);
     wsm[t][i % DW_CB] = c < cs ? (t < 9 ? w9[(long)t * cs + c] : bias[c]) : 0.f;
@@ -146,7 +155,7 @@ __global__ void __launch_bounds__(256) dwconv_kernel(const T* __restrict__ x, in
     for (int j = 0; j < 8; ++j) red[g_cur][pl][cg * 8 + j] = s[j];
   }
   __syncthreads();
-  const int npb = gridDim.z;
+  const int npb = gridDim.z;  // (pb = bz above)
   for (int i = threadIdx.x; i < G * DW_CB; i += 256) {
     const int g = i / DW_CB, cl = i % DW_CB, c = cb + cl;
     if (c >= cs || n0 + g >= N) continue;
