@@ -155,3 +155,20 @@ def test_vocoder_bf16x3_mrf_batched(rt, monkeypatch, B, T):
     np.testing.assert_allclose(bat, per, atol=6e-5, rtol=0)
     assert np.abs(bat - ref).max() <= 1.5 * np.abs(per - ref).max() + 1e-5
 
+
+
+def test_effnet_bf16x3_se_gemm128_path(rt, ac_state, monkeypatch):
+    """The A/B split SE-gated conv_pwl (gemm128.hip KIND_SP_SE: 128-byte [hi|lo] K-step rows, gate applied to
+    the activation fragments in registers; engine switch M2S_SE_SP=1) holds every IR block's tap and the GAP
+    features to the fp32 bar at 7 frames (odd count: the 8x8 stage's last two-image tile is half empty)."""
+    monkeypatch.setenv("M2S_SE_SP", "1")
+    sd = {k: torch.from_numpy(v) for k, v in ac_state.items()}
+    fr = torch.from_numpy(synth.synth_frames(1, 7, seed=12)[0])
+    taps = []
+    effnet.effnet_features(sd, fr, taps=taps)
+    eng = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    x = fr.to(DEV)
+    for i in range(9, len(taps)):  # blocks.3.0 on: the IR blocks
+        got = eng.probe(x, i).cpu().numpy()
+        assert _rel(got, taps[i].numpy()) <= 1e-4, f"block {i}: rel err {_rel(got, taps[i].numpy())}"
+    assert _rel(eng.effnet(x).cpu().numpy(), effnet.effnet_gap(sd, fr).numpy()) <= 1e-4

@@ -40,6 +40,10 @@ def counters(d):
 def main(src, prefix):
     sha = open(os.path.join(src, "src_sha.txt")).read().strip()
     fe, wr = per_kernel(os.path.join(src, "fetch"), "FETCH_SIZE"), per_kernel(os.path.join(src, "write"), "WRITE_SIZE")
+    if os.path.isdir(os.path.join(src, "fetch8")):  # the fp8 engine's passes (8 x 1000 frames): its own kernels
+        for d, tgt, cn in (("fetch8", fe, "FETCH_SIZE"), ("write8", wr, "WRITE_SIZE")):
+            for k, v in per_kernel(os.path.join(src, d), cn).items():
+                tgt.setdefault(k, v)
     kern = {}
     for k in sorted(set(fe) | set(wr)):
         f_kib, nf = fe.get(k, (0.0, 0))

@@ -6,7 +6,7 @@ OUT=gpurun_out/${1:-dw}
 ROOT=$(pwd)
 mkdir -p "$OUT"
 export TMPDIR=/tmp STEPS=2
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "effnet or config" > "$OUT/pytest.log" 2>&1 \
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "effnet or config or gemm128" > "$OUT/pytest.log" 2>&1 \
   || { tail -30 "$OUT/pytest.log"; exit 1; }
 tail -1 "$OUT/pytest.log"
 (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$ROOT/$OUT/fetch" -o run -- \
