@@ -395,9 +395,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) gemm128_kernel(const G128Args
   }
 }
 
-template <int KIND, int WM, int WN, int NT>
+template <int KIND, int WM, int WN, int NT, int S = 3>
 void launch_tile(G128Args& a, hipStream_t s, double flops, double bytes) {
-  constexpr int S = 3, BM = 64 * WM, BN = 16 * NT * WN;
+  constexpr int BM = 64 * WM, BN = 16 * NT * WN;
   const void* fn = reinterpret_cast<const void*>(&gemm128_kernel<KIND, WM, WN, NT, S>);
   allow_lds(fn);
   a.n_tiles = ceil_div(a.cs_out, BN);
@@ -516,6 +516,7 @@ void launch_se_gemm_sp(const void* x, int M, int P, int cs_in, const void* w, in
     const char* e = std::getenv("M2S_SE_SP_WAVES");
     return e && std::atoi(e) == 4 ? 4 : 8;
   }();
+
   if (cs_out <= 128) {
     M2S_CHECK(n_pad >= 128, "se_gemm_sp: weight rows");
     if (waves == 8)  // 256 x 128, two waves per SIMD (each gates its rows' fragments for its 64 columns)
