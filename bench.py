@@ -60,7 +60,7 @@ PRECISION = {
            "bf16; BiLSTM/head/glue fp32",
 }
 
-MFMA_KERNELS = ("conv_gemm_kernel", "f8_gemm_kernel", "conv_halo_kernel", "conv_igemm_kernel", "ir_pwdw", "lstm_persistent_kernel",
+MFMA_KERNELS = ("conv_gemm_kernel", "gemm128_kernel", "conv_halo_kernel", "conv_igemm_kernel", "ir_pwdw", "lstm_persistent_kernel",
                 "rb1_fused_kernel", "stem_b0_kernel", "se_excite_kernel", "er_fused_kernel", "er2_fused_kernel",
                 "ers2_fused_kernel")
 
@@ -70,7 +70,7 @@ def kernel_arith(name: str, dtype: str) -> str:
     if name.startswith("lstm_persistent") or name.startswith("lstm_step") or "<float" in name:
         return "fp32"
     if dtype == "fp8":  # only the e4m3 kernels run fp8 MFMA; the rest of an fp8 engine is bf16
-        return "fp8" if name.startswith("f8_gemm_kernel") else "bf16"
+        return "fp8" if name.startswith(("gemm128_kernel<0", "gemm128_kernel<1")) else "bf16"
     return dtype
 
 
