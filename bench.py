@@ -60,9 +60,9 @@ PRECISION = {
            "bf16; BiLSTM/head/glue fp32",
 }
 
-MFMA_KERNELS = ("conv_gemm_kernel", "gemm128_kernel", "conv_halo_kernel", "conv_igemm_kernel", "ir_pwdw", "lstm_persistent_kernel",
-                "rb1_fused_kernel", "stem_b0_kernel", "se_excite_kernel", "er_fused_kernel", "er2_fused_kernel",
-                "ers2_fused_kernel")
+MFMA_KERNELS = ("conv_gemm_kernel", "gemm128_kernel", "conv_halo_kernel", "conv1d_halo", "conv_igemm_kernel", "ir_pwdw",
+                "ir_ws_kernel", "lstm_persistent_kernel", "rb1_fused_kernel", "stem_b0_kernel", "se_excite_kernel",
+                "er_fused_kernel", "er2_fused_kernel", "ers2_fused_kernel", "er_sp_kernel", "ers2_sp_kernel")
 
 
 def kernel_arith(name: str, dtype: str) -> str:

@@ -35,6 +35,12 @@ def test_roofline_picks_the_dominant_kernel_and_its_arithmetic():
     assert bench.kernel_arith("lstm_persistent_kernel", "bf16x3") == "fp32"
     assert bench.kernel_arith("conv_igemm_kernel<float, 2, 4, 3>", "bf16") == "fp32"
     assert bench.PEAK_TFLOPS[bench.kernel_arith("conv_gemm_kernel<1>", "bf16x3")] == pytest.approx(2500.0 / 3)
+    # fp8 engines: only the block-scaled e4m3 kernels (gemm128 KIND 0 / 1) are priced at the fp8 peak
+    assert bench.kernel_arith("gemm128_kernel<0, 4, 1, 8, 3>", "fp8") == "fp8"
+    assert bench.kernel_arith("gemm128_kernel<1, 2, 2, 8, 3>", "fp8") == "fp8"
+    assert bench.kernel_arith("ir_pwdw_kernel<4, 1, 2>", "fp8") == "bf16"
+    assert all(any(n.startswith(k) for k in bench.MFMA_KERNELS) for n in ("gemm128_kernel<2, 4, 2, 4, 3>", "er_sp_kernel<16>",
+                                                                       "ir_ws_kernel<16, 4>", "conv1d_halo_sp_kernel<64>", "ers2_sp_kernel<16>"))
     fl = (4e9 * 36 + 2e10 + 1e12) / (2 * 1920)
     assert r["plan_gflop_per_frame"] == pytest.approx(fl / 1e9, rel=1e-3)
 
