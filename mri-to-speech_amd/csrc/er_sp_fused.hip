@@ -71,7 +71,8 @@ struct ErSpArgs {
 
 // TH: tile rows (tile = TH x 16 output pixels); CSI: input channel stride (32 / 64); NT: mid channels / 16;
 // ON: output channel stride / 16 (the skip needs ON * 16 == CSI)
-template <int TH, int CSI, int NT, int ON, int NW>
+// MRG = 2: one ring slot carries a W_hi stage and its W_lo stage (half the barriers; needs NPS == 1).
+template <int TH, int CSI, int NT, int ON, int NW, int MRG>
 __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) er_sp_kernel(const ErSpArgs a) {
   constexpr int TW = 16, HW = TW + 2, HH = TH + 2, HPIX = HH * HW;
   constexpr int HPB = (HPIX + 63) / 64;          // 64-pixel DMA pieces per (plane, chunk)
@@ -80,12 +81,13 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) er_sp_kernel(const E
   constexpr int HBUF = 2 * CH * HPLANE;          // hi + lo planes
   constexpr int HP = 2 * CH * HPB / NW;          // halo pieces per wave
   static_assert((2 * CH * HPB) % NW == 0, "halo pieces must divide over the waves");
-  constexpr int PPW = (NT + NW - 1) / NW;        // ring pieces per wave per stage
+  constexpr int PPW = (MRG * NT + NW - 1) / NW;  // ring pieces per wave per stage
   constexpr int SLOT = PPW * NW * 1024;
   constexpr int KC = CSI / 32, NCE = 9 * KC * 2;  // conv_exp stages (k-step x plane)
   constexpr int MID = NT * 16, KS = MID / 32, PN = ON * KS;
   constexpr int NPS = (PN + NT - 1) / NT;        // conv_pwl stages per plane
-  constexpr int NST = NCE + 2 * NPS;
+  constexpr int NST = (NCE + 2 * NPS) / MRG;     // ring stages per tile
+  static_assert(MRG == 1 || (MRG == 2 && NPS == 1 && NCE % 2 == 0), "merged stages");
   constexpr int RPW = TH / NW;                   // output rows (16-pixel subtiles) per wave
   constexpr int ST = RPW * ON * 2;               // output stores per wave per tile
   static_assert(NT % 2 == 0 && ON * 16 == CSI && TH % NW == 0, "er_sp shape");
@@ -103,7 +105,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) er_sp_kernel(const E
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
       const int piece = wave * PPW + j;
-      const void* src = piece < NT ? (const void*)(a.wst + ((size_t)(ls * NT + piece) * 64 + lane) * 8) : (const void*)g_ersp_zero;
+      const void* src = piece < MRG * NT ? (const void*)(a.wst + ((size_t)(ls * MRG * NT + piece) * 64 + lane) * 8) : (const void*)g_ersp_zero;
       dma16(src, ring + slot * SLOT + piece * 1024);
     }
   };
@@ -178,8 +180,9 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) er_sp_kernel(const E
     for (int ks = 0; ks < 9 * KC; ++ks) {
       const int t = ks / KC, kc = ks - t * KC, ky = t / 3, kx = t - (t / 3) * 3;
       bf16x8 bh[RPW], bl[RPW];
+      const char* wsm = MRG == 2 ? begin_stage(ks) : nullptr;  // merged: W_hi pieces [0, NT), W_lo [NT, 2 NT)
       {
-        const char* ws = begin_stage(2 * ks);  // W_hi
+        const char* ws = MRG == 2 ? wsm : begin_stage(2 * ks);  // W_hi
 #pragma unroll
         for (int i = 0; i < RPW; ++i) {
           const int pix = (RPW * wave + i + ky) * HW + r16 + kx;
@@ -194,7 +197,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) er_sp_kernel(const E
         }
       }
       {
-        const char* ws = begin_stage(2 * ks + 1);  // W_lo
+        const char* ws = MRG == 2 ? wsm + NT * 1024 : begin_stage(2 * ks + 1);  // W_lo
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
           const bf16x8 af = frag(ws + nt * 1024);
@@ -233,11 +236,12 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) er_sp_kernel(const E
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
       for (int on = 0; on < ON; ++on) o[i][on] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* wpm = MRG == 2 ? begin_stage(NCE / 2) : nullptr;
 #pragma unroll
     for (int pl = 0; pl < 2; ++pl)
 #pragma unroll
       for (int ps = 0; ps < NPS; ++ps) {
-        const char* ws = begin_stage(NCE + pl * NPS + ps);
+        const char* ws = MRG == 2 ? wpm + pl * NT * 1024 : begin_stage(NCE + pl * NPS + ps);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
           const int j = ps * NT + nt;
@@ -276,16 +280,16 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) er_sp_kernel(const E
   wait_vm<0>();
 }
 
-template <int TH, int CSI, int NT, int ON, int NW>
+template <int TH, int CSI, int NT, int ON, int NW, int MRG>
 void launch_t(const ErSpArgs& a, const char* name, double flops, double bytes, hipStream_t s) {
-  constexpr int HW = 18, HPB = ((TH + 2) * HW + 63) / 64, CH = CSI / 8, PPW = (NT + NW - 1) / NW;
+  constexpr int HW = 18, HPB = ((TH + 2) * HW + 63) / 64, CH = CSI / 8, PPW = (MRG * NT + NW - 1) / NW;
   const size_t lds = 3 * (size_t)PPW * NW * 1024 + 2 * (size_t)(2 * CH * HPB * 1024) + NT * 16 * sizeof(float);
   M2S_CHECK(lds <= (NW == 4 ? 80 : 160) * 1024, "er_sp: LDS budget");
-  allow_lds(reinterpret_cast<const void*>(&er_sp_kernel<TH, CSI, NT, ON, NW>));
+  allow_lds(reinterpret_cast<const void*>(&er_sp_kernel<TH, CSI, NT, ON, NW, MRG>));
   const int cus = device_cus();
   const int grid = std::min(a.N * a.tiles_x * a.tiles_y, (NW == 4 ? 2 : 1) * cus);
   ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((er_sp_kernel<TH, CSI, NT, ON, NW>), dim3(grid), dim3(64 * NW), lds, s, a);
+  hipLaunchKernelGGL((er_sp_kernel<TH, CSI, NT, ON, NW, MRG>), dim3(grid), dim3(64 * NW), lds, s, a);
   M2S_HIP(hipGetLastError());
 }
 
@@ -305,7 +309,7 @@ int er_sp_nt_stages(int cs_in, int mid, int cs_out, int* nt) {
 }
 
 void launch_er_sp(const void* x, int N, int H, int W, int cs_in, int mid, int cs_out, const void* wst, const float* bexp,
-                  const float* bpwl, void* y, double flops, double bytes, hipStream_t s) {
+                  const float* bpwl, void* y, double flops, double bytes, hipStream_t s, bool merged) {
   M2S_CHECK(er_sp_supported(H, W, cs_in, mid, cs_out) && N > 0, "er_sp: unsupported shape");
   ErSpArgs a;
   a.x = static_cast<const bf16_t*>(x);
@@ -318,10 +322,12 @@ void launch_er_sp(const void* x, int N, int H, int W, int cs_in, int mid, int cs
   a.W = W;
   a.tiles_x = W / 16;
   a.tiles_y = H / tile_rows(cs_in);
-  if (cs_in == 32)
-    launch_t<16, 32, 8, 2, 8>(a, "er_sp_kernel<16, 32, 8, 2, 8>", flops, bytes, s);
+  if (cs_in == 32 && merged)
+    launch_t<16, 32, 8, 2, 8, 2>(a, "er_sp_kernel<16, 32, 8, 2, 8, 2>", flops, bytes, s);
+  else if (cs_in == 32)
+    launch_t<16, 32, 8, 2, 8, 1>(a, "er_sp_kernel<16, 32, 8, 2, 8, 1>", flops, bytes, s);
   else
-    launch_t<8, 64, 14, 4, 8>(a, "er_sp_kernel<8, 64, 14, 4, 8>", flops, bytes, s);
+    launch_t<8, 64, 14, 4, 8, 1>(a, "er_sp_kernel<8, 64, 14, 4, 8, 1>", flops, bytes, s);
 }
 
 }  // namespace m2s

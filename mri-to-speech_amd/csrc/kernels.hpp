@@ -119,8 +119,9 @@ void launch_er2_fused(const bf16_t* x, int N, int H, int W, const bf16_t* wst, c
 // (er_sp_fused.hip)
 bool er_sp_supported(int H, int W, int cs_in, int mid, int cs_out);
 int er_sp_nt_stages(int cs_in, int mid, int cs_out, int* nt);
+// merged: blocks.1's W_hi and W_lo stages share one ring slot (half the barriers, same MFMA order).
 void launch_er_sp(const void* x, int N, int H, int W, int cs_in, int mid, int cs_out, const void* wst, const float* bexp,
-                  const float* bpwl, void* y, double flops, double bytes, hipStream_t s);
+                  const float* bpwl, void* y, double flops, double bytes, hipStream_t s, bool merged = true);
 
 // bf16 stride-2 EdgeResidual (no skip), (cs_in, mid, cs_out) in {(16, 64, 32), (32, 128, 64)}: conv_exp
 // 3x3/s2 TF-SAME + SiLU -> conv_pwl; x (N,H,W,cs_in) -> y (N,OH,OW,cs_out); wexp ers2_exp_elems() bf16 in

@@ -86,6 +86,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_SE_FUSED")) se_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER_FUSED")) er_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_SP")) se_sp_ = std::strcmp(e, "0") != 0;  // A/B only
+  if (const char* e = std::getenv("M2S_ER_MRG")) er_mrg_ = std::strcmp(e, "0") != 0;  // A/B and tests only
   if (const char* e = std::getenv("M2S_LSTM_PERSISTENT")) lstm_persistent_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_LSTM_MID")) lstm_mid_ = std::strcmp(e, "0") != 0;
   const std::string P = "cnn.backbone.";
@@ -547,7 +548,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                  er_sp_supported(nh, nw, b.c1.cs_in, b.mid, chan_stride(b.cout))) {
         const double px = (double)nc * nh * nw;
         launch_er_sp(cur, nc, nh, nw, b.c1.cs_in, b.mid, chan_stride(b.cout), arena_.ptr(b.er_sp_w), b.c1.b, b.c2.b, nxt,
-                     2.0 * px * b.mid * (9.0 * b.cin + b.cout), 4.0 * px * (b.c1.cs_in + chan_stride(b.cout)), s);
+                     2.0 * px * b.mid * (9.0 * b.cin + b.cout), 4.0 * px * (b.c1.cs_in + chan_stride(b.cout)), s, er_mrg_);
       } else if (b.type == 1 && std::is_same<T, sp_t>::value && er_fused_ && b.ers_sp && b.stride == 2 &&
                  ers2_sp_supported(nh, nw, b.c1.cs_in, b.mid, chan_stride(b.cout))) {
         const double px = (double)nc * nh * nw;

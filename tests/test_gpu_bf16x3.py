@@ -131,6 +131,18 @@ def test_ir_ws_matches_grid_kernel(rt, ac_state, monkeypatch, hw, n):
     assert _rel(ws.effnet(fr).cpu().numpy(), grid.effnet(fr).cpu().numpy()) <= 1e-4
 
 
+def test_er_sp_merged_ring_stages_are_bit_identical(rt, ac_state, monkeypatch):
+    """er_sp_fused.hip MRG = 2 (blocks.1.1/.2: a W_hi stage and its W_lo stage share one ring slot, half
+    the barriers) issues the same MFMAs in the same order as one stage per slot (M2S_ER_MRG=0), so the
+    block outputs are equal bit for bit; 5 frames = several 16-row tiles per workgroup pass."""
+    fr = torch.from_numpy(synth.synth_frames(1, 5, seed=13)[0]).to(DEV)
+    merged = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    monkeypatch.setenv("M2S_ER_MRG", "0")
+    single = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    for i in (4, 5):  # after blocks.1.1, blocks.1.2
+        assert torch.equal(merged.probe(fr, i), single.probe(fr, i)), i
+
+
 @pytest.mark.parametrize("B,T", [(1, 5), (3, 17), (4, 40)])
 def test_vocoder_bf16x3_mrf_batched(rt, monkeypatch, B, T):
     """The batched split MRF stages (one launch per pair for every resblock, grid.z = resblock;
