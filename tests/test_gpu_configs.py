@@ -5,7 +5,7 @@
   configs[2]  1 clip x 30 frames end to end to the 11 413 Hz wav, fp32 and bf16x3
   configs[3]  the per-GPU share of 512 clips over 8 GPUs: 64 clips x 30 frames end to end in the
               bench dtype (bf16x3); 17 clips (every 4th and the last) against the fp32 oracle in one
-              batched oracle run (all 64 passed once: gpurun_out/cfg3.log), every clip against the bf16 path
+              batched oracle run (all 64 passed once: profiles/r03_cfg3_all64_oracle.txt), every clip against the bf16 path
   configs[4]  a 1000-frame clip end to end (bf16x3), the clip length of the fp8 config
 Tolerances (fp32 = the reference's precision): mel_norm <= 1e-4, mel_log <= 5e-4, wav <= 2e-4
 (1000 frames: mel_norm <= 2e-4 — fp32 summation order over 1000 recurrent steps); bf16:
