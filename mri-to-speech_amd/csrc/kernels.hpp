@@ -62,6 +62,14 @@ bool ir_ws_supported(int H, int W, int cs_in, int kp, int cs_mid);
 void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_mid, const void* wpw, const float* bpw,
                   const float* wdw, const float* bdw, void* y, void* se_mean, double flops, double bytes,
                   hipStream_t s);
+// Stride-2 IR front half on bands of 4 output rows (blocks.3.0: 32x32 -> 16x16), split fp32 or bf16: y =
+// the SE GEMM's operand (N, OH*OW, cs_mid; split: interleaved hi/lo), psum = squeeze partial sums
+// (N, OH / 4, cs_mid) for launch_se_mean.  wdw: fp32 tap-major [9][cs_mid].  (ir_s2band.hip)
+int ir_s2band_bands(int OH);
+bool ir_s2band_supported(int IH, int IW, int OH, int OW, int cs_in, int kp, int cs_mid);
+void launch_ir_s2band(const void* x, int N, int IH, int IW, int cs_in, int kp, const void* wpw, const float* bpw,
+                      const float* wdw, const float* bdw, int OH, int OW, int pad_t, int pad_l, int cs_mid, void* y,
+                      float* psum, bool split, double flops, double bytes, hipStream_t s);
 bool ir_fused_s2_supported(int IH, int IW, int cs_in, int cs_mid, bool split);
 void launch_ir_pwdw_s2(const void* x, int N, int cs_in, int kp, const void* wpw, const float* bpw, const void* wdw,
                        const float* bdw, int IH, int IW, int OH, int OW, int pad_t, int pad_l, int cs_mid, void* y,

@@ -87,6 +87,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_ER_FUSED")) er_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_SP")) se_sp_ = std::strcmp(e, "0") != 0;  // A/B only
   if (const char* e = std::getenv("M2S_ER_MRG")) er_mrg_ = std::strcmp(e, "0") != 0;  // A/B and tests only
+  if (const char* e = std::getenv("M2S_IR_S2BAND")) ir_s2band_ = std::strcmp(e, "0") != 0;  // A/B and tests only
   if (const char* e = std::getenv("M2S_LSTM_PERSISTENT")) lstm_persistent_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_LSTM_MID")) lstm_mid_ = std::strcmp(e, "0") != 0;
   const std::string P = "cnn.backbone.";
@@ -412,6 +413,7 @@ void Acoustic::effnet_dims(int H, int W, size_t* io, size_t* mid, size_t* se) co
     if (b.type == 2) {
       mmid = std::max(mmid, (size_t)oh * ow * chan_stride(b.mid));
       mse = std::max(mse, (size_t)dw_pixel_blocks(nh, nw) * chan_stride(b.mid));
+      if (b.stride == 2 && nh % 4 == 0) mse = std::max(mse, (size_t)ir_s2band_bands(nh) * chan_stride(b.mid));
     }
     mio = std::max(mio, (size_t)nh * nw * chan_stride(b.cout));
     oh = nh;
@@ -611,6 +613,14 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
           launch_ir_pwdw_s2(cur, nc, b.c1.cs_in, b.c1.kp, b.c1.w, b.c1.b, wdw, static_cast<const float*>(arena_.ptr(b.dw_b)),
                             oh, ow, nh, nw, qt, ql, cs, M2, se_mean, SPL, 2.0 * nc * b.mid * (Pi * b.c1.cin + Po * 9),
                             es * nc * (Pi * b.c1.cs_in + Po * cs), s);
+        } else if (FUSABLE && b.stride == 2 && ir_fused_ && ir_s2band_ &&
+                   ir_s2band_supported(oh, ow, nh, nw, b.c1.cs_in, b.c1.kp, cs)) {
+          const double Pi = (double)oh * ow, Po = (double)nh * nw, es = SPL ? 4.0 : 2.0;
+          launch_ir_s2band(cur, nc, oh, ow, b.c1.cs_in, b.c1.kp, b.c1.w, b.c1.b, static_cast<const float*>(arena_.ptr(b.dw_w)),
+                           static_cast<const float*>(arena_.ptr(b.dw_b)), nh, nw, qt, ql, cs, M2, sums, SPL,
+                           2.0 * nc * b.mid * (Pi * 1.125 * b.c1.cin + Po * 9), es * nc * (Pi * b.c1.cs_in + Po * cs), s);
+          ProfScope ps(tname<T>("se_mean_kernel"), 0.0, 4.0 * nc * cs * ir_s2band_bands(nh) + es * nc * cs, s);
+          launch_se_mean<T>(sums, nc, ir_s2band_bands(nh), cs, 1.0f / (float)(nh * nw), se_mean, s);
         } else {
         ConvArgs e = conv_args(b.c1);
         e.x = cur;

@@ -100,6 +100,7 @@ class Acoustic {
                             // scaling: the two measured equal, 7.85 vs 7.88 ms per step, profiles/r03o_se_sp_ab.txt)
   bool er_mrg_ = true;      // split EdgeResidual blocks.1: merged W_hi / W_lo ring stages (env M2S_ER_MRG=0: one per
                             // slot; 2088 vs 2164 us per launch, gpurun_out r03er)
+  bool ir_s2band_ = true;   // blocks.3.0: fused banded conv_pw + stride-2 depthwise (env M2S_IR_S2BAND=0: unfused)
   bool lstm_persistent_ = true;  // one-launch BiLSTM recurrence (env M2S_LSTM_PERSISTENT=0: a launch per step)
   bool lstm_mid_ = true;         // 4 < B <= 64: granule-exchange recurrence (env M2S_LSTM_MID=0: counter barrier)
   // (the M2S_* switches are read once, when the engine is created: A/B tests of fused vs unfused)

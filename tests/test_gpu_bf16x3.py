@@ -131,6 +131,28 @@ def test_ir_ws_matches_grid_kernel(rt, ac_state, monkeypatch, hw, n):
     assert _rel(ws.effnet(fr).cpu().numpy(), grid.effnet(fr).cpu().numpy()) <= 1e-4
 
 
+@pytest.mark.parametrize("n", [3, 37])
+def test_ir_s2band_matches_unfused(rt, ac_state, monkeypatch, n):
+    """blocks.3.0 as one banded kernel (ir_s2band.hip: conv_pw + stride-2 depthwise on 4-row bands, squeeze
+    partials per band) against the conv_pw GEMM + dwconv + se_mean sequence it replaces (M2S_IR_S2BAND=0)
+    and the fp32 oracle: the expanded activation stays fp32 in LDS instead of a hi/lo round trip, so the
+    two agree to the split rounding; both at the 1e-4 parity bar."""
+    sd = {k: torch.from_numpy(v) for k, v in ac_state.items()}
+    fr = torch.from_numpy(synth.synth_frames(1, n, seed=17)[0])
+    band = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    monkeypatch.setenv("M2S_IR_S2BAND", "0")
+    plain = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    x = fr.to(DEV)
+    for i in (9, 10):  # after blocks.3.0 (the banded block) and blocks.3.1 (its SE-gated output feeds it)
+        a, b = band.probe(x, i).cpu().numpy(), plain.probe(x, i).cpu().numpy()
+        assert np.isfinite(a).all() and _rel(a, b) <= 1e-4, (i, _rel(a, b))
+    if n <= 3:
+        taps = []
+        effnet.effnet_features(sd, fr, taps=taps)
+        assert _rel(band.probe(x, 9).cpu().numpy(), taps[9].numpy()) <= 1e-4
+    assert _rel(band.effnet(x).cpu().numpy(), plain.effnet(x).cpu().numpy()) <= 1e-4
+
+
 def test_er_sp_merged_ring_stages_are_bit_identical(rt, ac_state, monkeypatch):
     """er_sp_fused.hip MRG = 2 (blocks.1.1/.2: a W_hi stage and its W_lo stage share one ring slot, half
     the barriers) issues the same MFMAs in the same order as one stage per slot (M2S_ER_MRG=0), so the

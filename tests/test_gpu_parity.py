@@ -203,6 +203,25 @@ def test_effnet_bf16_ir_fused_every_block(rt, ac_state, monkeypatch, hw):
     assert _cos(ga, gb) >= 0.99999
 
 
+def test_effnet_bf16_ir_s2band_matches_unfused(rt, ac_state, monkeypatch):
+    """blocks.3.0 in bf16 as one banded kernel (ir_s2band.hip SP = 0) against conv_pw + dwconv + se_mean
+    (M2S_IR_S2BAND=0): the banded kernel keeps the expanded activation fp32 in LDS where the unfused
+    sequence stores it as bf16, so they agree to bf16 rounding; both at the bf16 cosine bar vs the oracle."""
+    sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
+    fr = torch.from_numpy(synth.synth_frames(1, 3, seed=19)[0])
+    taps = []
+    effnet.effnet_features(sd, fr, taps=taps)
+    band = rt.AcousticEngine(ac_state[1], dtype="bf16", device=DEV)
+    monkeypatch.setenv("M2S_IR_S2BAND", "0")
+    plain = rt.AcousticEngine(ac_state[1], dtype="bf16", device=DEV)
+    x = fr.to(DEV)
+    for i in (9, 10):
+        a, b = band.probe(x, i).float().cpu().numpy(), plain.probe(x, i).float().cpu().numpy()
+        assert np.isfinite(a).all() and _rel(a, b) <= 2e-2, (i, _rel(a, b))
+        assert _cos(a, taps[i].numpy()) >= 0.999, (i, _cos(a, taps[i].numpy()))
+    assert _cos(band.effnet(x).cpu().numpy(), plain.effnet(x).cpu().numpy()) >= 0.99999
+
+
 @pytest.mark.parametrize("env,blocks", [("M2S_STEM_FUSED", (2, 3, 6, -1)), ("M2S_SE_FUSED", (9, 14, 20, -1)), ("M2S_IR_FUSED", (9, 10, 18, 19, -1)),
                                         ("M2S_ER_FUSED", (3, 4, 5, 6, 7, 8, -1))])
 @pytest.mark.parametrize("hw", [(256, 256), (96, 80), (67, 101)])
