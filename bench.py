@@ -51,7 +51,7 @@ PEAK_HBM_GBS = 8000.0
 FP32_TOL = {"mel_norm": 1e-4, "mel_log": 5e-4, "wav": 2e-4}  # tests/test_gpu_configs.py
 PRECISION = {
     "bf16x3": "split fp32: bf16 hi+lo pairs (17-bit), 3 bf16 MFMA terms per product, fp32 accumulate; "
-              "BiLSTM/head/glue exact fp32",
+              "BiLSTM/head/glue fp32 (exact products)",
     "fp32": "exact f32 MFMA products (v_mfma_f32_16x16x4_f32), fp32 storage",
     "bf16": "bf16 storage and operands, fp32 accumulate; BiLSTM/head/glue fp32",
     "fp8": "e4m3 storage + block-scaled e4m3 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, per-output-channel "
@@ -66,7 +66,7 @@ MFMA_KERNELS = ("conv_gemm_kernel", "gemm128_kernel", "conv_halo_kernel", "conv1
 
 
 def kernel_arith(name: str, dtype: str) -> str:
-    """Arithmetic of a kernel in a run of `dtype`: the BiLSTM and its input projection are exact f32."""
+    """Arithmetic of a kernel in a run of `dtype`: the BiLSTM and its input projection are f32."""
     if name.startswith("lstm_persistent") or name.startswith("lstm_step") or "<float" in name:
         return "fp32"
     if dtype == "fp8":  # only the e4m3 kernels run fp8 MFMA; the rest of an fp8 engine is bf16
