@@ -25,6 +25,7 @@
 // divide and tanhf cost 7.51 against 7.18 us per recurrent step at 8 x 1000 (gpurun_out lstmfa0/1).
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "kernels.hpp"
 
@@ -48,6 +49,11 @@ struct LstmSync {
   unsigned err;        // set on a barrier timeout
 };
 
+// SC1: h_t is handed off write-through (sc1 stores, drained, then the counter add: no release fence) and every
+// load of it is an sc1 buffer load (no acquire fence) - cdna_hip_programming.md Guideline 16, the valid form
+// of MI355X_MICROARCH.md's table row 1 (one lane adds for the whole workgroup behind a barrier, one
+// workgroup per CU, hipMalloc'd memory); the buffer offsets are 32-bit, so SC1 needs B x T x H x 4 < 2^31.
+template <bool SC1>
 __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __restrict__ pre,
                                                                  const float* __restrict__ whh, float* hs,
                                                                  int Btot, int b0, int B, int T, LstmSync* sync,
@@ -112,7 +118,10 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
             break;
           }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if constexpr (SC1)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the poll
+        else
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
@@ -134,6 +143,9 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
         for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
       if (step > 0) {
         float hb[LP_BT][LP_KH];
+        // SC1: every load of h is a buffer load with sc1 (aux 16) through a descriptor at h[0][tprev]
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(hsd + (size_t)tprev * H), (short)0, (int)((size_t)B * T * H * 4), 0x00020000);
 #pragma unroll
         for (int j = 0; j < LP_BT; ++j) {
           const int b = (bt0 + j) * 32 + l32;
@@ -141,7 +153,13 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
 #pragma unroll
           for (int s = 0; s < LP_KH; s += 4) {
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (b < B) v = *reinterpret_cast<const float4*>(hr + s);
+            if constexpr (SC1) {
+              if (b < B)
+                v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rs, (int)(((size_t)b * T * H + kbase + s) * 4), 0, 16));
+            } else if (b < B) {
+              v = *reinterpret_cast<const float4*>(hr + s);
+            }
             hb[j][s] = v.x;
             hb[j][s + 1] = v.y;
             hb[j][s + 2] = v.z;
@@ -178,7 +196,11 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
         const float go = lstm_sig(prf[k][3] + gs[3]);
         const float c = step > 0 ? gf * cst[u][b] + gi * gg : gi * gg;
         cst[u][b] = c;
-        hsd[((size_t)b * T + t) * H + unit] = go * lstm_tanh(c);
+        const float h = go * lstm_tanh(c);
+        if constexpr (SC1)
+          __hip_atomic_store(&hsd[((size_t)b * T + t) * H + unit], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          hsd[((size_t)b * T + t) * H + unit] = h;
       }
       __syncthreads();  // red reused by the next B tiles
     }
@@ -187,8 +209,10 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (!SC1) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -576,14 +600,23 @@ void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B
   // workgroups at one per CU; check it against the occupancy query once.  (A plain launch has the
   // same residency as a cooperative one, which only adds this check - and crashes rocprofv3 7.x's
   // kernel tracer at process exit.)
-  const int resident = device_resident(reinterpret_cast<const void*>(&lstm_persistent_kernel), 256, 0);
+  const int resident = device_resident(reinterpret_cast<const void*>(&lstm_persistent_kernel<false>), 256, 0);
   M2S_CHECK(grid <= resident, "lstm_persistent: grid not co-resident on this device");
+  static const bool sc1_env = [] {  // opt-in (M2S_LSTM_SC1=1) until measured on the box: the fence form is the default
+    const char* e = std::getenv("M2S_LSTM_SC1");
+    return e && std::strcmp(e, "0") != 0;
+  }();
   LstmSync* sp = static_cast<LstmSync*>(sync);
   for (int b0 = 0; b0 < B; b0 += LP_BMAX) {  // c lives in LDS: at most LP_BMAX sequences per launch
     const int nb = std::min(LP_BMAX, B - b0);
     M2S_HIP(hipMemsetAsync(sync, 0, lstm_persistent_sync_bytes(), s));
-    hipLaunchKernelGGL(lstm_persistent_kernel, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, b0, nb, T, sp, spin_max,
-                       err_host);
+    const bool sc1 = sc1_env && (size_t)nb * T * H * 4 < (size_t)1 << 31;
+    if (sc1)
+      hipLaunchKernelGGL(lstm_persistent_kernel<true>, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, b0, nb, T, sp,
+                         spin_max, err_host);
+    else
+      hipLaunchKernelGGL(lstm_persistent_kernel<false>, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, b0, nb, T, sp,
+                         spin_max, err_host);
     M2S_HIP(hipGetLastError());
   }
 }
