@@ -25,7 +25,6 @@
 // divide and tanhf cost 7.51 against 7.18 us per recurrent step at 8 x 1000 (gpurun_out lstmfa0/1).
 #include <algorithm>
 #include <cstdlib>
-#include <cstring>
 
 #include "kernels.hpp"
 
@@ -49,11 +48,6 @@ struct LstmSync {
   unsigned err;        // set on a barrier timeout
 };
 
-// SC1: h_t is handed off write-through (sc1 stores, drained, then the counter add: no release fence) and every
-// load of it is an sc1 buffer load (no acquire fence) - cdna_hip_programming.md Guideline 16, the valid form
-// of MI355X_MICROARCH.md's table row 1 (one lane adds for the whole workgroup behind a barrier, one
-// workgroup per CU, hipMalloc'd memory); the buffer offsets are 32-bit, so SC1 needs B x T x H x 4 < 2^31.
-template <bool SC1>
 __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __restrict__ pre,
                                                                  const float* __restrict__ whh, float* hs,
                                                                  int Btot, int b0, int B, int T, LstmSync* sync,
@@ -94,16 +88,6 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
   for (int step = 0; step < T; ++step) {
     const int t = dir == 0 ? step : T - 1 - step;
     const int tprev = dir == 0 ? t - 1 : t + 1;
-    // this thread's gate pre-activations for the cell update (pairs p = tid + 256 k; B <= LP_BMAX = 64, so
-    // one B-tile pass), fetched before the barrier wait so their latency hides under it
-    float prf[2][4];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int p = tid + 256 * k, u = p % LP_U, b = p / LP_U;
-      const float* pr = pre + ((size_t)b * T + t) * 8 * H + (size_t)dir * 4 * H + ug * LP_U + u;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) prf[k][q] = b < B ? pr[q * H] : 0.f;
-    }
     if (step > 0) {
       // ---- wait until every workgroup of this direction published h_{t-1} -----------------
       if (tid == 0) {
@@ -118,10 +102,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
             break;
           }
         }
-        if constexpr (SC1)
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the poll
-        else
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
@@ -143,9 +124,6 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
         for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
       if (step > 0) {
         float hb[LP_BT][LP_KH];
-        // SC1: every load of h is a buffer load with sc1 (aux 16) through a descriptor at h[0][tprev]
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<float*>(hsd + (size_t)tprev * H), (short)0, (int)((size_t)B * T * H * 4), 0x00020000);
 #pragma unroll
         for (int j = 0; j < LP_BT; ++j) {
           const int b = (bt0 + j) * 32 + l32;
@@ -153,13 +131,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
 #pragma unroll
           for (int s = 0; s < LP_KH; s += 4) {
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if constexpr (SC1) {
-              if (b < B)
-                v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   rs, (int)(((size_t)b * T * H + kbase + s) * 4), 0, 16));
-            } else if (b < B) {
-              v = *reinterpret_cast<const float4*>(hr + s);
-            }
+            if (b < B) v = *reinterpret_cast<const float4*>(hr + s);
             hb[j][s] = v.x;
             hb[j][s + 1] = v.y;
             hb[j][s + 2] = v.z;
@@ -178,9 +150,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
         for (int i = 0; i < 16; ++i) red[wave][j][8 * (i / 4) + 4 * kk + (i % 4)][l32] = acc[j][i];
       __syncthreads();
       // ---- cell update: thread -> (unit, sequence) pairs of these B tiles ---------------------
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int p = tid + 256 * k;
+      for (int p = tid; p < LP_U * LP_BT * 32; p += 256) {
         const int u = p % LP_U, bl = p / LP_U, j = bl / 32, b = bt0 * 32 + bl;
         if (b >= B) continue;
         float gs[4];
@@ -190,17 +160,14 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
           gs[g] = (red[0][j][r][bl % 32] + red[1][j][r][bl % 32]) + (red[2][j][r][bl % 32] + red[3][j][r][bl % 32]);
         }
         const int unit = ug * LP_U + u;
-        const float gi = lstm_sig(prf[k][0] + gs[0]);
-        const float gf = lstm_sig(prf[k][1] + gs[1]);
-        const float gg = lstm_tanh(prf[k][2] + gs[2]);
-        const float go = lstm_sig(prf[k][3] + gs[3]);
+        const float* pr = pre + ((size_t)b * T + t) * 8 * H + (size_t)dir * 4 * H;
+        const float gi = lstm_sig(pr[unit] + gs[0]);
+        const float gf = lstm_sig(pr[H + unit] + gs[1]);
+        const float gg = lstm_tanh(pr[2 * H + unit] + gs[2]);
+        const float go = lstm_sig(pr[3 * H + unit] + gs[3]);
         const float c = step > 0 ? gf * cst[u][b] + gi * gg : gi * gg;
         cst[u][b] = c;
-        const float h = go * lstm_tanh(c);
-        if constexpr (SC1)
-          __hip_atomic_store(&hsd[((size_t)b * T + t) * H + unit], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          hsd[((size_t)b * T + t) * H + unit] = h;
+        hsd[((size_t)b * T + t) * H + unit] = go * lstm_tanh(c);
       }
       __syncthreads();  // red reused by the next B tiles
     }
@@ -209,10 +176,8 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        if constexpr (!SC1) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -600,23 +565,14 @@ void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B
   // workgroups at one per CU; check it against the occupancy query once.  (A plain launch has the
   // same residency as a cooperative one, which only adds this check - and crashes rocprofv3 7.x's
   // kernel tracer at process exit.)
-  const int resident = device_resident(reinterpret_cast<const void*>(&lstm_persistent_kernel<false>), 256, 0);
+  const int resident = device_resident(reinterpret_cast<const void*>(&lstm_persistent_kernel), 256, 0);
   M2S_CHECK(grid <= resident, "lstm_persistent: grid not co-resident on this device");
-  static const bool sc1_env = [] {  // opt-in (M2S_LSTM_SC1=1) until measured on the box: the fence form is the default
-    const char* e = std::getenv("M2S_LSTM_SC1");
-    return e && std::strcmp(e, "0") != 0;
-  }();
   LstmSync* sp = static_cast<LstmSync*>(sync);
   for (int b0 = 0; b0 < B; b0 += LP_BMAX) {  // c lives in LDS: at most LP_BMAX sequences per launch
     const int nb = std::min(LP_BMAX, B - b0);
     M2S_HIP(hipMemsetAsync(sync, 0, lstm_persistent_sync_bytes(), s));
-    const bool sc1 = sc1_env && (size_t)nb * T * H * 4 < (size_t)1 << 31;
-    if (sc1)
-      hipLaunchKernelGGL(lstm_persistent_kernel<true>, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, b0, nb, T, sp,
-                         spin_max, err_host);
-    else
-      hipLaunchKernelGGL(lstm_persistent_kernel<false>, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, b0, nb, T, sp,
-                         spin_max, err_host);
+    hipLaunchKernelGGL(lstm_persistent_kernel, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, b0, nb, T, sp, spin_max,
+                       err_host);
     M2S_HIP(hipGetLastError());
   }
 }
