@@ -38,7 +38,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "mri-to-speech_amd"))
 
 from m2s import synth  # noqa: E402
-from m2s.config import HIFIGAN_H  # noqa: E402
+from m2s.config import CNN_CHUNK, HIFIGAN_H  # noqa: E402
 
 HOP = 420
 SR = 11413
@@ -49,6 +49,8 @@ PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "bf16x3": 2500.0 / 3,
                "fp8": 5000.0}
 PEAK_HBM_GBS = 8000.0
 FP32_TOL = {"mel_norm": 1e-4, "mel_log": 5e-4, "wav": 2e-4}  # tests/test_gpu_configs.py
+# 1000-frame clips: fp32 summation order over 1000 recurrent steps (tests/test_gpu_configs4.py)
+LONG_TOL = {"mel_norm": 2e-4, "mel_log": 1e-3, "wav": 2e-4}
 PRECISION = {
     "bf16x3": "split fp32: bf16 hi+lo pairs (17-bit), 3 bf16 MFMA terms per product, fp32 accumulate; "
               "BiLSTM/head/glue fp32 (exact products)",
@@ -118,7 +120,8 @@ def parse(argv=None):
     p.add_argument("--frames", type=int, default=30, help="frames per clip")
     p.add_argument("--hw", type=int, default=256)
     p.add_argument("--dtype", default="bf16x3", choices=["bf16x3", "fp32", "bf16", "fp8"])
-    p.add_argument("--chunk", type=int, default=1920, help="frames per CNN pass (1920 = one pass over the 64x30 step)")
+    p.add_argument("--chunk", type=int, default=CNN_CHUNK,
+                   help="frames per CNN pass (default: the engine's shipped m2s.config.CNN_CHUNK = one pass over the 64x30 step)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-profile", action="store_true")
@@ -181,19 +184,20 @@ def cpu_threads():
     return (min(aff, omp) if omp > 0 else aff), aff
 
 
-def oracle_clip(ac_sd, gen_sd, mean, std, frames_np):
+def oracle_clip(ac_sd, gen_sd, mean, std, frames_np, cnn_chunk=64):
     sys.path.insert(0, REPO)
     from oracle import pipeline
     t = lambda sd: {k: torch.from_numpy(v) for k, v in sd.items()}  # noqa: E731
-    return pipeline.e2e(t(ac_sd), t(gen_sd), HIFIGAN_H, frames_np, mean, std)
+    return pipeline.e2e(t(ac_sd), t(gen_sd), HIFIGAN_H, frames_np, mean, std, cnn_chunk=cnn_chunk)
 
 
-def parity_vs(ref, out, clip=0):
+def parity_vs(ref, out, clip=0, tol=None):
+    tol = tol or FP32_TOL
     got = {k: out[k][clip:clip + 1].float().cpu().numpy() for k in ("mel_norm", "mel_log", "wav")}
     w, rw = got["wav"].astype(np.float64), ref["wav"].astype(np.float64)
     res = {f"{k}_max_abs": float(np.abs(got[k] - ref[k]).max()) for k in got}
     res["wav_snr_db"] = round(float(10 * np.log10(np.sum(rw ** 2) / max(np.sum((w - rw) ** 2), 1e-30))), 2)
-    res["within_fp32_tol"] = all(res[f"{k}_max_abs"] <= t for k, t in FP32_TOL.items())
+    res["within_fp32_tol"] = all(res[f"{k}_max_abs"] <= t for k, t in tol.items())
     return res
 
 
@@ -237,7 +241,7 @@ def cpu_baseline(args, ac_sd, gen_sd, mean, std):
                       f"{threads} threads (sched_getaffinity {aff}, OMP_NUM_THREADS cap)"}
 
 
-def long_clip_lines(args, build, device, sync, world, clips=8, frames=1000, steps=3):
+def long_clip_lines(args, build, device, sync, world, ref_args, clips=8, frames=1000, steps=3):
     """configs[4]'s shape on this GPU: 8 clips x 1000 frames (its per-GPU share of >= 1000-frame clips),
     end to end, in fp8 (its precision: e4m3 backbone / MRF convs), bf16x3 and bf16, with the fp8 run's
     dominant-kernel roofline from the HIP-event pass.  Frames resident in HBM, same timing rules as the
@@ -245,14 +249,22 @@ def long_clip_lines(args, build, device, sync, world, clips=8, frames=1000, step
     from m2s import _native
     x = make_frames(clips, frames, args.hw, 0, device)
     res = {"workload": f"e2e rtMRI->wav, {clips} clips x {frames} frames at {args.hw}x{args.hw} (configs[4] per-GPU)"}
+    ref0 = None
+    if not args.no_parity:  # clip 0 of this batch through the fp32 oracle, outside every timed loop
+        torch.set_num_threads(cpu_threads()[0])
+        ref0 = oracle_clip(*ref_args, x[:1].cpu().numpy(), cnn_chunk=100)
     for dt in ("fp8", "bf16x3", "bf16"):
         p = build(dt)
-        for _ in range(1):
-            p.forward(x)
+        out = p.forward(x)
         el = timed_loop(lambda: p.forward(x), steps, world, sync, device)
         p.ac.check()
         line = {"value": round(clips * frames * steps / el, 2), "ms_per_step": round(1000.0 * el / steps, 2),
                 "rtf": round(el / (clips * frames * steps * HOP / SR), 6), "steps": steps}
+        if ref0 is not None:  # the warm-up call's outputs (same inputs, same engine as the timed steps)
+            line["parity"] = dict(parity_vs(ref0, out, tol=LONG_TOL), **cosine_vs(ref0, out), clip=0,
+                                  tolerance=LONG_TOL if dt == "bf16x3" else "cosine >= 0.99",
+                                  reference="fp32 CPU oracle")
+        del out
         if dt == "fp8":
             _native.prof_enable(True)
             timed_loop(lambda: p.forward(x), steps, world, sync, device)
@@ -380,13 +392,13 @@ def main():
         result["parity"] = dict(parity_vs(ref0, out), clip=0, tolerance=FP32_TOL, reference="fp32 CPU oracle")
     if world == 1 and not args.no_compare:  # secondary lines: the narrower dtypes on the same workload
         del pipe
-        for dt in ("bf16", "fp8"):
+        for dt in ("bf16", "fp8", "fp32"):
             if dt == args.dtype:
                 continue
             p2 = build(dt)
             for _ in range(args.warmup):
                 step(p2)
-            k = max(5, args.steps // 2)
+            k = 5 if dt == "fp32" else max(5, args.steps // 2)  # exact f32: ~0.2 s per step
             el = timed_loop(lambda: step(p2), k, world, sync, device)
             result[dt] = {"value": round(B * T * k / el, 2), "ms_per_step": round(1000.0 * el / k, 3), "steps": k,
                           "precision": PRECISION[dt]}
@@ -394,7 +406,7 @@ def main():
                 result[dt]["parity"] = dict(parity_vs(ref0, out), **cosine_vs(ref0, out))
             del p2
     if world == 1 and not args.no_long and not (args.clips == 8 and args.frames == 1000):
-        result["configs4"] = long_clip_lines(args, build, device, sync, world)
+        result["configs4"] = long_clip_lines(args, build, device, sync, world, (ac_sd, gen_sd, mean, std))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, ac_sd, gen_sd, mean, std)
     if rank == 0:

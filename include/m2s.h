@@ -48,10 +48,11 @@ enum m2s_status { M2S_OK = 0, M2S_E_ARG = 1, M2S_E_HIP = 2, M2S_E_STATE = 3, M2S
  *   M2S_DT_BF16X3 split fp32: every activation / weight is a bf16 pair hi + lo (17 significant
  *                 bits), products are the three bf16 MFMA terms hi*hi + hi*lo + lo*hi with fp32
  *                 accumulation; meets the fp32 tolerances of the parity tests
- *   M2S_DT_FP8    e4m3 operands (configs[4]): the backbone convs and the MRF resblock convs run
- *                 v_mfma_f32_16x16x32_fp8_fp8 on OCP e4m3fn weights with per-output-channel fp32
- *                 scales and activations rounded to e4m3 at the operand read; bf16 storage, SE
- *                 excitation, conv_pre / upsamplers and conv_post stay bf16 (ABI 3) */
+ *   M2S_DT_FP8    configs[4]: OCP e4m3 storage and block-scaled e4m3 MFMA
+ *                 (v_mfma_scale_f32_16x16x128_f8f6f4, unit E8M0 block scales, per-output-channel
+ *                 fp32 weight scales applied in the epilogue) for the IR blocks' expanded maps and
+ *                 SE-gated conv_pwl GEMMs and the C = 128 / 256 MRF convs; every other conv is the
+ *                 bf16 path */
 enum m2s_dtype { M2S_DT_F32 = 0, M2S_DT_BF16 = 1, M2S_DT_BF16X3 = 2, M2S_DT_FP8 = 3 };
 /* host tensor element types */
 enum m2s_elem { M2S_ELEM_F32 = 0, M2S_ELEM_I64 = 1 };
@@ -80,7 +81,7 @@ typedef struct m2s_acoustic m2s_acoustic;
 int m2s_acoustic_create(const m2s_tensor* sd, int n, int n_mels, int rnn_hidden, int dtype, int device,
                         m2s_acoustic** out);
 void m2s_acoustic_destroy(m2s_acoustic* m);
-/* frames per CNN pass (bounds the CNN workspace); default 256 */
+/* frames per CNN pass (bounds the CNN workspace); default 1920 (= m2s.config.CNN_CHUNK, the size bench.py times) */
 int m2s_acoustic_set_chunk(m2s_acoustic* m, int frames);
 /* Asynchronous failure report.  The persistent BiLSTM waits at a grid barrier once per time step;
  * a wait that exceeds its poll limit (workgroups not co-resident) poisons the outputs with NaN and
@@ -128,14 +129,15 @@ typedef struct m2s_hifigan_h {
 } m2s_hifigan_h;
 
 typedef struct m2s_vocoder m2s_vocoder;
-/* Packs a Generator state dict (weight_g/weight_v or plain weight after remove_weight_norm).
- * Strict like load_state_dict(ckpt['generator']): a missing key is M2S_E_ARG.  Synchronous. */
+
 /* Frame preprocessing after the host decode (replaces _preprocess_frame,
  * run_mri_video_inference.py:34-54, except the cv2.resize): frames uint8 (n,h,w) grey
  * (channels = 1) or (n,h,w,3) BGR (channels = 3) -> out (n,h,w) fp32, per frame z-score then
  * min-max to [0, 1]; a constant frame gives zeros.  Device pointers, stream-ordered. */
 int m2s_preprocess_frames(const uint8_t* frames, int n, int h, int w, int channels, float* out, void* stream);
 
+/* Packs a Generator state dict (weight_g/weight_v or plain weight after remove_weight_norm).
+ * Strict like load_state_dict(ckpt['generator']): a missing key is M2S_E_ARG.  Synchronous. */
 int m2s_vocoder_create(const m2s_tensor* sd, int n, const m2s_hifigan_h* h, int dtype, int device, m2s_vocoder** out);
 void m2s_vocoder_destroy(m2s_vocoder* v);
 size_t m2s_vocoder_workspace_bytes(const m2s_vocoder* v, int B, int T);

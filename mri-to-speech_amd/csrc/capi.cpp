@@ -271,6 +271,7 @@ int m2s_cam_bn_channels(const m2s_cam* c, int layer) {
 
 size_t m2s_cam_workspace_bytes(const m2s_cam* c, int N, int H, int W) {
   size_t r = 0;
+  if (!c) return 0;  // like the other size queries: 0 for a null handle
   guarded([&] { r = c->impl.workspace_bytes(N, H, W); });
   return r;
 }

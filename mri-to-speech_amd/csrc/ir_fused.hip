@@ -427,7 +427,7 @@ void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, co
   M2S_IRF(1, 1, 1) M2S_IRF(1, 2, 1) M2S_IRF(1, 4, 1)
   M2S_IRF(2, 1, 1) M2S_IRF(2, 2, 1) M2S_IRF(2, 4, 1)
   M2S_IRF(4, 1, 1) M2S_IRF(4, 2, 1) M2S_IRF(4, 4, 1)
-  M2S_IRF(4, 1, 2) M2S_IRF(4, 4, 2)
+  M2S_IRF(4, 1, 2) M2S_IRF(4, 2, 2) M2S_IRF(4, 4, 2)
 #undef M2S_IRF
   M2S_CHECK(false, "ir_pwdw: no variant for this shape");
 }

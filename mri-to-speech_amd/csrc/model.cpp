@@ -1161,7 +1161,13 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
       continue;
     }
     s_act = false;
-    if (std::is_same<T, bf16_t>::value && !rbs_[i * nk].q1.empty()) {
+    // every resblock of the stage must carry e4m3 weights (q8 is decided per resblock: k <= 31)
+    bool stage_f8 = std::is_same<T, bf16_t>::value;
+    for (int j = 0; j < nk && stage_f8; ++j) {
+      const RB& rb = rbs_[i * nk + j];
+      stage_f8 = rb.q1.size() == rb.dil.size() && rb.q2.size() == rb.dil.size() && !rb.dil.empty();
+    }
+    if (stage_f8) {
       // fp8 stage (C = 128 / 256): e4m3 operands.  X8 = e4m3(lrelu(x)) once; per pair, c1 stores only
       // e4m3(lrelu(xt)) (its sole consumer is c2), c2 adds the bf16 residual and stores x (bf16, the next
       // residual) and e4m3(lrelu(x)) (the next c1's operand); the last c2 accumulates the MRF sum in S.

@@ -90,7 +90,7 @@ class Acoustic {
   unsigned lstm_spin_max_ = LSTM_SPIN_MAX;  // fault injection: m2s_acoustic_set_lstm_spin_limit
   int device() const { return device_; }
   int n_mels() const { return n_mels_; }
-  int chunk = 256;
+  int chunk = 1920;  // = m2s.config.CNN_CHUNK (the benched pass size)
   bool ir_fused_ = true;  // bf16: fused conv_pw + conv_dw + SE squeeze (env M2S_IR_FUSED=0 disables)
   bool ir_ws_ = true;     // split fp32: the persistent warp-specialised form of it (env M2S_IR_WS=0 disables)
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
@@ -102,7 +102,7 @@ class Acoustic {
                             // slot; 2088 vs 2164 us per launch, gpurun_out r03er)
   bool ir_s2band_ = true;   // blocks.3.0: fused banded conv_pw + stride-2 depthwise (env M2S_IR_S2BAND=0: unfused)
   bool lstm_persistent_ = true;  // one-launch BiLSTM recurrence (env M2S_LSTM_PERSISTENT=0: a launch per step)
-  bool lstm_mid_ = true;         // 4 < B <= 64: granule-exchange recurrence (env M2S_LSTM_MID=0: counter barrier)
+  bool lstm_mid_ = true;         // 4 < B <= 16: granule-exchange recurrence (env M2S_LSTM_MID=0: counter barrier)
   // (the M2S_* switches are read once, when the engine is created: A/B tests of fused vs unfused)
 
   size_t workspace_bytes(int B, int T, int H, int W) const;

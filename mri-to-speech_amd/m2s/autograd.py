@@ -87,14 +87,16 @@ class CamEngine:
                 while r < red:
                     oh, ow, r = (oh + 1) // 2, (ow + 1) // 2, r * 2
                 cnt = n * oh * ow
+                rm, rv = buffers.get(name + ".running_mean"), buffers.get(name + ".running_var")
+                if name not in momenta or rm is None or rv is None:
+                    continue  # track_running_stats=False: torch's BatchNorm keeps no running statistics
                 nbt = buffers.get(name + ".num_batches_tracked")
                 if nbt is not None:
                     nbt.add_(1)
-                m = momenta.get(name, 0.1)
+                m = momenta[name]
                 if m is None:
                     m = 1.0 / float(nbt.item()) if nbt is not None else 0.0
                 unbiased = var * (cnt / max(cnt - 1, 1))
-                rm, rv = buffers[name + ".running_mean"], buffers[name + ".running_var"]
                 rm.mul_(1.0 - m).add_(mean.to(rm.device), alpha=m)
                 rv.mul_(1.0 - m).add_(unbiased.to(rv.device), alpha=m)
 

@@ -26,6 +26,11 @@ ACOUSTIC_DEFAULTS = dict(n_mels=64, cnn_pretrained=False, rnn_hidden=640, dropou
 
 FRAME_HW = (256, 256)
 
+# Frames per CNN pass of the acoustic engine: the one default the plug-in, the CLI, the drivers and
+# bench.py share (bench.py's 64 x 30 step is one pass; DESIGN.md §2.2 measured 256-frame passes 25 %
+# slower: 53.7 vs 43.0 ms per step).  The engine sizes its workspace for min(frames, CNN_CHUNK).
+CNN_CHUNK = 1920
+
 # (block_type, repeats, kernel, stride, exp_ratio, out_ch, se_ratio) per timm stage
 EFFNET_STAGES = [
     ("cn", 2, 3, 1, 1, 16, 0.0),

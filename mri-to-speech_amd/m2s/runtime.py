@@ -19,6 +19,7 @@ import torch
 
 from . import _native as N
 from . import ops as _ops
+from .config import CNN_CHUNK
 
 
 def _device(device) -> torch.device:
@@ -38,7 +39,7 @@ def _as_f32(t: torch.Tensor, device: torch.device) -> torch.Tensor:
 
 class AcousticEngine:
     def __init__(self, state_dict: Dict, n_mels: int = 64, rnn_hidden: int = 640, dtype: str = "bf16x3",
-                 device=None, chunk: int = 256):
+                 device=None, chunk: int = CNN_CHUNK):
         self.device = _device(device)
         self.n_mels, self.rnn_hidden, self.dtype = n_mels, rnn_hidden, dtype
         if dtype not in N.DTYPES:

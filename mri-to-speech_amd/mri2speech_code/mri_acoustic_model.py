@@ -40,7 +40,7 @@ _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if _PKG not in sys.path:
     sys.path.insert(0, _PKG)
 
-from m2s.config import BN_EPS, EFFNET_STEM, effnet_blocks  # noqa: E402
+from m2s.config import BN_EPS, CNN_CHUNK, EFFNET_STEM, effnet_blocks  # noqa: E402
 
 
 def _bn(c):
@@ -203,7 +203,7 @@ class OTNLikeCNNBiLSTM(nn.Module):
         self.rnn = BiLSTMSumMerge(in_dim=self.cnn.out_channels, hidden_size=rnn_hidden, dropout=dropout)
         self.head = _Head(rnn_hidden, n_mels)
         self.m2s_dtype = os.environ.get("M2S_DTYPE", "bf16x3")
-        self.m2s_chunk = int(os.environ.get("M2S_CHUNK", "256"))
+        self.m2s_chunk = int(os.environ.get("M2S_CHUNK", str(CNN_CHUNK)))
         root = lambda: self  # noqa: E731  (children reach the engine without registering a cycle)
         for m in (self.cnn, self.rnn, self.cnn.backbone):
             object.__setattr__(m, "_root", root)

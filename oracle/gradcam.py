@@ -3,13 +3,13 @@
 TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
 
 Restates scripts/mri_gradcam_formant.py of the reference:
-* ``_forward_with_features`` (:101-136): (B,T,1,H,W) frames -> (B*T,3,H,W) repeat -> backbone in train
+* ``_forward_with_features`` (:128-166): (B,T,1,H,W) frames -> (B*T,3,H,W) repeat -> backbone in train
   mode -> last feature map as a gradient leaf -> mean over (H,W) -> BiLSTM sum merge -> head;
 * ``compute_gradcam`` (:203-279): model.train() with the rnn dropout in eval (:221-225), de-normalised
-  mel (:229-230, denormalize_mel :95-98), power 10^(dB/10), band power summed over ``band_indices``
-  (:232-233), target = mean or sum over (B,T) (:242-245), backward, and per requested frame a target of
-  that frame's band power (:254-270);
-* ``_compute_cam_from_grads`` (:139-177): channel weights = spatial mean of the gradient, ReLU of the
+  mel (:230-231, denormalize_mel :122-125), power 10^(dB/10), band power summed over ``band_indices``
+  (:233-234), target = mean or sum over (B,T) (:243-247), backward, and per requested frame a target of
+  that frame's band power (:254-266);
+* ``_compute_cam_from_grads`` (:169-200): channel weights = spatial mean of the gradient, ReLU of the
   weighted feature sum, bilinear resize (align_corners=False) to the frame size, per-frame min-max
   normalisation with +1e-6.
 

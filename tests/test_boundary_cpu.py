@@ -159,3 +159,17 @@ def test_cli_wav_writer_pcm16(tmp_path):
         assert (w.getframerate(), w.getsampwidth(), w.getnchannels()) == (11413, 2, 1)
         pcm = np.frombuffer(w.readframes(5), dtype="<i2")
     assert pcm.tolist() == [0, 16384, -32767, 32767, 32767]
+
+
+def test_plugin_ships_the_benched_cnn_chunk(monkeypatch):
+    """The engine the plug-in builds (and so the CLI and export_predicted_mels.py) runs the CNN in the
+    chunk bench.py times (the plug-in shipped 256-frame passes while bench.py timed 1920)."""
+    import inspect
+
+    import bench
+    from m2s import runtime
+    from m2s.config import CNN_CHUNK
+    from mri_acoustic_model import build_acoustic_model
+    monkeypatch.delenv("M2S_CHUNK", raising=False)
+    assert build_acoustic_model().m2s_chunk == bench.parse([]).chunk == CNN_CHUNK
+    assert inspect.signature(runtime.AcousticEngine).parameters["chunk"].default == CNN_CHUNK

@@ -1,8 +1,8 @@
 """fp8 path (configs[4]: "fp8 MFMA CNN encoder + HiFi-GAN MRF dilated-conv path, >=1000-frame clips").
 
-M2S_DT_FP8 (include/m2s.h): the backbone convs and the MRF resblock convs run e4m3 x e4m3 MFMA
-(v_mfma_f32_16x16x32_fp8_fp8) on OCP e4m3fn weights with per-output-channel fp32 scales, activations
-rounded to e4m3 at the operand read.  Tolerance: cosine similarity >= 0.99 against
+M2S_DT_FP8 (include/m2s.h): OCP e4m3 storage and block-scaled e4m3 MFMA
+(v_mfma_scale_f32_16x16x128_f8f6f4, per-output-channel fp32 weight scales) in the fp8 engine's e4m3
+kernels; the remaining convs run the bf16 path.  Tolerance: cosine similarity >= 0.99 against
 the fp32 oracle for the mel at 1 x 1000 frames; the vocoder's wav is held to the same cosine.  The
 measured values are printed (pytest -s).  GPU box only.
 """
@@ -129,4 +129,18 @@ def test_effnet_fp8_odd_batch_per_frame(rt):
     f = rt.AcousticEngine(st, dtype="fp8", device=DEV).effnet(torch.from_numpy(fr).to(DEV)).cpu().numpy()
     cs = [_cos(f[i], ref[i]) for i in range(5)]
     print("\nfp8 per-frame feature cos (5 frames):", " ".join(f"{c:.5f}" for c in cs))
+    assert min(cs) >= 0.999
+
+
+def test_effnet_fp8_non_square_frames(rt):
+    """256 x 512 frames: the 8 x 16 maps of blocks.5 put two images in an e4m3-output ir_pwdw workgroup
+    (ir_group G = 2, the ir_pwdw_kernel<4, 2, 2> variant) in front of the e4m3 SE GEMM; every frame stays
+    within the cosine bar of the fp32 oracle."""
+    st = synth.synth_acoustic_state(6)
+    sd = {k: torch.from_numpy(v) for k, v in st.items()}
+    fr = synth.synth_frames(1, 3, hw=(256, 512), seed=12)[0]
+    ref = effnet.effnet_gap(sd, torch.from_numpy(fr)).numpy()
+    f = rt.AcousticEngine(st, dtype="fp8", device=DEV).effnet(torch.from_numpy(fr).to(DEV)).cpu().numpy()
+    cs = [_cos(f[i], ref[i]) for i in range(3)]
+    print("\nfp8 per-frame feature cos (256x512):", " ".join(f"{c:.5f}" for c in cs))
     assert min(cs) >= 0.999

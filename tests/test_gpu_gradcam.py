@@ -1,8 +1,8 @@
 """Grad-CAM path on the GPU vs torch-CPU autograd over the oracle.
 
 The caller below drives the plug-in exactly the way the reference's scripts/mri_gradcam_formant.py
-does (compute_gradcam :203-279 with _forward_with_features :101-136 and _compute_cam_from_grads
-:139-177): model.train() with the rnn dropout in eval, backbone of the RGB-repeated frames, last map
+does (compute_gradcam :203-279 with _forward_with_features :128-166 and _compute_cam_from_grads
+:169-200): model.train() with the rnn dropout in eval, backbone of the RGB-repeated frames, last map
 made a gradient leaf, mean -> rnn -> head, band power of the de-normalised mel, backward, feats.grad.
 """
 import numpy as np

@@ -298,12 +298,14 @@ def test_pipeline_end_to_end(rt, ac_state, dtype):
 
 # ------------------------------------------------------------------------------ persistent BiLSTM
 @pytest.mark.parametrize("B,T", [(1, 1000), (3, 64), (4, 40), (70, 6), (8, 1000), (5, 17), (20, 33), (64, 30),
-                                 (64, 200)])
+                                 (64, 200), (12, 33), (16, 200), (9, 1000)])
 def test_bilstm_persistent_long_and_wide(rt, ac_state, monkeypatch, B, T):
     """One-launch recurrence (lstm_persistent.hip) vs the oracle and vs the per-step kernel:
-    B <= 4 runs the granule-exchange lstm_small_kernel (1 x 1000 = configs[4]'s clip length), 4 < B
-    <= 64 the chunked granule-exchange lstm_mid_kernel (8 x 1000 = configs[4]'s per-GPU batch, ragged
-    last chunks at 5 and 20, the bench's 64 x 30), B > 64 the counter-barrier kernel."""
+    B <= 4 runs the granule-exchange lstm_small_kernel (1 x 1000 = configs[4]'s clip length); 4 < B
+    <= 16 the chunked granule-exchange lstm_mid_kernel, 4-sequence chunks up to B = 8 (8 x 1000 =
+    configs[4]'s per-GPU batch, a ragged last chunk at 5) and 8-sequence chunks above (12 x 33 and
+    9 x 1000 with ragged last chunks, 16 x 200 full); B > 16 the counter-barrier kernel (20 x 33, the
+    bench's 64 x 30, 70 x 6)."""
     sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
     x = torch.from_numpy(np.random.default_rng(B * 7 + T).normal(0, 0.5, (B, T, 208)).astype(np.float32))
     monkeypatch.setenv("M2S_LSTM_PERSISTENT", "1")
@@ -340,11 +342,12 @@ def test_preprocess_vs_oracle_shapes_and_bgr(rt, shape):
 
 
 # ------------------------------------------------------------------------------ asynchronous failure report
-@pytest.mark.parametrize("B", [1, 8, 70])
+@pytest.mark.parametrize("B", [1, 8, 12, 70])
 def test_bilstm_barrier_timeout_is_reported(rt, ac_state, B):
     """A BiLSTM hand-off wait that times out (forced: spin limit 0 = the first wait fails) poisons the outputs and is
     reported: m2s_acoustic_status -> M2SError, and the next forward on the engine fails too.  B = 1:
-    lstm_small_kernel, 8: lstm_mid_kernel (granule sweeps), 70: the counter barrier."""
+    lstm_small_kernel, 8 / 12: lstm_mid_kernel with 4- / 8-sequence chunks (granule sweeps), 70: the counter
+    barrier."""
     import ctypes
     from m2s import _native
     eng = rt.AcousticEngine(ac_state[1], dtype="fp32", device=DEV)

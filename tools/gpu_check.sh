@@ -9,7 +9,7 @@ ROOT=$(pwd)
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 run_tests() {
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
   && timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 }
 if [ "$2" = "skip-tests" ]; then t=0; else run_tests; t=$?; fi
