@@ -128,6 +128,9 @@ def parse(argv=None):
     p.add_argument("--no-parity", action="store_true", help="skip the oracle check of clip 0")
     p.add_argument("--no-compare", action="store_true", help="skip the secondary bf16 / fp8 lines (N = 1)")
     p.add_argument("--no-long", action="store_true", help="skip the configs[4] lines (8 x 1000-frame clips, N = 1)")
+    p.add_argument("--ragged", action="store_true",
+                   help="clips x gpus clips of 0.8 / 1.0 / 1.2 x --frames frames, sharded by length over the ranks "
+                        "(dp.shard_clips), one pipeline call per length group, results gathered to rank 0")
     return p.parse_args(argv)
 
 
@@ -165,6 +168,50 @@ def timed_loop(step, k: int, world: int, sync, device) -> float:
     if multi(world):
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     return float(el.item())
+
+
+def ragged_lengths(n, mean_frames, seed=99):
+    """Clip lengths of the ``--ragged`` workload: ``mean_frames`` x {0.8, 1.0, 1.2}, drawn per clip
+    (seeded, the same list on every rank): 24 / 30 / 36 frames around configs[3]'s 30."""
+    rng = np.random.default_rng(seed)
+    choices = [max(1, int(round(mean_frames * f))) for f in (0.8, 1.0, 1.2)]
+    return [int(c) for c in rng.choice(choices, size=n)]
+
+
+class RaggedPlan:
+    """The ``--ragged`` step: a global list of ragged clips sharded over the ranks by length
+    (``dp.shard_clips``, the same plan on every rank, no communication), each rank's clips ordered by
+    length so that every length group is one contiguous block of rows and ONE pipeline call; the
+    results of a step land in padded per-rank (clips, max length) buffers that travel to rank 0 in one
+    gather each (wav, dB mel) -- the product path of export_predicted_mels.py's torchrun mode."""
+
+    def __init__(self, lens_all, world, rank):
+        self.shards = [sorted(s, key=lambda i: (lens_all[i], i)) for s in dp_mod().shard_clips(lens_all, world)]
+        self.mine = self.shards[rank]
+        self.lens_by_rank = [[lens_all[i] for i in s] for s in self.shards]
+        mine_lens = self.lens_by_rank[rank]
+        self.tmax = max(mine_lens, default=0)
+        self.groups = []  # (length, first row, last row + 1)
+        for k, L in enumerate(mine_lens):
+            if self.groups and self.groups[-1][0] == L:
+                self.groups[-1][2] = k + 1
+            else:
+                self.groups.append([L, k, k + 1])
+
+    def step(self, forward, frames_by_len, wav, mel, multi_rank):
+        for L, r0, r1 in self.groups:
+            o = forward(frames_by_len[L])
+            wav[r0:r1, : L * HOP].copy_(o["wav"])
+            mel[r0:r1, :L].copy_(o["mel_db"])
+        if multi_rank:
+            return (dp_mod().gather_results(wav, self.lens_by_rank, per_step=HOP),
+                    dp_mod().gather_results(mel, self.lens_by_rank, per_step=1))
+        return None
+
+
+def dp_mod():
+    from m2s import dp
+    return dp
 
 
 def make_frames(clips, frames, hw, rank, device):
@@ -333,23 +380,39 @@ def main():
 
     pipe = build(args.dtype)
     B, T, HW = args.clips, args.frames, args.hw
-    frames = make_frames(B, T, HW, rank, device)
     out = {}
-    if multi(world):  # C3: clip lengths of every rank (the gather is sized from them)
-        all_lens = dp.all_gather_lengths([T] * B, device)
+    if args.ragged:  # ragged clip list sharded by length; one pipeline call per length group
+        lens_all = ragged_lengths(B * world, T)
+        plan = RaggedPlan(lens_all, world, rank)
+        fr_by_len = {L: make_frames(r1 - r0, L, HW, rank * 1000 + L, device) for L, r0, r1 in plan.groups}
+        wav_buf = torch.zeros(len(plan.mine), plan.tmax * HOP, device=device)
+        mel_buf = torch.zeros(len(plan.mine), plan.tmax, 64, device=device)
+        frames = fr_by_len[plan.groups[0][0]] if plan.groups else make_frames(1, T, HW, rank, device)
+        frames_per_step = sum(lens_all)
+        local_frames = sum(plan.lens_by_rank[rank])
+        args.no_compare = args.no_long = True
 
-    def step(p=None):
-        out.update((p or pipe).forward(frames))  # torch.ops.m2s.pipeline_forward on the current stream
-        if multi(world):  # C2: wav + dB mel of every clip to rank 0 over RCCL
-            dp.gather_results(out["wav"], all_lens, per_step=HOP)
-            dp.gather_results(out["mel_db"], all_lens, per_step=1)
+        def step(p=None):
+            plan.step((p or pipe).forward, fr_by_len, wav_buf, mel_buf, multi(world))
+    else:
+        frames = make_frames(B, T, HW, rank, device)
+        frames_per_step = world * B * T
+        local_frames = B * T
+        if multi(world):  # C3: clip lengths of every rank (the gather is sized from them)
+            all_lens = dp.all_gather_lengths([T] * B, device)
+
+        def step(p=None):
+            out.update((p or pipe).forward(frames))  # torch.ops.m2s.pipeline_forward on the current stream
+            if multi(world):  # C2: wav + dB mel of every clip to rank 0 over RCCL
+                dp.gather_results(out["wav"], all_lens, per_step=HOP)
+                dp.gather_results(out["mel_db"], all_lens, per_step=1)
 
     sync = lambda: torch.cuda.synchronize(device)  # noqa: E731
     for _ in range(args.warmup):
         step()
     elapsed = timed_loop(step, args.steps, world, sync, device)
     pipe.ac.check()  # a BiLSTM hand-off timeout in the timed steps raises here (m2s_acoustic_status)
-    frames_total = world * B * T * args.steps
+    frames_total = frames_per_step * args.steps
     fps = frames_total / elapsed
     audio_s = frames_total * HOP / SR
     result = {
@@ -367,8 +430,11 @@ def main():
         "precision": PRECISION[args.dtype],
         "data": "synthetic (seeded U[0,1) frames, per-frame min-max; random-init weights of the reference architecture)",
         "rtf": round(elapsed / audio_s, 6),
-        "config": {"workload": f"e2e rtMRI->wav, {B} clips x {T} frames per GPU at {HW}x{HW} " +
-                               ("(configs[4] clip length)" if T >= 1000 else "(configs[3] per-GPU share)"),
+        "config": {"workload": (f"e2e rtMRI->wav, {B * world} ragged clips of {sorted(set(lens_all))} frames "
+                                f"(mean {frames_per_step / (B * world):.1f}) sharded by length over {world} GPU(s) "
+                                f"at {HW}x{HW}") if args.ragged else
+                               (f"e2e rtMRI->wav, {B} clips x {T} frames per GPU at {HW}x{HW} " +
+                                ("(configs[4] clip length)" if T >= 1000 else "(configs[3] per-GPU share)")),
                    "clips_per_gpu": B, "frames_per_clip": T, "global_batch_clips": B * world, "hw": HW,
                    "parallelism": f"dp{world}", "chunk": args.chunk},
     }
@@ -379,7 +445,7 @@ def main():
         timed_loop(step, args.steps, world, sync, device)
         _native.prof_enable(False)
         stats = _native.prof_collect()
-        result["roofline"] = roofline(stats, args.dtype, args.steps, fps, B * T)
+        result["roofline"] = roofline(stats, args.dtype, args.steps, fps, local_frames)
         if rank == 0 and os.environ.get("M2S_BENCH_KERNELS"):
             for s in sorted(stats, key=lambda s: -s["ms"]):
                 print(f"# {s['name']:40s} n={s['launches']:6d} ms={s['ms']:9.3f} "
@@ -388,6 +454,8 @@ def main():
 
     ref0 = None
     if rank == 0 and not args.no_parity:  # clip 0 of this rank's workload through the fp32 oracle
+        if args.ragged:  # clip 0 of the first length group
+            out.update(pipe.forward(frames))
         ref0 = oracle_clip(ac_sd, gen_sd, mean, std, frames[:1].cpu().numpy())
         result["parity"] = dict(parity_vs(ref0, out), clip=0, tolerance=FP32_TOL, reference="fp32 CPU oracle")
     if world == 1 and not args.no_compare:  # secondary lines: the narrower dtypes on the same workload

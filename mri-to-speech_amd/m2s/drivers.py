@@ -35,6 +35,7 @@ class Job:
     src: Path
     stem: str
     array: Optional[np.ndarray] = None   # conformed input, host
+    length: int = 0                      # time steps of the input (frames), for length-balanced sharding
     result: Optional[np.ndarray] = None  # model output, host
     notes: List[str] = field(default_factory=list)
     error: Optional[str] = None
@@ -76,6 +77,70 @@ def run_batches(batches: Sequence[Sequence[Job]], fn: Callable[[torch.Tensor], t
             continue
         for j, row in zip(batch, out):
             j.result = row
+
+
+def run_sharded(jobs: Sequence[Job], fn: Callable[[torch.Tensor], torch.Tensor], device: torch.device,
+                lengths: Sequence[int], feat_shape: Sequence[int], max_batch: int = 16,
+                load: Optional[Callable[[Job], Job]] = None, time_axis: int = -1, per_step: int = 1) -> List[Job]:
+    """``run_batches`` over one process per GPU (torch.distributed; a no-op wrapper at world 1).
+
+    Every rank holds the same job list and ``lengths`` (time steps per job, e.g. frames), so every rank
+    derives the same length-balanced plan (``dp.shard_clips``) with no communication.  A rank loads
+    (``load``) and runs only its own shard, batched by shape as in a single process; then every rank's
+    results travel to rank 0 in ONE padded gather (``dp.gather_results``: RCCL "nccl" over xGMI on
+    MI355X, gloo in the CPU tests), plus a gather of the per-job status and error text.  On rank 0
+    every job of the list ends with ``result`` / ``error`` as a single-process ``run_batches`` leaves
+    them; the other ranks return their own shard.
+
+    A job's result is an array whose ``time_axis`` holds ``length * per_step`` steps and whose other
+    axes are ``feat_shape`` (an ln-mel: (n_mels, T), time_axis -1)."""
+    import torch.distributed as dist
+
+    from . import dp
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        mine = [load(j) for j in jobs] if load else list(jobs)
+        run_batches(plan_batches(mine, max_batch), fn, device)
+        return list(jobs)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if len(lengths) != len(jobs):
+        raise ValueError("one length per job")
+    shards = dp.shard_clips(lengths, world)
+    mine = [jobs[i] for i in shards[rank]]
+    if load:
+        mine = [load(j) for j in mine]
+    run_batches(plan_batches(mine, max_batch), fn, device)
+
+    comm = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    lens_by_rank = [[int(lengths[i]) for i in s] for s in shards]
+    tmax = max(lens_by_rank[rank], default=0) * per_step
+    local = torch.zeros((len(mine), tmax) + tuple(feat_shape), dtype=torch.float32)
+    status = torch.zeros((len(mine), 1), dtype=torch.float32)
+    errors = {}
+    for k, j in enumerate(mine):
+        if j.result is not None and j.error is None:
+            r = np.moveaxis(np.asarray(j.result, np.float32), time_axis, 0)
+            local[k, : r.shape[0]] = torch.from_numpy(np.ascontiguousarray(r))
+            status[k, 0] = 1.0
+        else:
+            errors[shards[rank][k]] = j.error or "no result"
+    got = dp.gather_results(local.to(comm), lens_by_rank, per_step=per_step)
+    ok = dp.gather_results(status.to(comm), [[1] * len(s) for s in shards], per_step=1)
+    errs = [None] * world if rank == 0 else None
+    dist.gather_object(errors, errs, dst=0)
+    if rank != 0:
+        return mine
+    all_errors = {i: e for d in errs for i, e in d.items()}
+    for r, s in enumerate(shards):
+        rows, flags = got[r].cpu().numpy(), ok[r].cpu().numpy()
+        for k, i in enumerate(s):
+            j = jobs[i]
+            if flags[k, 0] > 0:
+                j.result, j.error = np.moveaxis(rows[k, : int(lengths[i]) * per_step], 0, time_axis).copy(), None
+            else:
+                j.result = None
+                j.error = all_errors.get(i, "no result") if r == 0 else f"rank {r}: {all_errors.get(i, 'no result')}"
+    return list(jobs)
 
 
 def vocode(generator, jobs: Sequence[Job], device: torch.device, max_batch: int = 64) -> None:
@@ -146,6 +211,11 @@ def build_acoustic(checkpoint, device: torch.device, code_dir=None, n_mels: int 
         raise ImportError("cannot import mri_acoustic_model; point the code-dir flag at the directory holding it") from e
     model = build_acoustic_model(n_mels=n_mels, cnn_pretrained=False, rnn_hidden=rnn_hidden, dropout=dropout,
                                  use_checkpoint=False, ckpt_segments=2, use_reentrant=False).to(device)
+    if checkpoint is None:  # weights arrive later (a non-zero rank of a multi-GPU run: dp.broadcast_state)
+        model.eval()
+        if dtype:
+            model.m2s_dtype = dtype
+        return model
     ck = load_state(checkpoint)
     missing, unexpected = model.load_state_dict(ck.get("model_state_dict", ck), strict=False)
     for kind, keys in (("missing", missing), ("unexpected", unexpected)):

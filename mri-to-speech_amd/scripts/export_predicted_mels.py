@@ -13,6 +13,14 @@ How it runs: the sample list is read first, clips with the same frame-stack shap
 acoustic model together (``--batch`` per call, m2s/drivers.py), and the de-normalisation
 y*std+mean -> 10^(x/10) -> clamp(1e-5) -> ln runs on the device (``torch.ops.m2s.mel_glue``) before
 the one copy back.  ``--cpu`` is refused: there is no CPU path.
+
+Several GPUs (one process per GPU): ``python -m torch.distributed.run --nproc-per-node N
+--master-addr 127.0.0.1 scripts/export_predicted_mels.py ...``.  Every rank lists the samples and reads
+their frame counts from the .npy headers; the ragged clips are sharded by length (``dp.shard_clips``:
+longest first onto the least-loaded rank); rank 0 loads the checkpoint and its state dict reaches the
+other ranks in ONE broadcast (``dp.broadcast_state``); each rank reads and runs only its own clips;
+the ln-mels are gathered to rank 0 in one padded gather (``drivers.run_sharded``) and rank 0 writes
+every file.  Backend: RCCL ("nccl") over xGMI, or ``M2S_DIST_BACKEND=gloo``.
 """
 from __future__ import annotations
 
@@ -41,8 +49,9 @@ def scaler_arrays(path: Path):
     return mean, std
 
 
-def pending_samples(samples_dir: Path, out_dir: Path, overwrite: bool):
-    """Jobs for the samples that still need a mel (frames loaded); missing mri.npy is reported."""
+def pending_samples(samples_dir: Path, out_dir: Path, overwrite: bool, load: bool = True):
+    """Jobs for the samples that still need a mel (frames loaded unless ``load`` is False: then only
+    ``job.length``, the frame count from the .npy header, is read); missing mri.npy is reported."""
     if not samples_dir.is_dir():
         raise SystemExit(f"samples directory not found: {samples_dir}")
     dirs = sorted((p for p in samples_dir.iterdir() if p.is_dir()), key=lambda p: p.name)
@@ -56,9 +65,45 @@ def pending_samples(samples_dir: Path, out_dir: Path, overwrite: bool):
         if not job.src.is_file():
             print(f"[WARN] MRI file missing for {d.name}, skipping")
             continue
-        job.array = np.load(job.src, allow_pickle=False).astype(np.float32, copy=False)
+        if load:
+            load_frames(job)
+        else:
+            try:
+                job.length = int(np.load(job.src, mmap_mode="r", allow_pickle=False).shape[0])
+            except Exception as e:  # noqa: BLE001 - reported per job (rank 0 writes the warning)
+                job.error = f"{type(e).__name__}: {e}"
         jobs.append(job)
     return jobs
+
+
+def load_frames(job):
+    """(T,H,W) float32 frames of one sample into ``job.array`` (a read failure becomes ``job.error``)."""
+    if job.error is not None or job.array is not None:
+        return job
+    try:
+        job.array = np.load(job.src, allow_pickle=False).astype(np.float32, copy=False)
+        job.length = int(job.array.shape[0])
+    except Exception as e:  # noqa: BLE001 - reported per job
+        job.error = f"{type(e).__name__}: {e}"
+    return job
+
+
+def init_distributed():
+    """(world, rank, local_rank); joins the process group when launched by torch.distributed.run."""
+    import os
+
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank, local = int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        backend = os.environ.get("M2S_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return world, rank, local
 
 
 def export_mels(args: argparse.Namespace) -> list:
@@ -69,17 +114,28 @@ def export_mels(args: argparse.Namespace) -> list:
         raise SystemExit("--cpu: m2s runs on MI355X only (no CPU path); drop the flag")
     if not torch.cuda.is_available():
         raise SystemExit("m2s needs an MI355X (HIP) device; none is visible")
-    device = torch.device("cuda")
-    model = drivers.build_acoustic(Path(args.mri_checkpoint).resolve(), device, code_dir=args.mri_code_dir,
-                                   n_mels=mean.numel(), dtype=args.dtype)
+    world, rank, local = init_distributed()
+    # one GPU per rank; more ranks than GPUs wrap round (a gloo rehearsal on a one-GPU box)
+    device = torch.device("cuda", local % torch.cuda.device_count()) if world > 1 else torch.device("cuda")
+    ckpt = Path(args.mri_checkpoint).resolve()
+    # rank 0 reads the checkpoint; the other ranks build the same module tree and receive its weights
+    model = drivers.build_acoustic(ckpt if rank == 0 else None, device, code_dir=args.mri_code_dir,
+                                   n_mels=mean.numel(), dtype=args.dtype,
+                                   log=print if rank == 0 else (lambda *a: None))
+    if world > 1:
+        broadcast_model_state(model, device)
     mean, std = mean.to(device), std.to(device)
-    jobs = pending_samples(Path(args.processed_dir).resolve() / "samples", out_dir, args.overwrite)
+    jobs = pending_samples(Path(args.processed_dir).resolve() / "samples", out_dir, args.overwrite,
+                           load=world == 1)
 
     def mels(frames):  # (B,T,H,W) -> (B, n_mels, T) ln-mel
         _, ln = mel_glue(model(frames[:, :, None]), mean, std)
         return ln.transpose(1, 2)
 
-    drivers.run_batches(drivers.plan_batches(jobs, args.batch), mels, device)
+    drivers.run_sharded(jobs, mels, device, lengths=[j.length for j in jobs], feat_shape=(mean.numel(),),
+                        max_batch=args.batch, load=load_frames, time_axis=-1)
+    if rank != 0:
+        return []
     written = []
     for job in jobs:
         if job.result is None:
@@ -90,6 +146,18 @@ def export_mels(args: argparse.Namespace) -> list:
         written.append(path)
     print(f"[INFO] {len(written)} mel file(s) written to {out_dir}")
     return written
+
+
+def broadcast_model_state(model, device) -> None:
+    """Rank 0's loaded weights to every rank in one flat broadcast (C1, m2s/dp.py)."""
+    import torch.distributed as dist
+
+    from m2s import dp
+
+    comm = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    got = dp.broadcast_state(sd, comm)
+    model.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in got.items()}, strict=True)
 
 
 def parse_args(argv=None) -> argparse.Namespace:

@@ -92,3 +92,57 @@ def test_timed_loop_and_gather_world2_gloo():
     res = sorted(q.get(timeout=10) for _ in range(2))
     assert all(ok for _, ok, _ in res), res
     assert res[0][2] == res[1][2]  # every rank reports the same (max) time
+
+
+def _ragged_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lens_all = bench.ragged_lengths(13, 30)
+        plan = bench.RaggedPlan(lens_all, world, rank)
+        calls = []
+
+        def forward(x):  # stand-in pipeline: every output row carries its clip id
+            calls.append(tuple(x.shape))
+            n, L = x.shape[:2]
+            ids = x[:, 0, 0, 0]
+            return {"wav": ids[:, None].expand(n, L * bench.HOP).clone(), "mel_db": ids[:, None, None].expand(n, L, 64).clone()}
+
+        fr = {}
+        for L, r0, r1 in plan.groups:  # frames whose first pixel is the global clip id
+            fr[L] = torch.zeros(r1 - r0, L, 2, 2)
+            fr[L][:, 0, 0, 0] = torch.tensor([float(i) for i in plan.mine[r0:r1]])
+        wav = torch.zeros(len(plan.mine), plan.tmax * bench.HOP)
+        mel = torch.zeros(len(plan.mine), plan.tmax, 64)
+        got = plan.step(forward, fr, wav, mel, True)
+        ok = len(calls) == len(plan.groups) == len({L for L, _, _ in plan.groups})
+        if rank == 0:
+            seen = []
+            for r, s in enumerate(plan.shards):
+                for k, i in enumerate(s):
+                    L = lens_all[i]
+                    ok &= bool((got[0][r][k, : L * bench.HOP] == i).all()) and bool((got[0][r][k, L * bench.HOP:] == 0).all())
+                    ok &= bool((got[1][r][k, :L] == i).all())
+                    seen.append(i)
+            ok &= sorted(seen) == list(range(13))
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ragged_bench_step_gloo(world):
+    """bench.py --ragged: a ragged clip list sharded by length, one forward per length group, every
+    clip's wav / mel back on rank 0 in its own row and length (rank 3 of 4 may hold few clips)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ragged_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    assert all(ok for _, ok in res), res
+    assert sorted(set(bench.ragged_lengths(64, 30))) == [24, 30, 36]

@@ -157,6 +157,51 @@ def test_export_predicted_mels(tmp_path):
                      "--scaler_json", str(tmp_path / "scaler.json"), "--output_dir", str(out_dir)]) == []
 
 
+def test_export_predicted_mels_torchrun_ragged(tmp_path):
+    """export_predicted_mels.py under torch.distributed.run, 2 ranks on this box's GPU (gloo for the
+    collectives: RCCL takes one rank per GPU): ragged clips sharded by length, rank 0's weights broadcast,
+    the mels gathered to rank 0, which writes every file.  Every file equals the single-process run's
+    (1e-5: a clip may share its CNN / BiLSTM launch with other clips) and the oracle (5e-4)."""
+    import socket
+    import subprocess
+    import sys
+    ac_sd = synth.synth_acoustic_state(7)
+    mean, std = synth.synth_scaler()
+    ck = tmp_path / "best.pt"
+    torch.save({"model_state_dict": _t(ac_sd)}, ck)
+    (tmp_path / "scaler.json").write_text(json.dumps({"mean": mean.tolist(), "std": std.tolist()}))
+    rng = np.random.default_rng(4)
+    lens = {"utt_a": 5, "utt_b": 3, "utt_c": 5, "utt_d": 7, "utt_e": 2}
+    for stem, T in lens.items():
+        d = tmp_path / "proc" / "samples" / stem
+        d.mkdir(parents=True)
+        np.save(d / "mri.npy", (rng.integers(0, 256, (T, 256, 256)) / 255.0).astype(np.float32))
+    script = os.path.join(REPO, "mri-to-speech_amd", "scripts", "export_predicted_mels.py")
+    common = ["--processed_dir", str(tmp_path / "proc"), "--mri_checkpoint", str(ck),
+              "--scaler_json", str(tmp_path / "scaler.json"),
+              "--mri_code_dir", os.path.join(REPO, "mri-to-speech_amd", "mri2speech_code")]
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    env = dict(os.environ, M2S_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), script, *common,
+                        "--output_dir", str(tmp_path / "dist")], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    single = _load(os.path.join("scripts", "export_predicted_mels.py"), "m2s_export_mels_1")
+    single.main([*common, "--output_dir", str(tmp_path / "one")])
+    sd = _t(ac_sd)
+    for stem, T in lens.items():
+        got, one = np.load(tmp_path / "dist" / f"{stem}.npy"), np.load(tmp_path / "one" / f"{stem}.npy")
+        assert got.shape == (64, T)
+        np.testing.assert_allclose(got, one, atol=1e-5, rtol=0, err_msg=stem)
+        fr = torch.from_numpy(np.load(tmp_path / "proc" / "samples" / stem / "mri.npy"))
+        mn = acoustic.head(sd, acoustic.bilstm_summerge(sd, effnet.effnet_gap(sd, fr).view(1, T, -1)))[0]
+        ref = acoustic.mel_db_to_log(acoustic.denormalize_mel(mn, mean, std)).t().numpy()
+        np.testing.assert_allclose(got, ref, atol=5e-4, rtol=0, err_msg=stem)
+
+
 def test_vocoder_only_callers(tmp_path):
     """inference_e2e.py and mel_to_audio_synthesis.py drop-ins: (64, T) ln-mel files -> wav, files of
     equal length batched into one generator call, malformed files reported and skipped."""
