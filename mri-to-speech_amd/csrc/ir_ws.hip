@@ -163,10 +163,15 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   auto issue_wd = [&](int f, Step d) {  // the slice's depthwise taps [9][32] + bias: 80 lanes of 16 B
     const int c0 = d.sl * WS_SL;
     float* dst = wdl + (f & 1) * 320;
+    // the lane's source offset is rebuilt here each time (asm barrier): hoisted out of the slice loop
+    // it became two 64-bit pointers spilled to scratch, and their reload's vmcnt wait drained the
+    // weight DMA in flight
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
     if (wave == WS_NP - 2) {
-      dma16(wdw + (size_t)(lane >> 3) * cs_mid + c0 + 4 * (lane & 7), lds_addr(dst));
-    } else if (wave == WS_NP - 1 && lane < 16) {
-      const float* src = lane < 8 ? wdw + (size_t)8 * cs_mid + c0 + 4 * lane : bdw + c0 + 4 * (lane - 8);
+      dma16(wdw + ((ln >> 3) * cs_mid + c0 + 4 * (ln & 7)), lds_addr(dst));
+    } else if (wave == WS_NP - 1 && ln < 16) {
+      const float* src = ln < 8 ? wdw + (8 * cs_mid + c0 + 4 * ln) : bdw + (c0 + 4 * (ln - 8));
       dma16(src, lds_addr(dst + 256));
     }
   };
@@ -245,10 +250,19 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
 
   // ---- consumer pieces -----------------------------------------------------------------------
   const int ct = tid - 64 * WS_NP, cw = ct >> 6, cg = ct & 7, cpl = ct >> 3;
+  // A consumer lane's pixels are cpl + 64 k of the band (k < WS_PXL): in the tile they sit 64 / W rows
+  // apart (a compile-time offset from the first), and in the SE GEMM's interleaved operand layout
+  // (il_st4: position p, channel c -> element p * 2 cs + 2 (c & ~31) + (c & 31)) 64 positions apart.
+  // The byte offset of a store is one 24-bit multiply-add on the band's scalar position base; the
+  // per-pixel 64-bit position arithmetic (two v_mul_lo_u32 a pixel) was a fifth of the consumer VALU.
+  const int toff0 = ((cpl / W) * WT + cpl % W) * 16;
   auto consume = [&](int f, Step d) {
-    const int img = d.img, c0 = d.sl * WS_SL, r0 = d.band * WS_BR, br = min(WS_BR, H - r0);
+    const int c0 = d.sl * WS_SL, r0 = d.band * WS_BR, br = min(WS_BR, H - r0);
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     TR(f + 1, 4);
+    const uint32_t pbase = (uint32_t)(d.img * P + r0 * W);  // uniform
+    const uint32_t yoff0 = __builtin_amdgcn_readfirstlane(4u * (uint32_t)c0) + 8u * (uint32_t)cg +
+                           (pbase + (uint32_t)cpl) * (4u * (uint32_t)cs_mid);  // launch_ir_ws: < 2^32
     // lane = (4-channel plane cg, pixels cpl + 64 k): the plane's 9 taps stay in registers
     const float* wd = wdl + (f & 1) * 320 + 4 * cg;
     float w[9][4], b[4];
@@ -262,30 +276,36 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       b[0] = v.x; b[1] = v.y; b[2] = v.z; b[3] = v.w;
     }
     const char* tpl = tiles + (f & 1) * 8 * PLT + cg * PLT;
-    sp_t* ys = reinterpret_cast<sp_t*>(y);
+    auto pixel = [&](int k) {
+      const char* tp = tpl + toff0 + k * (64 / W) * WT * 16;
+      float a[4] = {b[0], b[1], b[2], b[3]};
 #pragma unroll
-    for (int k = 0; k < WS_PXL; ++k) {
-      const int p = cpl + 64 * k;
-      if (p < br * W) {
-        const int oy = p / W, ox = p - (p / W) * W;  // band-relative output pixel
-        const char* tp = tpl + (oy * WT + ox) * 16;
-        float a[4] = {b[0], b[1], b[2], b[3]};
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const float4 u = *reinterpret_cast<const float4*>(tp + ((t / 3) * WT + (t % 3)) * 16);
-          a[0] += w[t][0] * u.x;
-          a[1] += w[t][1] * u.y;
-          a[2] += w[t][2] * u.z;
-          a[3] += w[t][3] * u.w;
-          if (t % 3 == 2) asm volatile("" ::: "memory");  // one tap row of loads in flight (registers)
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          a[j] = silu(a[j]);
-          s[j] += a[j];
-        }
-        il_st4(ys, (long)img * P + (long)(r0 + oy) * W + ox, cs_mid, c0 + 4 * cg, a);  // the SE GEMM's interleaved operand
+      for (int t = 0; t < 9; ++t) {
+        const float4 u = *reinterpret_cast<const float4*>(tp + ((t / 3) * WT + (t % 3)) * 16);
+        a[0] += w[t][0] * u.x;
+        a[1] += w[t][1] * u.y;
+        a[2] += w[t][2] * u.z;
+        a[3] += w[t][3] * u.w;
+        if (t % 3 == 2) asm volatile("" ::: "memory");  // one tap row of loads in flight (registers)
       }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] = silu(a[j]);
+        s[j] += a[j];
+      }
+      uint2 hi, lo;  // the SE GEMM's interleaved operand: [hi 32 | lo 32] per 32-channel group
+      split4(a, hi, lo);
+      char* u = reinterpret_cast<char*>(y) + (yoff0 + (uint32_t)k * 256u * (uint32_t)cs_mid);
+      *reinterpret_cast<uint2*>(u) = hi;
+      *reinterpret_cast<uint2*>(u + 64) = lo;
+    };
+    if (br == WS_BR) {  // a full band: every lane's pixels exist, so their chains interleave
+#pragma unroll
+      for (int k = 0; k < WS_PXL; ++k) pixel(k);
+    } else {
+#pragma unroll
+      for (int k = 0; k < WS_PXL; ++k)
+        if (cpl + 64 * k < br * W) pixel(k);
     }
     TR(f + 1, 5);
     // squeeze partials: the wave's 8 pixel lanes of each plane (lane bits 3..5): a DPP row rotation
@@ -386,6 +406,7 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
                   const float* wdw, const float* bdw, void* y, void* se_mean, double flops, double bytes,
                   hipStream_t s) {
   M2S_CHECK(ir_ws_supported(H, W, cs_in, kp, cs_mid) && N > 0, "ir_ws: unsupported shape");
+  M2S_CHECK((double)N * H * W * cs_mid * 4.0 < 4294967296.0, "ir_ws: output map too large for 32-bit offsets");
   const WsLayout L = ws_layout(H, W, cs_in, cs_mid);
   const int n_cu = device_cus();
   const dim3 grid(std::min(N, n_cu));

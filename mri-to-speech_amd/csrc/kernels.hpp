@@ -53,6 +53,14 @@ bool se_gemm_sp_supported(int P, int cs_in, int cs_out);
 void launch_se_gemm_sp(const void* x, int M, int P, int cs_in, const void* w, int n_pad, const float* bias,
                        const void* gate, const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes);
 
+// The same split SE-gated conv_pwl as a persistent warp-specialised GEMM: loader waves fill a 3-slot LDS
+// ring by LDS-DMA and consumer waves compute, synchronised by per-slot FULL / FREE counters in LDS (no
+// per-K-step barrier; the ring runs across tiles).  Same operands as launch_se_gemm_sp; P % 256 == 0 with
+// cs_out <= 128 (16x16 maps) or P == 64 with 128 < cs_out <= 224 (8x8 maps).  (se_ws.hip)
+bool se_ws_supported(int P, int cs_in, int cs_out);
+void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_pad, const float* bias, const void* gate,
+                  const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes);
+
 // The same for a stride-2 depthwise (TF-SAME, top / left pads pad_t / pad_l) on an IH x IW <= 256-pixel
 // conv_pw map: y (N, OH*OW, cs_mid), se_mean over the OH x OW output.  (ir_fused.hip)
 // Split-fp32 stride-1 IR front half (conv_pw + bn1 + SiLU + conv_dw + bn2 + SiLU + SE squeeze) on

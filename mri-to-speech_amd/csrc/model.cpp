@@ -86,6 +86,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_SE_FUSED")) se_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER_FUSED")) er_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_SP")) se_sp_ = std::strcmp(e, "0") != 0;  // A/B only
+  if (const char* e = std::getenv("M2S_SE_WS")) se_ws_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER_MRG")) er_mrg_ = std::strcmp(e, "0") != 0;  // A/B and tests only
   if (const char* e = std::getenv("M2S_IR_S2BAND")) ir_s2band_ = std::strcmp(e, "0") != 0;  // A/B and tests only
   if (const char* e = std::getenv("M2S_LSTM_PERSISTENT")) lstm_persistent_ = std::strcmp(e, "0") != 0;
@@ -665,6 +666,11 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                             scale, b.skip ? cur : nullptr, nxt, chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
                             rows * cs + 2.0 * rows * co * (b.skip ? 2.0 : 1.0) + (double)b.f8_npad * b.f8_kp +
                                 2.0 * nc * cs);
+        } else if (SPL && se_ws_ && se_ws_supported(nh * nw, cs, chan_stride(b.cout))) {
+          const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
+          launch_se_ws(M2, nc * nh * nw, nh * nw, cs, b.c2.w, b.c2.n_pad, b.c2.b, scale, b.skip ? cur : nullptr, nxt,
+                       chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
+                       4.0 * rows * cs + 4.0 * rows * co * (b.skip ? 2.0 : 1.0) + 4.0 * b.c2.n_pad * b.c2.kp + 4.0 * nc * cs);
         } else if (SPL && se_sp_ && se_gemm_sp_supported(nh * nw, cs, chan_stride(b.cout))) {
           const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
           launch_se_gemm_sp(M2, nc * nh * nw, nh * nw, cs, b.c2.w, b.c2.n_pad, b.c2.b, scale, b.skip ? cur : nullptr, nxt,

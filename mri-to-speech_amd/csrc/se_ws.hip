@@ -1,0 +1,360 @@
+// Split-fp32 SE-gated conv_pwl (+ bn3 + skip) of the stride-1 IR blocks as a persistent, warp-specialised
+// GEMM with a flag-synchronised LDS ring (no per-K-step barrier):
+//
+//   y[m][n] = sum_k W[n][k] * (gate[img(m)][k] * X[m][k]) + bias[n] (+ res[m][n]),  all split fp32
+//
+// (timm InvertedResidual se.conv_expand gate x conv_pwl + bn3 + skip; mri_acoustic_model.py:28-34,46.)
+// Operands as gemm128.hip KIND_SP_SE: X interleaved split [M][cs_in / 32][hi 32 | lo 32] bf16 (ir_ws /
+// ir_pwdw il_st8), W split rows [n_pad][hi kp | lo kp] (kp = cs_in), gate split [M / P][hi cs_in | lo cs_in],
+// res / y split [M][hi cs_out | lo cs_out].  A K step is 32 channels = one 128-byte LDS row per operand row.
+//
+// Why.  The barrier-synchronous rings (conv_gemm's in-LDS scaling, gemm128 KIND_SP_SE) stream this operand
+// at ~3.2 TB/s while the same access pattern streams at 6.1 TB/s when every wave keeps its own DMAs in
+// flight without a barrier (tools/bw_probe.hip): a barrier per K step ties every wave to the
+// slowest DMA and every tile starts with an empty ring.  Here one workgroup per CU walks its tiles
+// (tile = blockIdx.x + i * gridDim.x) and the ring runs across tile boundaries:
+//
+//   loader waves (NL): for the flat step s (tile, K step) wait until FREE[s % NS] shows the consumers
+//     released the slot's previous use, issue their share of the step's DMAs (weights rows, activation
+//     rows; at a tile's first step loader 0 also DMAs the tile's gate rows), then, with step s in flight,
+//     wait for step s - 1's DMAs (counted vmcnt) and publish it: FULL[(s - 1) % NS] += 1.
+//   consumer waves (WM x WN, 64 x 16 NT each): wait until FULL[s % NS] reached NL x (use + 1), read the
+//     step's gate, activation and weight fragments, release the slot (FREE += 1) as soon as the reads
+//     returned, gate the activations in fp32 and re-split them (17 bits), three bf16 MFMA terms; after a
+//     tile's last step the epilogue (bias, skip, split store) runs while the loaders already fill the next
+//     tile's first slots.
+//
+// Flags are monotonic per-slot counters in LDS (ds_add_u32 by one lane, ds_read polls with s_sleep); every
+// wait is bounded (a poll limit, then the wave goes on: a wrong result, never a hang).  LDS-DMA data is in
+// LDS when the issuing wave's vmcnt retires it, and a consumer reads a slot only after the loader's flag
+// update that follows that vmcnt wait, so the flag orders the data.
+#include <cstdlib>
+#include <cstring>
+
+#include "kernels.hpp"
+#include "prof.hpp"
+
+namespace m2s {
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int ROWB = 128;            // bytes per LDS row: 32 channels [hi 32 | lo 32] bf16
+constexpr int NS = 3;                // ring slots
+constexpr unsigned SPIN_MAX = 1u << 20;  // ~0.1 s of polls: a broken protocol gives wrong results, not a hang
+
+__device__ __attribute__((aligned(16))) uint4 g_se_ws_zero[4];  // DMA source of padding lanes
+
+// physical 16-byte chunk of logical chunk c in LDS row r: c ^ (r & 6) (gemm128.hip swz128<SP>: a fragment
+// reads chunks g (hi) and g + 4 (lo) of row r16, conflict-free for ds_read_b128's lane groups)
+__device__ __forceinline__ int swz(int r) { return r & 6; }
+
+__device__ __forceinline__ void dma16(const void* src, uint32_t lds_wave_base) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds_wave_base)
+               : "memory");
+}
+__device__ __forceinline__ uint32_t lds_u32(const void* p) { return (uint32_t)(uintptr_t)p; }
+
+// flag poll: one ds_read (all lanes read the same dword), then a scalar copy; bounded
+__device__ __forceinline__ void wait_flag(uint32_t addr, unsigned target) {
+  for (unsigned i = 0; i < SPIN_MAX; ++i) {
+    unsigned v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    if (__builtin_amdgcn_readfirstlane(v) >= target) return;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+__device__ __forceinline__ void bump_flag(uint32_t addr, int lane) {
+  if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"(addr), "v"(1u) : "memory");
+}
+
+struct SeWsArgs {
+  const uint8_t* x;     // interleaved split activations
+  const uint8_t* w;     // split weight rows
+  const float* bias;    // [n_pad]
+  const uint8_t* gate;  // split gates
+  const bf16_t* res;    // split skip or null
+  bf16_t* y;            // split output
+  int M, P, cs_in, cs_out, n_tiles_m;
+};
+
+template <int WM, int WN, int NT, int NL>
+__global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeWsArgs a) {
+  constexpr int NC = WM * WN;                       // consumer waves
+  constexpr int BM = 64 * WM, BN = 16 * NT * WN, MT = 4;
+  constexpr int BLK = (BN + BM) / 8;                // 8-row (1 KB) DMA blocks per step: weights, then activations
+  static_assert(BLK % NL == 0, "DMA blocks per loader");
+  constexpr int PER = BLK / NL;                     // DMAs per loader wave per step
+  static_assert(2 * PER <= 63, "two steps in flight per loader within vmcnt");
+  constexpr int SLOT = (BN + BM) * ROWB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nimg = BM / a.P > 0 ? BM / a.P : 1;     // images a tile covers (P % BM == 0 or BM % P == 0)
+  const int gimg = (2 * a.cs_in * 2 + 1023) / 1024 * 1024;  // LDS bytes of one image's split gate row
+  char* gbuf = smem + NS * SLOT;                    // [2][nimg][gimg]
+  unsigned* flags = reinterpret_cast<unsigned*>(gbuf + 2 * nimg * gimg);  // FULL[NS], FREE[NS]
+  const uint32_t full0 = lds_u32(flags), free0 = lds_u32(flags + NS);
+  const int nsteps = a.cs_in / 32;
+  const int n_tiles = a.n_tiles_m;                  // one n tile: BN covers cs_out
+  const int my_tiles = (int)blockIdx.x < n_tiles ? (n_tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+
+  if (tid < 2 * NS) flags[tid] = 0u;
+  __syncthreads();  // the only workgroup barrier
+
+  if (wave >= NC) {
+    // ---------------------------------------------------------------- loaders
+    const int l = wave - NC;
+    const char* zp = reinterpret_cast<const char*>(g_se_ws_zero);
+    const int lrow = lane >> 3, pch = lane & 7;
+    // this loader's blocks b = l + NL j: weight rows (b < BN / 8) or activation rows; a lane's row and
+    // logical chunk follow from (b, lane) with a few integer ops per DMA (precomputed per block they were
+    // 3 x PER registers, which spilled the consumer role)
+    const int wrow_b = a.cs_in * 4, wlo = a.cs_in * 2;
+    int s = 0;
+    for (int it = 0; it < my_tiles; ++it) {
+      const int tile = blockIdx.x + it * gridDim.x;
+      const int m0 = tile * BM;
+      const uint8_t* xt = a.x + (size_t)m0 * a.cs_in * 4;
+      for (int st = 0; st < nsteps; ++st, ++s) {
+        const int slot = s % NS, use = s / NS;
+        if (use > 0) wait_flag(free0 + 4 * slot, (unsigned)(NC * use));
+        if (st == 0 && l == 0) {  // the tile's gate rows: nimg x 2 cs_in bf16, 16 B a lane
+          const int img0 = m0 / a.P, nb = (2 * a.cs_in * 2) / 16;
+          char* gdst = gbuf + (it & 1) * nimg * gimg;
+          for (int im = 0; im < nimg; ++im)
+            for (int o = 0; o < gimg / 16; o += 64) {
+              const int e = o + lane;
+              const bool ok = e < nb && (img0 + im) * a.P < a.M;
+              const void* src = ok ? static_cast<const void*>(a.gate + ((size_t)(img0 + im) * a.cs_in * 2 * 2 + e * 16))
+                                   : static_cast<const void*>(zp);
+              dma16(src, lds_u32(gdst + im * gimg + o * 16));
+            }
+        }
+        char* base = smem + slot * SLOT;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+          const int b = l + NL * j, r = b * 8 + lrow;
+          const int c = pch ^ swz(r & 15);
+          const void* src;
+          if (b < BN / 8) {
+            src = a.w + ((size_t)r * wrow_b + (c < 4 ? c * 16 : wlo + (c - 4) * 16) + st * 64);
+          } else {
+            const int m = m0 + r - BN;
+            src = m < a.M ? static_cast<const void*>(xt + ((r - BN) * wrow_b + c * 16 + st * ROWB))
+                          : static_cast<const void*>(zp);
+          }
+          dma16(src, lds_u32(base + b * 1024));
+        }
+        if (s > 0) {  // step s - 1 landed: everything but this step's PER DMAs retired
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+          bump_flag(full0 + 4 * ((s - 1) % NS), lane);
+        }
+      }
+    }
+    if (s > 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bump_flag(full0 + 4 * ((s - 1) % NS), lane);
+    }
+    return;
+  }
+
+  // ---------------------------------------------------------------- consumers
+  const int wm = wave / WN, wn = wave % WN;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int sw = swz(r16);
+  const uint32_t ch0 = (uint32_t)((g ^ sw) << 4), ch1 = (uint32_t)(((g + 4) ^ sw) << 4);
+  const uint32_t sm0 = lds_u32(smem);
+  const uint32_t a_lds0 = sm0 + (uint32_t)((wn * NT * 16 + r16) * ROWB);
+  const uint32_t b_lds0 = sm0 + (uint32_t)((BN + wm * 64 + r16) * ROWB);
+  const uint32_t g_lds0 = lds_u32(gbuf) + (uint32_t)(g * 16);
+  int s = 0;
+  for (int it = 0; it < my_tiles; ++it) {
+    const int tile = blockIdx.x + it * gridDim.x;
+    const int m0 = tile * BM;
+    const int wimg = (min(m0 + wm * 64, a.M - 1)) / a.P - m0 / a.P;  // this wave's image within the tile
+    const uint32_t gl = g_lds0 + (uint32_t)(((it & 1) * nimg + wimg) * gimg);
+    f32x4 acc[NT][MT];
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) acc[ni][mi] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int st = 0; st < nsteps; ++st, ++s) {
+      const int slot = s % NS, use = s / NS;
+      wait_flag(full0 + 4 * slot, (unsigned)(NL * (use + 1)));
+      const uint32_t so = (uint32_t)(slot * SLOT);
+      // gates k = 32 st + 8 g + j (hi and lo halves) and the MT activation fragments first; their gating
+      // runs while the NT weight fragments are read; the slot is released once those returned too
+      u32x4 gh, glo, bh[MT], bl[MT], ah[NT], al[NT];
+      const uint32_t ga = gl + (uint32_t)(st * 64), ba0 = b_lds0 + so + ch0, ba1 = b_lds0 + so + ch1;
+      const uint32_t gal = ga + (uint32_t)(a.cs_in * 2);  // the lo halves of the gate row
+      asm volatile(
+          "ds_read_b128 %0, %10\n\tds_read_b128 %1, %13\n\t"
+          "ds_read_b128 %2, %11\n\tds_read_b128 %3, %12\n\tds_read_b128 %4, %11 offset:2048\n\t"
+          "ds_read_b128 %5, %12 offset:2048\n\tds_read_b128 %6, %11 offset:4096\n\tds_read_b128 %7, %12 offset:4096\n\t"
+          "ds_read_b128 %8, %11 offset:6144\n\tds_read_b128 %9, %12 offset:6144\n\ts_waitcnt lgkmcnt(0)"
+          : "=&v"(gh), "=&v"(glo), "=&v"(bh[0]), "=&v"(bl[0]), "=&v"(bh[1]), "=&v"(bl[1]), "=&v"(bh[2]), "=&v"(bl[2]),
+            "=&v"(bh[3]), "=&v"(bl[3])
+          : "v"(ga), "v"(ba0), "v"(ba1), "v"(gal)
+          : "memory");
+      static_assert(MT == 4, "the read statement above covers four 16-row fragments");
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) {
+        const uint32_t aa = a_lds0 + so + (uint32_t)(ni * 16 * ROWB);
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3" : "=&v"(ah[ni]), "=&v"(al[ni]) : "v"(aa + ch0), "v"(aa + ch1) : "memory");
+      }
+      // gate hi + lo (fp32), gated activations re-split (17 significant bits kept)
+      float gsc[8], gl8[8];
+      unpack_bf16x4(make_uint2(gh[0], gh[1]), gsc);
+      unpack_bf16x4(make_uint2(gh[2], gh[3]), gsc + 4);
+      unpack_bf16x4(make_uint2(glo[0], glo[1]), gl8);
+      unpack_bf16x4(make_uint2(glo[2], glo[3]), gl8 + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gsc[j] += gl8[j];
+      // per activation fragment: gate + re-split, then its NT x 3 MFMAs (the next fragment's VALU
+      // overlaps them); the slot is released after the first fragment, once the weight reads returned
+      auto gate_frag = [&](int mi, bf16x8& xh, bf16x8& xl) {
+        float v[8], w[8];
+        unpack_bf16x4(make_uint2(bh[mi][0], bh[mi][1]), v);
+        unpack_bf16x4(make_uint2(bh[mi][2], bh[mi][3]), v + 4);
+        unpack_bf16x4(make_uint2(bl[mi][0], bl[mi][1]), w);
+        unpack_bf16x4(make_uint2(bl[mi][2], bl[mi][3]), w + 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (v[j] + w[j]) * gsc[j];
+        uint2 h0, l0, h1, l1;
+        split4(v, h0, l0);
+        split4(v + 4, h1, l1);
+        xh = __builtin_bit_cast(bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+        xl = __builtin_bit_cast(bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+      };
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) {
+        bf16x8 xh, xl;
+        gate_frag(mi, xh, xl);
+        if (mi == 0) {  // every read of the slot returned: release it to the loaders
+          static_assert(NT <= 8, "wait operands");
+          if constexpr (NT == 4)
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ah[0]), "+v"(al[0]), "+v"(ah[1]), "+v"(al[1]), "+v"(ah[2]),
+                         "+v"(al[2]), "+v"(ah[3]), "+v"(al[3])::"memory");
+          else
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ah[0]), "+v"(al[0]), "+v"(ah[1]), "+v"(al[1]), "+v"(ah[2]),
+                         "+v"(al[2]), "+v"(ah[3]), "+v"(al[3]), "+v"(ah[NT > 4 ? 4 : 0]), "+v"(al[NT > 4 ? 4 : 0]),
+                         "+v"(ah[NT > 5 ? 5 : 0]), "+v"(al[NT > 5 ? 5 : 0]), "+v"(ah[NT > 6 ? 6 : 0]),
+                         "+v"(al[NT > 6 ? 6 : 0]), "+v"(ah[NT > 7 ? 7 : 0]), "+v"(al[NT > 7 ? 7 : 0])::"memory");
+          bump_flag(free0 + 4 * slot, lane);
+        }
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni) {
+          const bf16x8 wh = __builtin_bit_cast(bf16x8, ah[ni]), wl = __builtin_bit_cast(bf16x8, al[ni]);
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xh, acc[ni][mi], 0, 0, 0);
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xl, acc[ni][mi], 0, 0, 0);
+          acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xh, acc[ni][mi], 0, 0, 0);
+        }
+      }
+    }
+
+    // ---- epilogue: lane = 4 consecutive output channels of one position; skip operand fetched first
+    const bf16_t* __restrict__ R = a.res;
+    bf16_t* __restrict__ Y = a.y;
+    uint2 rv[MT][NT][2];
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) {
+        const int m = m0 + wm * 64 + mi * 16 + r16, n4 = wn * NT * 16 + ni * 16 + 4 * g;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          rv[mi][ni][h] = (R && m < a.M && n4 < a.cs_out)
+                              ? *reinterpret_cast<const uint2*>(R + (size_t)m * a.cs_out * 2 + h * a.cs_out + n4)
+                              : make_uint2(0u, 0u);
+      }
+    float4 bias4[NT];
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni) {
+      const int n4 = wn * NT * 16 + ni * 16 + 4 * g;
+      bias4[ni] = n4 < a.cs_out ? *reinterpret_cast<const float4*>(a.bias + n4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) {
+      const int m = m0 + wm * 64 + mi * 16 + r16;
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) {
+        const int n4 = wn * NT * 16 + ni * 16 + 4 * g;
+        if (n4 >= a.cs_out) continue;
+        const float4 bb = bias4[ni];
+        float r[4], rl[4];
+        unpack_bf16x4(rv[mi][ni][0], r);
+        unpack_bf16x4(rv[mi][ni][1], rl);
+        const float v[4] = {acc[ni][mi][0] + bb.x + (r[0] + rl[0]), acc[ni][mi][1] + bb.y + (r[1] + rl[1]),
+                            acc[ni][mi][2] + bb.z + (r[2] + rl[2]), acc[ni][mi][3] + bb.w + (r[3] + rl[3])};
+        uint2 hi, lo;
+        split4(v, hi, lo);
+        bf16_t* yo = Y + (size_t)m * a.cs_out * 2 + n4;
+        *reinterpret_cast<uint2*>(yo) = hi;
+        *reinterpret_cast<uint2*>(yo + a.cs_out) = lo;
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int NT, int NL>
+void launch_cfg(SeWsArgs& a, hipStream_t s, double flops, double bytes) {
+  constexpr int BM = 64 * WM, BN = 16 * NT * WN;
+  const void* fn = reinterpret_cast<const void*>(&se_ws_kernel<WM, WN, NT, NL>);
+  allow_lds(fn);
+  const int nimg = BM / a.P > 0 ? BM / a.P : 1;
+  const int gimg = (2 * a.cs_in * 2 + 1023) / 1024 * 1024;
+  const size_t lds = (size_t)NS * (BN + BM) * ROWB + (size_t)2 * nimg * gimg + 2 * NS * sizeof(unsigned);
+  M2S_CHECK(lds <= 160 * 1024, "se_ws: LDS budget");
+  M2S_CHECK(BM % a.P == 0 || a.P % BM == 0, "se_ws: tile rows vs image size");
+  M2S_CHECK(a.cs_out <= BN, "se_ws: one n tile covers the outputs");
+  M2S_CHECK(a.cs_in / 32 >= NS, "se_ws: K steps per tile >= ring slots (gate rows are double-buffered per tile)");
+  a.n_tiles_m = ceil_div(a.M, BM);
+  const dim3 grid(std::min(a.n_tiles_m, device_cus()));
+  char name[64];
+  snprintf(name, sizeof(name), "se_ws_kernel<%d, %d, %d, %d>", WM, WN, NT, NL);  // rocprof's symbol
+  ProfScope ps(name, flops, bytes, s);
+  hipLaunchKernelGGL((se_ws_kernel<WM, WN, NT, NL>), grid, dim3(64 * (WM * WN + NL)), lds, s, a);
+  M2S_HIP(hipGetLastError());
+}
+
+}  // namespace
+
+bool se_ws_supported(int P, int cs_in, int cs_out) {
+  return cs_in % 32 == 0 && cs_in / 32 >= NS && ((P % 256 == 0 && cs_out <= 128) || (P == 64 && cs_out > 128 && cs_out <= 224));
+}
+
+void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_pad, const float* bias, const void* gate,
+                  const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes) {
+  M2S_CHECK(se_ws_supported(P, cs_in, cs_out) && M % P == 0 && cs_out % 4 == 0, "se_ws: unsupported shape");
+  M2S_CHECK(x && w && bias && gate && y && y != res && y != x, "se_ws: operand pointers");
+  M2S_CHECK((double)M * cs_in * 4 < 2147483647.0 * 2, "se_ws: input too large");
+  if (M <= 0) return;
+  SeWsArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.x = static_cast<const uint8_t*>(x);
+  a.w = static_cast<const uint8_t*>(w);
+  a.bias = bias;
+  a.gate = static_cast<const uint8_t*>(gate);
+  a.res = static_cast<const bf16_t*>(res);
+  a.y = static_cast<bf16_t*>(y);
+  a.M = M;
+  a.P = P;
+  a.cs_in = cs_in;
+  a.cs_out = cs_out;
+  if (cs_out <= 128) {
+    M2S_CHECK(n_pad >= 128, "se_ws: weight rows");
+    launch_cfg<4, 2, 4, 2>(a, s, flops, bytes);  // 256 x 128 (one 16x16 image), 8 consumers + 2 loaders
+  } else {
+    M2S_CHECK(n_pad >= 224, "se_ws: weight rows");
+    launch_cfg<2, 2, 7, 2>(a, s, flops, bytes);  // 128 x 224 (two 8x8 images), 4 consumers + 2 loaders
+  }
+}
+
+}  // namespace m2s

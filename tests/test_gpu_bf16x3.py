@@ -206,3 +206,24 @@ def test_effnet_bf16x3_se_gemm128_path(rt, ac_state, monkeypatch):
         got = eng.probe(x, i).cpu().numpy()
         assert _rel(got, taps[i].numpy()) <= 1e-4, f"block {i}: rel err {_rel(got, taps[i].numpy())}"
     assert _rel(eng.effnet(x).cpu().numpy(), effnet.effnet_gap(sd, fr).numpy()) <= 1e-4
+
+
+@pytest.mark.parametrize("n", [5, 300, 600])
+def test_se_ws_matches_barrier_ring(rt, ac_state, monkeypatch, n):
+    """The SE-gated conv_pwl on the warp-specialised flag ring (se_ws.hip: loader / consumer waves, FULL /
+    FREE counters in LDS, the ring running across tiles) against conv_gemm's barrier ring (M2S_SE_WS=0):
+    the same split fp32 products in the same K order, so the two agree to the last split rounding.
+    5 frames: a half-empty last 8x8 tile; 300 / 600: more 16x16 / 8x8 tiles than workgroups (each
+    workgroup walks several tiles and its ring carries over)."""
+    fr = torch.from_numpy(synth.synth_frames(1, n, seed=41)[0]).to(DEV)
+    ws = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    monkeypatch.setenv("M2S_SE_WS", "0")
+    ring = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    for i in (13, 18, 20, 28):  # after blocks 4.0 (16x16, no skip), 4.5, 5.1 (8x8, skip), 5.9
+        a, b = ws.probe(fr, i).cpu().numpy(), ring.probe(fr, i).cpu().numpy()
+        assert np.isfinite(a).all() and _rel(a, b) <= 1e-5, f"tap {i}: {_rel(a, b)}"
+    assert _rel(ws.effnet(fr).cpu().numpy(), ring.effnet(fr).cpu().numpy()) <= 1e-5
+    if n == 5:  # and against the fp32 oracle
+        sd = {k: torch.from_numpy(v) for k, v in ac_state.items()}
+        ref = effnet.effnet_gap(sd, fr.cpu()).numpy()
+        assert _rel(ws.effnet(fr).cpu().numpy(), ref) <= 1e-4
