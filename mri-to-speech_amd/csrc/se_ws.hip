@@ -40,7 +40,6 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int ROWB = 128;            // bytes per LDS row: 32 channels [hi 32 | lo 32] bf16
-constexpr int NS = 3;                // ring slots
 constexpr unsigned SPIN_MAX = 1u << 20;  // ~0.1 s of polls: a broken protocol gives wrong results, not a hang
 
 __device__ __attribute__((aligned(16))) uint4 g_se_ws_zero[4];  // DMA source of padding lanes
@@ -81,14 +80,15 @@ struct SeWsArgs {
   int M, P, cs_in, cs_out, n_tiles_m;
 };
 
-template <int WM, int WN, int NT, int NL>
+// NS ring slots; a loader keeps IF steps in flight behind the one it publishes (IF <= NS - 1)
+template <int WM, int WN, int NT, int NL, int NS, int IF>
 __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeWsArgs a) {
   constexpr int NC = WM * WN;                       // consumer waves
   constexpr int BM = 64 * WM, BN = 16 * NT * WN, MT = 4;
   constexpr int BLK = (BN + BM) / 8;                // 8-row (1 KB) DMA blocks per step: weights, then activations
   static_assert(BLK % NL == 0, "DMA blocks per loader");
   constexpr int PER = BLK / NL;                     // DMAs per loader wave per step
-  static_assert(2 * PER <= 63, "two steps in flight per loader within vmcnt");
+  static_assert((IF + 1) * PER <= 63 && IF >= 1 && IF <= NS - 1, "steps in flight per loader within vmcnt");
   constexpr int SLOT = (BN + BM) * ROWB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -150,15 +150,21 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
           }
           dma16(src, lds_u32(base + b * 1024));
         }
-        if (s > 0) {  // step s - 1 landed: everything but this step's PER DMAs retired
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-          bump_flag(full0 + 4 * ((s - 1) % NS), lane);
+        if (s >= IF) {  // step s - IF landed: everything but the IF younger steps' DMAs retired
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(IF * PER) : "memory");
+          bump_flag(full0 + 4 * ((s - IF) % NS), lane);
         }
       }
     }
-    if (s > 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      bump_flag(full0 + 4 * ((s - 1) % NS), lane);
+    // the last IF steps (fewer if the workgroup had fewer steps), oldest first
+#pragma unroll
+    for (int k = IF - 1; k >= 0; --k) {
+      const int q = s - 1 - k;
+      if (q < 0 || q < s - IF) continue;
+      if (k == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+      else if (k == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bump_flag(full0 + 4 * (q % NS), lane);
     }
     return;
   }
@@ -258,29 +264,33 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
       }
     }
 
-    // ---- epilogue: lane = 4 consecutive output channels of one position; skip operand fetched first
+    // ---- epilogue: lane = 4 consecutive output channels of one position.  The skip rows of fragment
+    // mi + 1 are fetched while fragment mi is finished (all of them at once spilled the NT = 7 variant)
     const bf16_t* __restrict__ R = a.res;
     bf16_t* __restrict__ Y = a.y;
-    uint2 rv[MT][NT][2];
-#pragma unroll
-    for (int mi = 0; mi < MT; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < NT; ++ni) {
-        const int m = m0 + wm * 64 + mi * 16 + r16, n4 = wn * NT * 16 + ni * 16 + 4 * g;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-          rv[mi][ni][h] = (R && m < a.M && n4 < a.cs_out)
-                              ? *reinterpret_cast<const uint2*>(R + (size_t)m * a.cs_out * 2 + h * a.cs_out + n4)
-                              : make_uint2(0u, 0u);
-      }
     float4 bias4[NT];
 #pragma unroll
     for (int ni = 0; ni < NT; ++ni) {
       const int n4 = wn * NT * 16 + ni * 16 + 4 * g;
       bias4[ni] = n4 < a.cs_out ? *reinterpret_cast<const float4*>(a.bias + n4) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    auto load_res = [&](int mi, uint2 (&rv)[NT][2]) {
+      const int m = m0 + wm * 64 + mi * 16 + r16;
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) {
+        const int n4 = wn * NT * 16 + ni * 16 + 4 * g;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          rv[ni][h] = (R && m < a.M && n4 < a.cs_out)
+                          ? *reinterpret_cast<const uint2*>(R + (size_t)m * a.cs_out * 2 + h * a.cs_out + n4)
+                          : make_uint2(0u, 0u);
+      }
+    };
+    uint2 rv[2][NT][2];
+    load_res(0, rv[0]);
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) {
+      if (mi + 1 < MT) load_res(mi + 1, rv[(mi + 1) & 1]);
       const int m = m0 + wm * 64 + mi * 16 + r16;
       if (m >= a.M) continue;
 #pragma unroll
@@ -289,8 +299,8 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
         if (n4 >= a.cs_out) continue;
         const float4 bb = bias4[ni];
         float r[4], rl[4];
-        unpack_bf16x4(rv[mi][ni][0], r);
-        unpack_bf16x4(rv[mi][ni][1], rl);
+        unpack_bf16x4(rv[mi & 1][ni][0], r);
+        unpack_bf16x4(rv[mi & 1][ni][1], rl);
         const float v[4] = {acc[ni][mi][0] + bb.x + (r[0] + rl[0]), acc[ni][mi][1] + bb.y + (r[1] + rl[1]),
                             acc[ni][mi][2] + bb.z + (r[2] + rl[2]), acc[ni][mi][3] + bb.w + (r[3] + rl[3])};
         uint2 hi, lo;
@@ -303,10 +313,11 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
   }
 }
 
-template <int WM, int WN, int NT, int NL>
+template <int WM, int WN, int NT, int NL, int NS, int IF>
 void launch_cfg(SeWsArgs& a, hipStream_t s, double flops, double bytes) {
+  static_assert(IF <= 3, "tail waits");
   constexpr int BM = 64 * WM, BN = 16 * NT * WN;
-  const void* fn = reinterpret_cast<const void*>(&se_ws_kernel<WM, WN, NT, NL>);
+  const void* fn = reinterpret_cast<const void*>(&se_ws_kernel<WM, WN, NT, NL, NS, IF>);
   allow_lds(fn);
   const int nimg = BM / a.P > 0 ? BM / a.P : 1;
   const int gimg = (2 * a.cs_in * 2 + 1023) / 1024 * 1024;
@@ -318,16 +329,16 @@ void launch_cfg(SeWsArgs& a, hipStream_t s, double flops, double bytes) {
   a.n_tiles_m = ceil_div(a.M, BM);
   const dim3 grid(std::min(a.n_tiles_m, device_cus()));
   char name[64];
-  snprintf(name, sizeof(name), "se_ws_kernel<%d, %d, %d, %d>", WM, WN, NT, NL);  // rocprof's symbol
+  snprintf(name, sizeof(name), "se_ws_kernel<%d, %d, %d, %d, %d, %d>", WM, WN, NT, NL, NS, IF);  // rocprof's symbol
   ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((se_ws_kernel<WM, WN, NT, NL>), grid, dim3(64 * (WM * WN + NL)), lds, s, a);
+  hipLaunchKernelGGL((se_ws_kernel<WM, WN, NT, NL, NS, IF>), grid, dim3(64 * (WM * WN + NL)), lds, s, a);
   M2S_HIP(hipGetLastError());
 }
 
 }  // namespace
 
 bool se_ws_supported(int P, int cs_in, int cs_out) {
-  return cs_in % 32 == 0 && cs_in / 32 >= NS && ((P % 256 == 0 && cs_out <= 128) || (P == 64 && cs_out > 128 && cs_out <= 224));
+  return cs_in % 32 == 0 && cs_in / 32 >= 5 && ((P % 256 == 0 && cs_out <= 128) || (P == 64 && cs_out > 128 && cs_out <= 224));
 }
 
 void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_pad, const float* bias, const void* gate,
@@ -348,12 +359,25 @@ void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_p
   a.P = P;
   a.cs_in = cs_in;
   a.cs_out = cs_out;
+  // tile / ring variants (M2S_SE_WS_CFG, A/B only; 0 = the default)
+  static const int cfg = [] {
+    const char* e = std::getenv("M2S_SE_WS_CFG");
+    return e ? std::atoi(e) : 0;
+  }();
   if (cs_out <= 128) {
     M2S_CHECK(n_pad >= 128, "se_ws: weight rows");
-    launch_cfg<4, 2, 4, 2>(a, s, flops, bytes);  // 256 x 128 (one 16x16 image), 8 consumers + 2 loaders
+    switch (cfg) {
+      case 1: return launch_cfg<4, 2, 4, 2, 3, 1>(a, s, flops, bytes);  // 256 x 128, 3 slots, 1 step in flight
+      case 2: return launch_cfg<2, 2, 4, 4, 4, 2>(a, s, flops, bytes);  // 128 x 128, 4 slots, 2 in flight
+      case 3: return launch_cfg<2, 2, 4, 4, 4, 1>(a, s, flops, bytes);  // 128 x 128, 4 slots, 1 in flight
+      default: return launch_cfg<4, 2, 4, 4, 3, 2>(a, s, flops, bytes);  // 256 x 128 (one 16x16 image), 3 slots
+    }
   } else {
     M2S_CHECK(n_pad >= 224, "se_ws: weight rows");
-    launch_cfg<2, 2, 7, 2>(a, s, flops, bytes);  // 128 x 224 (two 8x8 images), 4 consumers + 2 loaders
+    switch (cfg) {
+      case 1: return launch_cfg<2, 2, 7, 2, 3, 1>(a, s, flops, bytes);  // 128 x 224 (two 8x8 images)
+      default: return launch_cfg<2, 2, 7, 4, 3, 2>(a, s, flops, bytes);
+    }
   }
 }
 
