@@ -88,6 +88,16 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
   for (int step = 0; step < T; ++step) {
     const int t = dir == 0 ? step : T - 1 - step;
     const int tprev = dir == 0 ? t - 1 : t + 1;
+    // this thread's gate pre-activations for the cell update (pairs p = tid + 256 k; B <= LP_BMAX = 64, so
+    // one B-tile pass), fetched before the barrier wait so their latency hides under it
+    float prf[2][4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int p = tid + 256 * k, u = p % LP_U, b = p / LP_U;
+      const float* pr = pre + ((size_t)b * T + t) * 8 * H + (size_t)dir * 4 * H + ug * LP_U + u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) prf[k][q] = b < B ? pr[q * H] : 0.f;
+    }
     if (step > 0) {
       // ---- wait until every workgroup of this direction published h_{t-1} -----------------
       if (tid == 0) {
@@ -150,7 +160,9 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
         for (int i = 0; i < 16; ++i) red[wave][j][8 * (i / 4) + 4 * kk + (i % 4)][l32] = acc[j][i];
       __syncthreads();
       // ---- cell update: thread -> (unit, sequence) pairs of these B tiles ---------------------
-      for (int p = tid; p < LP_U * LP_BT * 32; p += 256) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int p = tid + 256 * k;
         const int u = p % LP_U, bl = p / LP_U, j = bl / 32, b = bt0 * 32 + bl;
         if (b >= B) continue;
         float gs[4];
@@ -160,11 +172,10 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
           gs[g] = (red[0][j][r][bl % 32] + red[1][j][r][bl % 32]) + (red[2][j][r][bl % 32] + red[3][j][r][bl % 32]);
         }
         const int unit = ug * LP_U + u;
-        const float* pr = pre + ((size_t)b * T + t) * 8 * H + (size_t)dir * 4 * H;
-        const float gi = lstm_sig(pr[unit] + gs[0]);
-        const float gf = lstm_sig(pr[H + unit] + gs[1]);
-        const float gg = lstm_tanh(pr[2 * H + unit] + gs[2]);
-        const float go = lstm_sig(pr[3 * H + unit] + gs[3]);
+        const float gi = lstm_sig(prf[k][0] + gs[0]);
+        const float gf = lstm_sig(prf[k][1] + gs[1]);
+        const float gg = lstm_tanh(prf[k][2] + gs[2]);
+        const float go = lstm_sig(prf[k][3] + gs[3]);
         const float c = step > 0 ? gf * cst[u][b] + gi * gg : gi * gg;
         cst[u][b] = c;
         hsd[((size_t)b * T + t) * H + unit] = go * lstm_tanh(c);
