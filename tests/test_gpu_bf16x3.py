@@ -216,6 +216,7 @@ def test_se_ws_matches_barrier_ring(rt, ac_state, monkeypatch, n):
     5 frames: a half-empty last 8x8 tile; 300 / 600: more 16x16 / 8x8 tiles than workgroups (each
     workgroup walks several tiles and its ring carries over)."""
     fr = torch.from_numpy(synth.synth_frames(1, n, seed=41)[0]).to(DEV)
+    monkeypatch.setenv("M2S_SE_WS", "1")
     ws = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
     monkeypatch.setenv("M2S_SE_WS", "0")
     ring = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)

@@ -16,4 +16,4 @@ run() {  # run <name> <env...>
   echo "== $n: $(cut -c1-200 "$OUT/bench_$n.json")"
   grep -E "^# (se_ws|conv_gemm_kernel<128, 128, 4, 4, 2, 3, 2, 1>|ir_ws)" "$OUT/bench_$n.err"
 }
-run ring M2S_SE_WS=0 && run cfg0 M2S_SE_WS_CFG=0 && run cfg1 M2S_SE_WS_CFG=1 && run cfg2 M2S_SE_WS_CFG=2 && run cfg3 M2S_SE_WS_CFG=3
+run ring M2S_SE_WS=0 && run cfg0 M2S_SE_WS=1 M2S_SE_WS_CFG=0 && run cfg1 M2S_SE_WS=1 M2S_SE_WS_CFG=1 && run cfg2 M2S_SE_WS=1 M2S_SE_WS_CFG=2 && run cfg3 M2S_SE_WS=1 M2S_SE_WS_CFG=3
