@@ -98,8 +98,8 @@ class Acoustic {
   bool er_fused_ = true;    // bf16: EdgeResidual 32->128->32 in one kernel (env M2S_ER_FUSED=0 disables)
   bool se_sp_ = false;      // split: SE-gated conv_pwl on gemm128.hip (env M2S_SE_SP=1; default conv_gemm's in-LDS
                             // scaling: the two measured equal, 7.85 vs 7.88 ms per step, profiles/r03o_se_sp_ab.txt)
-  bool se_ws_ = false;     // split: SE-gated conv_pwl on the warp-specialised flag ring (se_ws.hip; env M2S_SE_WS=1;
-                            // default conv_gemm's barrier ring until the ring is measured faster on the box)
+  bool se_ws_ = true;      // split: SE-gated conv_pwl on the warp-specialised flag ring (se_ws.hip; env M2S_SE_WS=0:
+                            // conv_gemm's barrier ring; 8.03 -> 7.17 ms per step, gpurun_out s4a)
   bool er_mrg_ = true;      // split EdgeResidual blocks.1: merged W_hi / W_lo ring stages (env M2S_ER_MRG=0: one per
                             // slot; 2088 vs 2164 us per launch, gpurun_out r03er)
   bool ir_s2band_ = true;   // blocks.3.0: fused banded conv_pw + stride-2 depthwise (env M2S_IR_S2BAND=0: unfused)
