@@ -30,6 +30,7 @@
 //         distinct bank slots (searched exhaustively over plane strides).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "kernels.hpp"
@@ -39,6 +40,11 @@ namespace m2s {
 namespace {
 
 __device__ __attribute__((aligned(16))) uint4 g_ws_zero[4];  // DMA source of padding chunks
+#ifdef IRWS_TRACE
+// diagnostic ablations (M2S_IRWS_ABL bits): 1 = consumers skip their work, 2 = producers skip MFMA + epilogue,
+// 4 = no weight / tap DMA per slice (stale LDS weights); results are wrong by design
+__device__ int g_irws_abl;
+#endif
 
 constexpr int WS_SL = 32;  // expanded channels per slice
 constexpr int WS_BR = 8;   // output rows per band
@@ -83,7 +89,7 @@ __host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mi
   L.tile_bytes = 2 * 8 * L.TROWS * 16;
   L.w_bytes = 2 * (cs_in / 32) * 4096;
   const int nb = (H + WS_BR - 1) / WS_BR;
-  L.total = L.x_bytes + L.tile_bytes + L.w_bytes + (2 * 320 + 2 * 32 + 2 * WS_NC * 32) * 4 + (nb > 1 ? cs_mid * 4 : 0);
+  L.total = L.x_bytes + L.tile_bytes + L.w_bytes + (2 * 320 + 2 * 32 + 2 * WS_NC * 32) * 4 + (nb > 1 ? cs_mid * 4 : 0) + 16;
   return L;
 }
 
@@ -109,6 +115,8 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   float* bpl = wdl + 2 * 320;                                 // [2][32] expand bias
   float* red = bpl + 2 * 32;                                  // [2][WS_NC][32]
   float* se_acc = red + 2 * WS_NC * 32;                       // [cs_mid] (NB > 1)
+  // producer waves that finished slice f's MFMAs (monotonic): W(f + 2) may then overwrite W(f)'s slot
+  unsigned* pdone = reinterpret_cast<unsigned*>(smem + Lg.total - 16);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -142,6 +150,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     return d;
   };
 
+  if (tid == 0) *pdone = 0u;  // ordered before any use by the first barrier of the slice loop
   // the tiles' halo columns are zero for good (the producers write only interior columns)
   for (int i = tid; i < 2 * 8 * Lg.TROWS; i += 64 * (WS_NP + WS_NC)) {
     const int pl = i / Lg.TROWS, r = i - pl * Lg.TROWS, c = r % WT;
@@ -152,12 +161,14 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   auto issue_w = [&](int f, Step d) {  // the slice's expand weights (4 * KS DMA pieces) + expand bias
     const int sl = d.sl;
     char* base = wbuf + (f & 1) * KS * 4096;
-    if (wave == 0 && lane < 8) dma16(bpw + sl * WS_SL + 4 * lane, lds_addr(bpl + (f & 1) * 32));
-    const int q = (lane & 3) ^ swz_f((lane >> 4) & 3);
+    int ln = lane;  // rebuilt per call (asm barrier): hoisted lane offsets cost registers the consumers need
+    asm volatile("" : "+v"(ln));
+    if (wave == 0 && ln < 8) dma16(bpw + (sl * WS_SL + 4 * ln), lds_addr(bpl + (f & 1) * 32));
+    const int q = (ln & 3) ^ swz_f((ln >> 4) & 3);
     for (int j = wave; j < 4 * KS; j += WS_NP) {
       const int ks = j >> 2, plane = (j >> 1) & 1, half = j & 1;
-      const int row = sl * WS_SL + half * 16 + (lane >> 2);
-      dma16(wpw + (size_t)row * CS * 2 + plane * CS + ks * 32 + q * 8, lds_addr(base + ks * 4096 + plane * 2048 + half * 1024));
+      const int row = sl * WS_SL + half * 16 + (ln >> 2);
+      dma16(wpw + (row * CS * 2 + plane * CS + ks * 32 + q * 8), lds_addr(base + ks * 4096 + plane * 2048 + half * 1024));
     }
   };
   auto issue_wd = [&](int f, Step d) {  // the slice's depthwise taps [9][32] + bias: 80 lanes of 16 B
@@ -188,57 +199,92 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       dma16(src, lds_addr(xs + j * 1024));
     }
   };
-  auto produce = [&](int f, Step d) {
+  // after its MFMAs of slice f a producer wave counts itself done with W(f)'s slot; once all WS_NP are,
+  // it DMAs its pieces of W(f + 2) there, ~1.5 slices before they are needed (issued after the barrier
+  // of slice f + 1 they arrived one slice ahead only, and the wait for them was exposed: without the
+  // per-slice weight DMA ir_ws ran 11-15 % faster, ablation M2S_IRWS_ABL=4, gpurun_out)
+  auto after_mfma = [&](int f, bool more, Step d2) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"((uint32_t)(uintptr_t)pdone), "v"(1u) : "memory");
+    if (!more) return;
+    const unsigned target = (unsigned)(WS_NP * (f + 1));
+    for (unsigned n = 0; n < (1u << 20); ++n) {
+      unsigned v;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((uint32_t)(uintptr_t)pdone) : "memory");
+      if (__builtin_amdgcn_readfirstlane(v) >= target) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    issue_w(f + 2, d2);
+  };
+  auto produce = [&](int f, Step d, bool more, Step d2) {
     const int r0 = d.band * WS_BR, br = min(WS_BR, H - r0), xr0 = max(r0 - 1, 0), xr1 = min(r0 + WS_BR + 1, H);
     const int PB = (xr1 - xr0) * W, nunit = 2 * ((PB + 15) / 16);
     const char* wb = wbuf + (f & 1) * KS * 4096;
     const int hxl = hx_of(r16);
     // units = (16-position subtile t, 16-channel tile nt), dealt round-robin over the producer waves
-    // (9 subtiles x 2 on a 16x16 band: at most 3 units = 36 MFMAs a wave)
-    f32x4 acc[WS_UMAX];
-#pragma unroll
-    for (int k = 0; k < WS_UMAX; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // (9 subtiles x 2 on a 16x16 band: at most 3 units = 36 MFMAs a wave).  The wave's unit count NU is
+    // uniform, so each count gets a straight-line body: every fragment of a k-step is read at once and
+    // the next k-step's reads are issued before this one's MFMAs (with a runtime `u < nunit` test per
+    // unit the loads were issued and waited for unit by unit: the MFMA phase took ~2k cycles a slice
+    // for 12-36 MFMAs, in-kernel stamps gpurun_out t4a)
+    static_assert(WS_NP % 2 == 0, "unit -> channel tile");
     // every unit of a wave has the same 16-channel tile (u & 1 == wave & 1: WS_NP is even), so the
     // weight fragments are read once per k-step, not once per unit
-    static_assert(WS_NP % 2 == 0, "unit -> channel tile");
     const int wrow = (wave & 1) * 16 + r16;
     const int wo = wrow * 64 + ((g ^ swz_f((wrow >> 2) & 3)) << 4);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int Lh = ks * 4 + g, Ll = CPP + ks * 4 + g;
-      const int ph = ((Lh & ~15) | ((Lh & 15) ^ hxl)) << 4, pl = ((Ll & ~15) | ((Ll & 15) ^ hxl)) << 4;
-      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(wb + ks * 4096 + wo);
-      const bf16x8 al = *reinterpret_cast<const bf16x8*>(wb + ks * 4096 + 2048 + wo);
-#pragma unroll
-      for (int k = 0; k < WS_UMAX; ++k) {
-        const int u = wave + WS_NP * k;
-        if (u < nunit) {
-          const int t = u >> 1;
-          const char* xr = xs + (t * 16 + r16) * XP;
-          const bf16x8 bh = *reinterpret_cast<const bf16x8*>(xr + ph);
-          const bf16x8 bl = *reinterpret_cast<const bf16x8*>(xr + pl);
-          acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[k], 0, 0, 0);
-          acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[k], 0, 0, 0);
-          acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[k], 0, 0, 0);
-        }
-      }
-      asm volatile("" ::: "memory");  // one k-step of fragments in flight (registers)
-    }
-    TR(f, 6);
-    // bias + SiLU -> tile[f % 2]; lane holds channels 4g..4g+3 (of 16-channel tile nt) of position r16
+    const int nu = nunit > wave ? (nunit - wave + WS_NP - 1) / WS_NP : 0;
     char* tb = tiles + (f & 1) * 8 * PLT;
     const int trow0 = xr0 - r0 + 1;  // tile row of x row 0
+    // from LDS (staged with the weights): a global load here would make hipcc drain the DMA
+    const float4 bb = *reinterpret_cast<const float4*>(bpl + (f & 1) * 32 + (wave & 1) * 16 + 4 * g);
+    auto units = [&](auto nuc) {
+      constexpr int NU = decltype(nuc)::value;
+      f32x4 acc[NU];
 #pragma unroll
-    for (int k = 0; k < WS_UMAX; ++k) {
-      const int u = wave + WS_NP * k, nt = u & 1, m = (u >> 1) * 16 + r16;
-      if (u < nunit && m < PB) {
-        // from LDS (staged with the weights): a global load here would make hipcc drain the DMA
-        const float4 bb = *reinterpret_cast<const float4*>(bpl + (f & 1) * 32 + nt * 16 + 4 * g);
-        const int ti = (m / W + trow0) * WT + (m % W) + 1;
-        *reinterpret_cast<float4*>(tb + (nt * 4 + g) * PLT + ti * 16) =
-            make_float4(silu(acc[k][0] + bb.x), silu(acc[k][1] + bb.y), silu(acc[k][2] + bb.z), silu(acc[k][3] + bb.w));
+      for (int k = 0; k < NU; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bf16x8 ah[2], al[2], bh[2][NU], bl[2][NU];
+      auto load = [&](int ks, int bsel) {
+        const int Lh = ks * 4 + g, Ll = CPP + ks * 4 + g;
+        const int ph = ((Lh & ~15) | ((Lh & 15) ^ hxl)) << 4, pl = ((Ll & ~15) | ((Ll & 15) ^ hxl)) << 4;
+        ah[bsel] = *reinterpret_cast<const bf16x8*>(wb + ks * 4096 + wo);
+        al[bsel] = *reinterpret_cast<const bf16x8*>(wb + ks * 4096 + 2048 + wo);
+#pragma unroll
+        for (int k = 0; k < NU; ++k) {
+          const char* xr = xs + (((wave + WS_NP * k) >> 1) * 16 + r16) * XP;
+          bh[bsel][k] = *reinterpret_cast<const bf16x8*>(xr + ph);
+          bl[bsel][k] = *reinterpret_cast<const bf16x8*>(xr + pl);
+        }
+      };
+      load(0, 0);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int c = ks & 1;
+        if (ks + 1 < KS) load(ks + 1, c ^ 1);
+#pragma unroll
+        for (int k = 0; k < NU; ++k) {
+          acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[c], bh[c][k], acc[k], 0, 0, 0);
+          acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[c], bl[c][k], acc[k], 0, 0, 0);
+          acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[c], bh[c][k], acc[k], 0, 0, 0);
+        }
       }
-    }
+      TR(f, 6);
+      after_mfma(f, more, d2);
+      // bias + SiLU -> tile[f % 2]; lane holds channels 4g..4g+3 (of 16-channel tile nt) of position r16
+#pragma unroll
+      for (int k = 0; k < NU; ++k) {
+        const int u = wave + WS_NP * k, nt = u & 1, m = (u >> 1) * 16 + r16;
+        if (m < PB) {
+          const int ti = (m / W + trow0) * WT + (m % W) + 1;
+          *reinterpret_cast<float4*>(tb + (nt * 4 + g) * PLT + ti * 16) =
+              make_float4(silu(acc[k][0] + bb.x), silu(acc[k][1] + bb.y), silu(acc[k][2] + bb.z), silu(acc[k][3] + bb.w));
+        }
+      }
+    };
+    static_assert(WS_UMAX == 3, "unit counts 1..3");
+    if (nu == 3) units(std::integral_constant<int, 3>());
+    else if (nu == 2) units(std::integral_constant<int, 2>());
+    else if (nu == 1) units(std::integral_constant<int, 1>());
+    else after_mfma(f, more, d2);
     // halo rows outside the image (above the first band, below the last) hold zeros
     if (tid < 8 * W) {
       const int pl = tid / W, c = tid - pl * W;
@@ -286,7 +332,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
         a[1] += w[t][1] * u.y;
         a[2] += w[t][2] * u.z;
         a[3] += w[t][3] * u.w;
-        if (t % 3 == 2) asm volatile("" ::: "memory");  // one tap row of loads in flight (registers)
+        if (t == 5) asm volatile("" ::: "memory");  // two tap rows of loads in flight (registers)
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -309,12 +355,15 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     }
     TR(f + 1, 5);
     // squeeze partials: the wave's 8 pixel lanes of each plane (lane bits 3..5): a DPP row rotation
-    // inside each 16-lane row, then two cross-row shuffles; one row of 32 channels per wave
+    // inside each 16-lane row, then gfx950's row / half swaps (v_permlane16_swap, v_permlane32_swap: VALU,
+    // no LDS round trip, where two ds_bpermute shuffles were); one row of 32 channels per wave
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       s[j] += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s[j]), 0x128, 0xF, 0xF, false));
-      s[j] += __shfl_xor(s[j], 16);
-      s[j] += __shfl_xor(s[j], 32);
+      const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(s[j]), __float_as_uint(s[j]), false, false);
+      s[j] = __uint_as_float(q[0]) + __uint_as_float(q[1]);
+      const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(s[j]), __float_as_uint(s[j]), false, false);
+      s[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
     }
     if (lane < 8)
 #pragma unroll
@@ -336,11 +385,25 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
 
   // ---- the slice pipeline: producers on f = i, consumers on f = i - 1 (and the squeeze of i - 2) --
   Step cur{(int)blockIdx.x, 0, 0}, prev{}, prev2{};  // steps i, i - 1, i - 2
+  // DMA pieces a producer wave issues per slice (W pieces j = wave + 8 k of 4 KS, + the bias on wave 0)
+  const int npw = (wave < 4 * KS ? (4 * KS - 1 - wave) / WS_NP + 1 : 0) + (wave == 0 ? 1 : 0);
+  Step nxt = next_step(cur);
   if (prod && T > 0) issue_w(0, cur);
+  if (prod && T > 1) issue_w(1, nxt);
   for (int i = 0; i <= T + 1; ++i) {
-    const Step nxt = next_step(cur);
+    nxt = next_step(cur);
+    const Step nxt2 = next_step(nxt);
     TR(i, 0);
-    if (prod) wait_vm0();  // this wave's pieces of W(i) (and taps of i - 1) landed
+    if (prod) {  // this wave's pieces of W(i) (and taps of i - 1) landed; W(i + 1) may stay in flight
+      const int young = i + 1 < T ? npw : 0;
+      static_assert(4 * KS <= 4 * WS_NP, "pieces per wave");
+      if (young == 0) wait_vm0();
+      else if (young == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if (young == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else if (young == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (young == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else wait_vm0();
+    }
     TR(i, 1);
     lds_fence();
     __builtin_amdgcn_s_barrier();  // W(i) everywhere; tile[i % 2], W[(i + 1) % 2], taps[i % 2] free
@@ -352,15 +415,20 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       }
       __builtin_amdgcn_s_barrier();
     }
+#ifdef IRWS_TRACE
+    const int abl = g_irws_abl;
+#else
+    constexpr int abl = 0;
+#endif
     if (prod) {
-      if (i + 1 < T) issue_w(i + 1, nxt);
       TR(i, 4);
       if (i < T) {
-        issue_wd(i, cur);  // read by the consumers next iteration
+        if (!(abl & 4)) issue_wd(i, cur);  // read by the consumers next iteration
         TR(i, 5);
-        produce(i, cur);
+        if (!(abl & 2)) produce(i, cur, i + 2 < T && !(abl & 4), nxt2);
+        else after_mfma(i, i + 2 < T && !(abl & 4), nxt2);
       }
-    } else {  // no global loads here: the consumers' VM counter holds only their stores
+    } else if (!(abl & 1)) {  // no global loads here: the consumers' VM counter holds only their stores
       if (i >= 2) finalize(i - 2, prev2);
       if (i >= 1 && i <= T) consume(i - 1, prev);
     }
@@ -416,6 +484,13 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
     if (getenv("M2S_IR_WS_TRACE")) M2S_HIP(hipMalloc(&p, 64 * 2 * 8 * 64 * 8));
     return p;
   }();
+  static const int abl_set = [] {
+    const char* e = getenv("M2S_IRWS_ABL");
+    const int v = e ? atoi(e) : 0;
+    M2S_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_irws_abl), &v, sizeof(int)));
+    return v;
+  }();
+  (void)abl_set;
 #define M2S_IRWS_DUMP(tag) \
   if (tr) dump_trace(tr, s, tag);
 #else
