@@ -63,7 +63,7 @@ PRECISION = {
 }
 
 MFMA_KERNELS = ("conv_gemm_kernel", "gemm128_kernel", "conv_halo_kernel", "conv1d_halo", "conv_igemm_kernel", "ir_pwdw",
-                "ir_ws_kernel", "lstm_persistent_kernel", "rb1_fused_kernel", "stem_b0_kernel", "se_excite_kernel",
+                "ir_ws_kernel", "se_ws_kernel", "lstm_persistent_kernel", "rb1_fused_kernel", "stem_b0_kernel", "se_excite_kernel",
                 "er_fused_kernel", "er2_fused_kernel", "ers2_fused_kernel", "er_sp_kernel", "ers2_sp_kernel")
 
 
@@ -72,7 +72,8 @@ def kernel_arith(name: str, dtype: str) -> str:
     if name.startswith("lstm_persistent") or name.startswith("lstm_step") or "<float" in name:
         return "fp32"
     if dtype == "fp8":  # only the e4m3 kernels run fp8 MFMA; the rest of an fp8 engine is bf16
-        return "fp8" if name.startswith(("gemm128_kernel<0", "gemm128_kernel<1")) else "bf16"
+        e4m3 = name.startswith(("gemm128_kernel<0", "gemm128_kernel<1")) or (name.startswith("se_ws_kernel") and "true" in name)
+        return "fp8" if e4m3 else "bf16"
     return dtype
 
 

@@ -61,6 +61,13 @@ bool se_ws_supported(int P, int cs_in, int cs_out);
 void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_pad, const float* bias, const void* gate,
                   const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes);
 
+// fp8 engines: launch_se_gemm_f8's operation (e4m3 x8 / w8, bf16 gate / res / y) on the same warp-specialised
+// flag ring.  (se_ws.hip)
+bool se_ws_f8_supported(int P, int cs_in, int cs_out);
+void launch_se_ws_f8(const void* x8, int M, int P, int cs_in, const void* w8, int kp, int n_pad, const float* wscale,
+                     const float* bias, const void* gate, const void* res, void* y, int cs_out, hipStream_t s, double flops,
+                     double bytes);
+
 // The same for a stride-2 depthwise (TF-SAME, top / left pads pad_t / pad_l) on an IH x IW <= 256-pixel
 // conv_pw map: y (N, OH*OW, cs_mid), se_mean over the OH x OW output.  (ir_fused.hip)
 // Split-fp32 stride-1 IR front half (conv_pw + bn1 + SiLU + conv_dw + bn2 + SiLU + SE squeeze) on

@@ -659,7 +659,13 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         r2.act = ACT_SIGMOID;
         run_conv<T>(r2, b.se2, s);
         }
-        if (f8) {
+        if (f8 && se_ws_ && se_ws_f8_supported(nh * nw, cs, chan_stride(b.cout))) {
+          const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
+          launch_se_ws_f8(M2, nc * nh * nw, nh * nw, cs, arena_.ptr(b.f8_w), b.f8_kp, b.f8_npad,
+                          static_cast<const float*>(arena_.ptr(b.f8_s)), static_cast<const float*>(arena_.ptr(b.f8_b)),
+                          scale, b.skip ? cur : nullptr, nxt, chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
+                          rows * cs + 2.0 * rows * co * (b.skip ? 2.0 : 1.0) + (double)b.f8_npad * b.f8_kp + 2.0 * nc * cs);
+        } else if (f8) {
           const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
           launch_se_gemm_f8(M2, nc * nh * nw, nh * nw, cs, arena_.ptr(b.f8_w), b.f8_kp, b.f8_npad,
                             static_cast<const float*>(arena_.ptr(b.f8_s)), static_cast<const float*>(arena_.ptr(b.f8_b)),

@@ -44,9 +44,6 @@ constexpr unsigned SPIN_MAX = 1u << 20;  // ~0.1 s of polls: a broken protocol g
 
 __device__ __attribute__((aligned(16))) uint4 g_se_ws_zero[4];  // DMA source of padding lanes
 
-// physical 16-byte chunk of logical chunk c in LDS row r: c ^ (r & 6) (gemm128.hip swz128<SP>: a fragment
-// reads chunks g (hi) and g + 4 (lo) of row r16, conflict-free for ds_read_b128's lane groups)
-__device__ __forceinline__ int swz(int r) { return r & 6; }
 
 __device__ __forceinline__ void dma16(const void* src, uint32_t lds_wave_base) {
   unsigned keep;
@@ -71,17 +68,36 @@ __device__ __forceinline__ void bump_flag(uint32_t addr, int lane) {
 }
 
 struct SeWsArgs {
-  const uint8_t* x;     // interleaved split activations
-  const uint8_t* w;     // split weight rows
-  const float* bias;    // [n_pad]
-  const uint8_t* gate;  // split gates
-  const bf16_t* res;    // split skip or null
-  bf16_t* y;            // split output
-  int M, P, cs_in, cs_out, n_tiles_m;
+  const uint8_t* x;       // interleaved split activations; F8: e4m3 [M][cs_in]
+  const uint8_t* w;       // split weight rows; F8: e4m3 [n_pad][kp]
+  const float* bias;      // [n_pad]
+  const float* wscale;    // F8: per-output-channel weight scale [n_pad]
+  const uint8_t* gate;    // split gates; F8: bf16 [M / P][cs_in]
+  const bf16_t* res;      // split skip or null; F8: bf16 [M][cs_out]
+  bf16_t* y;              // split output; F8: bf16 [M][cs_out]
+  int M, P, cs_in, cs_out, n_tiles_m, kp;  // kp: F8 weight row bytes (cs_in rounded up to 128)
 };
 
-// NS ring slots; a loader keeps IF steps in flight behind the one it publishes (IF <= NS - 1)
-template <int WM, int WN, int NT, int NL, int NS, int IF>
+constexpr int E8M0_ONE = 0x7f7f7f7f;  // 2^0 block scale in every byte
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+// physical 16-byte chunk of logical chunk c in LDS row r: c ^ f(r).  Split rows: a fragment reads chunks g (hi)
+// and g + 4 (lo) of row r16, f(r) = r & 6; e4m3 rows (F8): chunks 2g and 2g + 1, f(r) = ((r >> 1) & 1) | (r & 4).
+// Both are conflict-free for ds_read_b128's lane groups (gemm128.hip swz128 / f8_swz)
+template <bool F8>
+__device__ __forceinline__ int swz_k(int r) { return F8 ? (((r >> 1) & 1) | (r & 4)) : (r & 6); }
+// 4 e4m3 (one dword) x 4 gates -> 4 e4m3 (gemm128.hip gate4; the gate is in (0, 1): no new saturation)
+__device__ __forceinline__ int gate4_f8(int d, const float* s) {
+  const f32x2_t lo = __builtin_amdgcn_cvt_pk_f32_fp8(d, false);
+  const f32x2_t hi = __builtin_amdgcn_cvt_pk_f32_fp8(d, true);
+  const int r = __builtin_amdgcn_cvt_pk_fp8_f32(lo[0] * s[0], lo[1] * s[1], 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(hi[0] * s[2], hi[1] * s[3], r, true);
+}
+
+// NS ring slots; a loader keeps IF steps in flight behind the one it publishes (IF <= NS - 1).  F8: the fp8
+// engines' e4m3 form (K step = 128 e4m3 channels, v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales,
+// the gate applied to the e4m3 activation fragments in registers, wscale in the epilogue, bf16 in / out) of
+// gemm128.hip KIND_F8_SE, on the same ring.
+template <int WM, int WN, int NT, int NL, int NS, int IF, bool F8>
 __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeWsArgs a) {
   constexpr int NC = WM * WN;                       // consumer waves
   constexpr int BM = 64 * WM, BN = 16 * NT * WN, MT = 4;
@@ -95,11 +111,12 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nimg = BM / a.P > 0 ? BM / a.P : 1;     // images a tile covers (P % BM == 0 or BM % P == 0)
-  const int gimg = (2 * a.cs_in * 2 + 1023) / 1024 * 1024;  // LDS bytes of one image's split gate row
+  const int grow = F8 ? a.cs_in * 2 : a.cs_in * 4;  // bytes of one image's gate row (bf16 / split bf16)
+  const int gimg = (grow + 1023) / 1024 * 1024;     // ... in LDS
   char* gbuf = smem + NS * SLOT;                    // [2][nimg][gimg]
   unsigned* flags = reinterpret_cast<unsigned*>(gbuf + 2 * nimg * gimg);  // FULL[NS], FREE[NS]
   const uint32_t full0 = lds_u32(flags), free0 = lds_u32(flags + NS);
-  const int nsteps = a.cs_in / 32;
+  const int nsteps = F8 ? a.kp / 128 : a.cs_in / 32;
   const int n_tiles = a.n_tiles_m;                  // one n tile: BN covers cs_out
   const int my_tiles = (int)blockIdx.x < n_tiles ? (n_tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
 
@@ -114,23 +131,23 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
     // this loader's blocks b = l + NL j: weight rows (b < BN / 8) or activation rows; a lane's row and
     // logical chunk follow from (b, lane) with a few integer ops per DMA (precomputed per block they were
     // 3 x PER registers, which spilled the consumer role)
-    const int wrow_b = a.cs_in * 4, wlo = a.cs_in * 2;
+    const int wrow_b = F8 ? a.kp : a.cs_in * 4, wlo = a.cs_in * 2, xrow_b = F8 ? a.cs_in : a.cs_in * 4;
     int s = 0;
     for (int it = 0; it < my_tiles; ++it) {
       const int tile = blockIdx.x + it * gridDim.x;
       const int m0 = tile * BM;
-      const uint8_t* xt = a.x + (size_t)m0 * a.cs_in * 4;
+      const uint8_t* xt = a.x + (size_t)m0 * xrow_b;
       for (int st = 0; st < nsteps; ++st, ++s) {
         const int slot = s % NS, use = s / NS;
         if (use > 0) wait_flag(free0 + 4 * slot, (unsigned)(NC * use));
         if (st == 0 && l == 0) {  // the tile's gate rows: nimg x 2 cs_in bf16, 16 B a lane
-          const int img0 = m0 / a.P, nb = (2 * a.cs_in * 2) / 16;
+          const int img0 = m0 / a.P, nb = grow / 16;
           char* gdst = gbuf + (it & 1) * nimg * gimg;
           for (int im = 0; im < nimg; ++im)
             for (int o = 0; o < gimg / 16; o += 64) {
               const int e = o + lane;
               const bool ok = e < nb && (img0 + im) * a.P < a.M;
-              const void* src = ok ? static_cast<const void*>(a.gate + ((size_t)(img0 + im) * a.cs_in * 2 * 2 + e * 16))
+              const void* src = ok ? static_cast<const void*>(a.gate + ((size_t)(img0 + im) * grow + e * 16))
                                    : static_cast<const void*>(zp);
               dma16(src, lds_u32(gdst + im * gimg + o * 16));
             }
@@ -139,14 +156,15 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
           const int b = l + NL * j, r = b * 8 + lrow;
-          const int c = pch ^ swz(r & 15);
+          const int c = pch ^ swz_k<F8>(r & 15);
           const void* src;
           if (b < BN / 8) {
-            src = a.w + ((size_t)r * wrow_b + (c < 4 ? c * 16 : wlo + (c - 4) * 16) + st * 64);
+            src = F8 ? a.w + ((size_t)r * wrow_b + st * ROWB + c * 16)
+                     : a.w + ((size_t)r * wrow_b + (c < 4 ? c * 16 : wlo + (c - 4) * 16) + st * 64);
           } else {
             const int m = m0 + r - BN;
-            src = m < a.M ? static_cast<const void*>(xt + ((r - BN) * wrow_b + c * 16 + st * ROWB))
-                          : static_cast<const void*>(zp);
+            const bool in = m < a.M && (!F8 || st * ROWB + c * 16 < a.cs_in);  // F8: zeros past cs_in
+            src = in ? static_cast<const void*>(xt + ((r - BN) * xrow_b + c * 16 + st * ROWB)) : static_cast<const void*>(zp);
           }
           dma16(src, lds_u32(base + b * 1024));
         }
@@ -172,12 +190,13 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
   // ---------------------------------------------------------------- consumers
   const int wm = wave / WN, wn = wave % WN;
   const int g = lane >> 4, r16 = lane & 15;
-  const int sw = swz(r16);
-  const uint32_t ch0 = (uint32_t)((g ^ sw) << 4), ch1 = (uint32_t)(((g + 4) ^ sw) << 4);
+  const int sw = swz_k<F8>(r16);
+  // a lane's two 16-byte chunks of a fragment row: split hi g / lo g + 4; F8 e4m3 2g, 2g + 1 (32 consecutive k)
+  const uint32_t ch0 = (uint32_t)(((F8 ? 2 * g : g) ^ sw) << 4), ch1 = (uint32_t)(((F8 ? 2 * g + 1 : g + 4) ^ sw) << 4);
   const uint32_t sm0 = lds_u32(smem);
   const uint32_t a_lds0 = sm0 + (uint32_t)((wn * NT * 16 + r16) * ROWB);
   const uint32_t b_lds0 = sm0 + (uint32_t)((BN + wm * 64 + r16) * ROWB);
-  const uint32_t g_lds0 = lds_u32(gbuf) + (uint32_t)(g * 16);
+  const uint32_t g_lds0 = lds_u32(gbuf) + (uint32_t)(g * (F8 ? 64 : 16));
   int s = 0;
   for (int it = 0; it < my_tiles; ++it) {
     const int tile = blockIdx.x + it * gridDim.x;
@@ -194,6 +213,63 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
       const int slot = s % NS, use = s / NS;
       wait_flag(full0 + 4 * slot, (unsigned)(NL * (use + 1)));
       const uint32_t so = (uint32_t)(slot * SLOT);
+      if constexpr (F8) {
+        // the lane's 32 gates k = 128 st + 32 g + j (bf16) and its MT activation fragments (e4m3 chunks 2g,
+        // 2g + 1 of a row), then the NT weight fragments; released once every read returned
+        u32x4 q[4], b0[MT], b1[MT], a0[NT], a1[NT];
+        const uint32_t ga = gl + (uint32_t)(st * 256), ba0 = b_lds0 + so + ch0, ba1 = b_lds0 + so + ch1;
+        asm volatile(
+            "ds_read_b128 %0, %12\n\tds_read_b128 %1, %12 offset:16\n\tds_read_b128 %2, %12 offset:32\n\t"
+            "ds_read_b128 %3, %12 offset:48\n\tds_read_b128 %4, %13\n\tds_read_b128 %5, %14\n\t"
+            "ds_read_b128 %6, %13 offset:2048\n\tds_read_b128 %7, %14 offset:2048\n\tds_read_b128 %8, %13 offset:4096\n\t"
+            "ds_read_b128 %9, %14 offset:4096\n\tds_read_b128 %10, %13 offset:6144\n\tds_read_b128 %11, %14 offset:6144\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(b0[0]), "=&v"(b1[0]), "=&v"(b0[1]), "=&v"(b1[1]),
+              "=&v"(b0[2]), "=&v"(b1[2]), "=&v"(b0[3]), "=&v"(b1[3])
+            : "v"(ga), "v"(ba0), "v"(ba1)
+            : "memory");
+        static_assert(MT == 4, "the read statement above covers four 16-row fragments");
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni) {
+          const uint32_t aa = a_lds0 + so + (uint32_t)(ni * 16 * ROWB);
+          asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3" : "=&v"(a0[ni]), "=&v"(a1[ni]) : "v"(aa + ch0), "v"(aa + ch1) : "memory");
+        }
+        float gs[32];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          unpack_bf16x4(make_uint2(q[i][0], q[i][1]), gs + 8 * i);
+          unpack_bf16x4(make_uint2(q[i][2], q[i][3]), gs + 8 * i + 4);
+        }
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi) {
+          i32x8 bx;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            bx[i] = gate4_f8((int)b0[mi][i], gs + 4 * i);
+            bx[4 + i] = gate4_f8((int)b1[mi][i], gs + 16 + 4 * i);
+          }
+          if (mi == 0) {  // every read of the slot returned: release it to the loaders
+            static_assert(NT <= 8, "wait operands");
+            if constexpr (NT == 4)
+              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0[0]), "+v"(a1[0]), "+v"(a0[1]), "+v"(a1[1]), "+v"(a0[2]),
+                           "+v"(a1[2]), "+v"(a0[3]), "+v"(a1[3])::"memory");
+            else
+              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0[0]), "+v"(a1[0]), "+v"(a0[1]), "+v"(a1[1]), "+v"(a0[2]),
+                           "+v"(a1[2]), "+v"(a0[3]), "+v"(a1[3]), "+v"(a0[NT > 4 ? 4 : 0]), "+v"(a1[NT > 4 ? 4 : 0]),
+                           "+v"(a0[NT > 5 ? 5 : 0]), "+v"(a1[NT > 5 ? 5 : 0]), "+v"(a0[NT > 6 ? 6 : 0]),
+                           "+v"(a1[NT > 6 ? 6 : 0]), "+v"(a0[NT > 7 ? 7 : 0]), "+v"(a1[NT > 7 ? 7 : 0])::"memory");
+            bump_flag(free0 + 4 * slot, lane);
+          }
+#pragma unroll
+          for (int ni = 0; ni < NT; ++ni) {
+            const i32x8 af = {(int)a0[ni][0], (int)a0[ni][1], (int)a0[ni][2], (int)a0[ni][3],
+                              (int)a1[ni][0], (int)a1[ni][1], (int)a1[ni][2], (int)a1[ni][3]};
+            acc[ni][mi] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bx, acc[ni][mi], 0, 0, 0, E8M0_ONE, 0,
+                                                                           E8M0_ONE);
+          }
+        }
+        continue;
+      } else {
       // gates k = 32 st + 8 g + j (hi and lo halves) and the MT activation fragments first; their gating
       // runs while the NT weight fragments are read; the slot is released once those returned too
       u32x4 gh, glo, bh[MT], bl[MT], ah[NT], al[NT];
@@ -262,8 +338,39 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
           acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xh, acc[ni][mi], 0, 0, 0);
         }
       }
+      }
     }
 
+    if constexpr (F8) {  // bf16 out = wscale * acc + bias (+ skip), skip rows fetched first
+      uint2 rv[MT][NT];
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni) {
+          const int m = m0 + wm * 64 + mi * 16 + r16, n4 = wn * NT * 16 + ni * 16 + 4 * g;
+          rv[mi][ni] = (a.res && m < a.M && n4 < a.cs_out) ? *reinterpret_cast<const uint2*>(a.res + (size_t)m * a.cs_out + n4)
+                                                           : make_uint2(0u, 0u);
+        }
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) {
+        const int m = m0 + wm * 64 + mi * 16 + r16;
+        if (m >= a.M) continue;
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni) {
+          const int n4 = wn * NT * 16 + ni * 16 + 4 * g;
+          if (n4 >= a.cs_out) continue;
+          const float4 bb = *reinterpret_cast<const float4*>(a.bias + n4);
+          const float4 ws = *reinterpret_cast<const float4*>(a.wscale + n4);
+          float r[4];
+          unpack_bf16x4(rv[mi][ni], r);
+          const float v[4] = {fmaf(acc[ni][mi][0], ws.x, bb.x) + r[0], fmaf(acc[ni][mi][1], ws.y, bb.y) + r[1],
+                              fmaf(acc[ni][mi][2], ws.z, bb.z) + r[2], fmaf(acc[ni][mi][3], ws.w, bb.w) + r[3]};
+          *reinterpret_cast<uint2*>(a.y + (size_t)m * a.cs_out + n4) =
+              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        }
+      }
+      continue;
+    }
     // ---- epilogue: lane = 4 consecutive output channels of one position.  The skip rows of fragment
     // mi + 1 are fetched while fragment mi is finished (all of them at once spilled the NT = 7 variant)
     const bf16_t* __restrict__ R = a.res;
@@ -313,25 +420,26 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
   }
 }
 
-template <int WM, int WN, int NT, int NL, int NS, int IF>
+template <int WM, int WN, int NT, int NL, int NS, int IF, bool F8 = false>
 void launch_cfg(SeWsArgs& a, hipStream_t s, double flops, double bytes) {
   static_assert(IF <= 3, "tail waits");
   constexpr int BM = 64 * WM, BN = 16 * NT * WN;
-  const void* fn = reinterpret_cast<const void*>(&se_ws_kernel<WM, WN, NT, NL, NS, IF>);
+  const void* fn = reinterpret_cast<const void*>(&se_ws_kernel<WM, WN, NT, NL, NS, IF, F8>);
   allow_lds(fn);
   const int nimg = BM / a.P > 0 ? BM / a.P : 1;
-  const int gimg = (2 * a.cs_in * 2 + 1023) / 1024 * 1024;
+  const int gimg = ((F8 ? a.cs_in * 2 : a.cs_in * 4) + 1023) / 1024 * 1024;
   const size_t lds = (size_t)NS * (BN + BM) * ROWB + (size_t)2 * nimg * gimg + 2 * NS * sizeof(unsigned);
   M2S_CHECK(lds <= 160 * 1024, "se_ws: LDS budget");
   M2S_CHECK(BM % a.P == 0 || a.P % BM == 0, "se_ws: tile rows vs image size");
   M2S_CHECK(a.cs_out <= BN, "se_ws: one n tile covers the outputs");
-  M2S_CHECK(a.cs_in / 32 >= NS, "se_ws: K steps per tile >= ring slots (gate rows are double-buffered per tile)");
+  M2S_CHECK((F8 ? a.kp / 128 : a.cs_in / 32) >= NS, "se_ws: K steps per tile >= ring slots (gate rows are double-buffered per tile)");
   a.n_tiles_m = ceil_div(a.M, BM);
   const dim3 grid(std::min(a.n_tiles_m, device_cus()));
   char name[64];
-  snprintf(name, sizeof(name), "se_ws_kernel<%d, %d, %d, %d, %d, %d>", WM, WN, NT, NL, NS, IF);  // rocprof's symbol
+  snprintf(name, sizeof(name), "se_ws_kernel<%d, %d, %d, %d, %d, %d, %s>", WM, WN, NT, NL, NS, IF,
+           F8 ? "true" : "false");  // rocprof's symbol
   ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((se_ws_kernel<WM, WN, NT, NL, NS, IF>), grid, dim3(64 * (WM * WN + NL)), lds, s, a);
+  hipLaunchKernelGGL((se_ws_kernel<WM, WN, NT, NL, NS, IF, F8>), grid, dim3(64 * (WM * WN + NL)), lds, s, a);
   M2S_HIP(hipGetLastError());
 }
 
@@ -378,6 +486,43 @@ void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_p
       case 1: return launch_cfg<2, 2, 7, 2, 3, 1>(a, s, flops, bytes);  // 128 x 224 (two 8x8 images)
       default: return launch_cfg<2, 2, 7, 4, 3, 2>(a, s, flops, bytes);
     }
+  }
+}
+
+bool se_ws_f8_supported(int P, int cs_in, int cs_out) {
+  return cs_in % 16 == 0 && (cs_in + 127) / 128 >= 3 && ((P % 256 == 0 && cs_out <= 128) || (P == 64 && cs_out > 128 && cs_out <= 224));
+}
+
+void launch_se_ws_f8(const void* x8, int M, int P, int cs_in, const void* w8, int kp, int n_pad, const float* wscale,
+                     const float* bias, const void* gate, const void* res, void* y, int cs_out, hipStream_t s, double flops,
+                     double bytes) {
+  M2S_CHECK(se_ws_f8_supported(P, cs_in, cs_out) && kp % 128 == 0 && kp >= cs_in && M % P == 0 && cs_out % 4 == 0,
+            "se_ws_f8: unsupported shape");
+  M2S_CHECK(x8 && w8 && wscale && bias && gate && y && y != res && y != x8, "se_ws_f8: operand pointers");
+  M2S_CHECK((double)M * cs_in < 2147483647.0, "se_ws_f8: input too large");
+  if (M <= 0) return;
+  SeWsArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.x = static_cast<const uint8_t*>(x8);
+  a.w = static_cast<const uint8_t*>(w8);
+  a.wscale = wscale;
+  a.bias = bias;
+  a.gate = static_cast<const uint8_t*>(gate);
+  a.res = static_cast<const bf16_t*>(res);
+  a.y = static_cast<bf16_t*>(y);
+  a.M = M;
+  a.P = P;
+  a.cs_in = cs_in;
+  a.cs_out = cs_out;
+  a.kp = kp;
+  if (cs_out <= 128) {
+    M2S_CHECK(n_pad >= 128, "se_ws_f8: weight rows");
+    // 128 x 128 (half a 16x16 image), 4 consumers + 4 loaders, 4 slots: the 8-consumer 256-row tile of the
+    // split form spills here (32 fp32 gates a lane next to e4m3 fragments)
+    launch_cfg<2, 2, 4, 4, 4, 2, true>(a, s, flops, bytes);
+  } else {
+    M2S_CHECK(n_pad >= 224, "se_ws_f8: weight rows");
+    launch_cfg<2, 2, 7, 4, 3, 2, true>(a, s, flops, bytes);  // 128 x 224 (two 8x8 images)
   }
 }
 

@@ -144,3 +144,25 @@ def test_effnet_fp8_non_square_frames(rt):
     cs = [_cos(f[i], ref[i]) for i in range(3)]
     print("\nfp8 per-frame feature cos (256x512):", " ".join(f"{c:.5f}" for c in cs))
     assert min(cs) >= 0.999
+
+
+@pytest.mark.parametrize("n", [5, 600])
+def test_se_ws_f8_matches_gemm128(rt, monkeypatch, n):
+    """The fp8 engine's SE-gated conv_pwl on the warp-specialised flag ring (se_ws.hip F8: loader / consumer
+    waves, FULL / FREE counters in LDS, ring across tiles) against gemm128.hip's barrier ring (M2S_SE_WS=0):
+    the same e4m3 operands and block-scaled MFMAs in the same K order.  5 frames: a half-empty last 8x8 tile;
+    600: more tiles than workgroups.  Plus the cosine bar against the fp32 oracle at 5 frames."""
+    st = synth.synth_acoustic_state(8)
+    fr = torch.from_numpy(synth.synth_frames(1, n, seed=44)[0]).to(DEV)
+    ws = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    monkeypatch.setenv("M2S_SE_WS", "0")
+    ring = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    for i in (13, 18, 20, 28):  # after blocks 4.0, 4.5, 5.1, 5.9
+        a, b = ws.probe(fr, i).cpu().numpy(), ring.probe(fr, i).cpu().numpy()
+        rel = float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-6))
+        assert np.isfinite(a).all() and rel <= 1e-3, (i, rel)
+    if n == 5:
+        sd = {k: torch.from_numpy(v) for k, v in st.items()}
+        ref = effnet.effnet_gap(sd, fr.cpu()).numpy()
+        f = ws.effnet(fr).cpu().numpy()
+        assert min(_cos(f[i], ref[i]) for i in range(n)) >= 0.999
