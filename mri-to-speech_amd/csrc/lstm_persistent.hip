@@ -32,6 +32,7 @@ namespace m2s {
 namespace {
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
 
 __device__ __forceinline__ float lstm_sig(float x) { return sigmoidf_(x); }
 __device__ __forceinline__ float lstm_tanh(float x) { return 2.f * sigmoidf_(2.f * x) - 1.f; }
@@ -195,6 +196,199 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
   }
 }
 
+// ---- wide batches in split fp32 (B > 16, up to 64 per launch; the bf16x3 / bf16 / fp8 engines) ---------
+// Measured against lstm_persistent_kernel's 24 us per step at B = 64 (gpurun_out lstm1), three changes:
+// * the recurrent products are three bf16 MFMA terms (W_hi h_lo + W_lo h_hi + W_hi h_hi, fp32
+//   accumulation; v_mfma_f32_32x32x16_bf16, K = 16 per instruction) over split operands: W_hh is split
+//   once per launch into resident hi / lo A fragments, and h_t is PUBLISHED split, [seq][hi 640 | lo 640]
+//   bf16, so a consumer loads its B fragments as they are (~0.8 instead of ~4.3 us of f32 MFMA chain).
+//   The split is the headline's arithmetic (relative error ~2^-16 per product); the fp32 engine keeps
+//   the exact-product kernel.
+// * the hand-off is per-workgroup flags with write-through payload instead of a counter barrier with
+//   a release and an acquire fence: each workgroup stores its units of h_t as 16-byte sc1
+//   (write-through) buffer stores, every wave drains them (vmcnt(0)), then after the workgroup barrier
+//   one lane stores the workgroup's flag = step + 1 (relaxed agent store = sc1); a consumer's wave 0
+//   polls its 40 producers' flags with sc1 loads, the workgroup barrier follows, and EVERY load of the
+//   payload is an sc1 buffer load (MI355X_MICROARCH.md § visibility, Valid forms, table row 1; one
+//   workgroup per CU is forced by the launch's LDS size).  No fence either side.
+// * a workgroup owns 16 units x 32 sequences (not 8 units x 64): it loads h_{t-1} of its 32 sequences
+//   only (82 instead of 164 KB a step; at 164 KB the L2 -> CU delivery to the 20 workgroups of an XCD set
+//   the step: 24 -> 12.7 us with the first two changes, 7.8 us at 32 sequences).  8 waves, each a
+//   80-wide K slice of both 32-row tiles; the 8 partials are summed in LDS.
+// Payload buffers alternate by step parity: a workgroup publishes h_{t+1} only after its producers'
+// flags of step t are set, i.e. after every reader of the buffer it overwrites finished loading h_{t-1}.
+constexpr int LX_U = 16;                     // units per workgroup (64 gate rows = two MFMA M tiles)
+constexpr int LX_S = 32;                     // sequences per workgroup (one MFMA N tile)
+constexpr int LX_W = 8;                      // waves
+constexpr int LX_KW = LP_H / LX_W;           // K slice per wave (80)
+constexpr int LX_KS = LX_KW / 16;            // k-steps of 16 per wave (5)
+constexpr int LX_G = LP_H / LX_U;            // unit groups per direction (40)
+constexpr int LX_FLAGS = 1024;               // [err word | pad | flags 2 dir x 2 halves x 40] (zeroed per launch)
+constexpr int LX_PAD_LDS = 16 * 1024;        // dynamic LDS that keeps the workgroups one per CU
+
+__global__ void __launch_bounds__(64 * LX_W, 1) lstm_x3_kernel(const float* __restrict__ pre, const float* __restrict__ whh,
+                                                                float* hs, int Btot, int b0, int B, int T, unsigned* sync,
+                                                                bf16_t* hx, unsigned spin_max, unsigned* err_host) {
+  __shared__ float red[LX_W][2 * 32][LX_S + 1];
+  __shared__ float cst[LX_U][LX_S];
+  __shared__ __attribute__((aligned(16))) float hst[LX_S][LX_U];
+  __shared__ int abort_flag;
+  extern __shared__ char lx_pad[];  // occupancy only (LX_PAD_LDS)
+  const int H = LP_H;
+  // workgroup -> (direction, sequence half, unit group)
+  const int dir = blockIdx.x / (2 * LX_G), sh = (blockIdx.x / LX_G) & 1, ug = blockIdx.x % LX_G;
+  const int s0 = sh * LX_S, nb = min(LX_S, B - s0);  // this workgroup's sequences [s0, s0 + nb)
+  if (nb <= 0) return;  // no live sequence in this half: nobody waits for this workgroup
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hh = lane >> 5, l32 = lane & 31;
+  const int kw = wave * LX_KW;
+  unsigned* err = sync;
+  unsigned* flags = sync + 64 + (dir * 2 + sh) * LX_G;  // the 40 producers of this (direction, half)
+  float* hsd = hs + (size_t)dir * Btot * T * H + (size_t)(b0 + s0) * T * H;
+  pre += (size_t)(b0 + s0) * T * 8 * H;
+  if (tid == 0) lx_pad[0] = 0;
+
+  // ---- W_hh rows of this workgroup, split -> resident hi / lo A fragments -------------------------
+  // tile m, lane (row 32 m + l32 = gate g x 16 + unit, k half hh): k = kw + 16 s + 8 hh + j
+  bf16x8 whi[2][LX_KS], wlo[2][LX_KS];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int r = 32 * m + l32, g = r / LX_U, u = ug * LX_U + (r % LX_U);
+    const float* wr = whh + ((size_t)dir * 4 * H + (size_t)g * H + u) * H + kw + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < LX_KS; ++s) {
+      const float4 a = *reinterpret_cast<const float4*>(wr + 16 * s);
+      const float4 b = *reinterpret_cast<const float4*>(wr + 16 * s + 4);
+      const float v0[4] = {a.x, a.y, a.z, a.w}, v1[4] = {b.x, b.y, b.z, b.w};
+      uint2 h0, l0, h1, l1;
+      split4(v0, h0, l0);
+      split4(v1, h1, l1);
+      whi[m][s] = __builtin_bit_cast(bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+      wlo[m][s] = __builtin_bit_cast(bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+    }
+  }
+  for (int i = tid; i < LX_U * LX_S; i += 64 * LX_W) (&cst[0][0])[i] = 0.f;
+  if (tid == 0) abort_flag = 0;
+  __syncthreads();
+
+  constexpr int HXS = 2 * LP_H;               // bf16 per published sequence row [hi | lo]
+  const size_t hx_par = (size_t)LP_BMAX * HXS;  // one parity buffer of one direction
+  bf16_t* hxd = hx + (size_t)dir * 2 * hx_par;
+  const int cu = tid % LX_U, cb = tid / LX_U;  // cell-update pair (unit, sequence) of this thread
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? step : T - 1 - step;
+    // the cell update's gate pre-activations, fetched before the wait (their latency hides under it)
+    float prf[4];
+    {
+      const float* pr = pre + ((size_t)cb * T + t) * 8 * H + (size_t)dir * 4 * H + ug * LX_U + cu;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) prf[q] = cb < nb ? pr[q * H] : 0.f;
+    }
+    f32x16 acc[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][i] = 0.f;
+    if (step > 0) {
+      // ---- wave 0 polls its 40 producers' flags (sc1 loads) until every one reached `step` ----------
+      if (wave == 0) {
+        unsigned spins = 0;
+        for (;;) {
+          const bool ok = lane >= LX_G ||
+                          __hip_atomic_load(flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)step;
+          if (__all(ok) && spin_max != 0) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > spin_max || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+            if (lane == 0) {
+              __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              abort_flag = 1;
+            }
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      if (abort_flag) {  // a peer stopped publishing: flag the host, poison the remaining outputs, leave
+        if (tid == 0 && err_host) __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int st = step; st < T; ++st) {
+          const int tt = dir == 0 ? st : T - 1 - st;
+          for (int p = tid; p < LX_U * nb; p += 64 * LX_W)
+            hsd[((size_t)(p / LX_U) * T + tt) * H + ug * LX_U + p % LX_U] = __builtin_nanf("");
+        }
+        return;
+      }
+      // ---- B fragments of h_{t-1}: sequence s0 + l32, k = kw + 16 s + 8 hh (hi and lo), sc1 loads -------
+      // (the descriptor's range ends at the last live sequence: lanes past it read zeros)
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          hxd + (size_t)((step - 1) & 1) * hx_par, 0, B * HXS * (int)sizeof(bf16_t), 0x00020000);
+      uint4 bh[LX_KS], bl[LX_KS];
+      const int o = ((s0 + l32) * HXS + kw + 8 * hh) * (int)sizeof(bf16_t);
+#pragma unroll
+      for (int s = 0; s < LX_KS; ++s) {
+        bh[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 32 * s, 0, 16));
+        bl[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 32 * s + 2 * LP_H, 0, 16));
+      }
+      // three terms per k-step, small ones first; the two row tiles' chains interleave
+#pragma unroll
+      for (int s = 0; s < LX_KS; ++s)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wlo[m][s], __builtin_bit_cast(bf16x8, bh[s]), acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(whi[m][s], __builtin_bit_cast(bf16x8, bl[s]), acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(whi[m][s], __builtin_bit_cast(bf16x8, bh[s]), acc[m], 0, 0, 0);
+        }
+    }
+    // ---- K-slice partials -> LDS: acc[m][i] holds row 32 m + 8(i/4) + 4 hh + i%4, sequence l32 ----------
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) red[wave][32 * m + 8 * (i / 4) + 4 * hh + (i % 4)][l32] = acc[m][i];
+    __syncthreads();
+    // ---- cell update: thread -> (unit cu, sequence cb), partials summed in a fixed order ----------------
+    if (cb < nb) {
+      float gs[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int r = g * LX_U + cu;
+        gs[g] = ((red[0][r][cb] + red[1][r][cb]) + (red[2][r][cb] + red[3][r][cb])) +
+                ((red[4][r][cb] + red[5][r][cb]) + (red[6][r][cb] + red[7][r][cb]));
+      }
+      const float gi = lstm_sig(prf[0] + gs[0]);
+      const float gf = lstm_sig(prf[1] + gs[1]);
+      const float gg = lstm_tanh(prf[2] + gs[2]);
+      const float go = lstm_sig(prf[3] + gs[3]);
+      const float c = step > 0 ? gf * cst[cu][cb] + gi * gg : gi * gg;
+      cst[cu][cb] = c;
+      const float h = go * lstm_tanh(c);
+      hsd[((size_t)cb * T + t) * H + ug * LX_U + cu] = h;
+      hst[cb][cu] = h;
+    }
+    __syncthreads();  // hst complete; red free for the next step
+    // ---- publish h_t split: thread (sequence, plane, 8-unit half) stores 16 B, write-through ----------
+    if (step + 1 < T) {
+      if (tid < 4 * nb) {
+        const int b = tid >> 2, plane = (tid >> 1) & 1, half = tid & 1;
+        const float4 v0 = *reinterpret_cast<const float4*>(&hst[b][8 * half]);
+        const float4 v1 = *reinterpret_cast<const float4*>(&hst[b][8 * half + 4]);
+        const float a0[4] = {v0.x, v0.y, v0.z, v0.w}, a1[4] = {v1.x, v1.y, v1.z, v1.w};
+        uint2 h0, l0, h1, l1;
+        split4(a0, h0, l0);
+        split4(a1, h1, l1);
+        const uint4 w = plane ? make_uint4(l0.x, l0.y, l1.x, l1.y) : make_uint4(h0.x, h0.y, h1.x, h1.y);
+        const __amdgpu_buffer_rsrc_t rd =
+            __builtin_amdgcn_make_buffer_rsrc(hxd + (size_t)(step & 1) * hx_par, 0, (int)(hx_par * sizeof(bf16_t)), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, w), rd,
+                                               ((s0 + b) * HXS + plane * LP_H + ug * LX_U + 8 * half) * (int)sizeof(bf16_t),
+                                               0, 16);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_store(sync + 64 + (dir * 2 + sh) * LX_G + ug, (unsigned)(step + 1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 
 // ---- small batches (B <= LS_BMAX: the 1 x 1000-frame configs[4] clip, the 1 x 30 configs[0] clip) -----
 // At B = 1 the 32-wide MFMA B tile is 1/32 used and the counter barrier (store drain, agent release,
@@ -584,6 +778,25 @@ void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B
     M2S_HIP(hipMemsetAsync(sync, 0, lstm_persistent_sync_bytes(), s));
     hipLaunchKernelGGL(lstm_persistent_kernel, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, b0, nb, T, sp, spin_max,
                        err_host);
+    M2S_HIP(hipGetLastError());
+  }
+}
+
+size_t lstm_x3_sync_bytes() { return LX_FLAGS + (size_t)2 * 2 * LP_BMAX * 2 * LP_H * sizeof(bf16_t); }
+
+void launch_lstm_x3(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,
+                    unsigned* err_host, hipStream_t s) {
+  M2S_CHECK(lstm_persistent_supported(H) && B > 0 && T > 0, "lstm_x3: unsupported shape");
+  const int grid = 2 * 2 * LX_G;  // (direction, sequence half, unit group)
+  const int resident = device_resident(reinterpret_cast<const void*>(&lstm_x3_kernel), 64 * LX_W, LX_PAD_LDS);
+  M2S_CHECK(grid <= resident, "lstm_x3: grid not co-resident on this device");
+  unsigned* sp = static_cast<unsigned*>(sync);
+  bf16_t* hx = reinterpret_cast<bf16_t*>(static_cast<char*>(sync) + LX_FLAGS);
+  for (int b0 = 0; b0 < B; b0 += LP_BMAX) {  // c lives in LDS: at most LP_BMAX sequences per launch
+    const int nb = std::min(LP_BMAX, B - b0);
+    M2S_HIP(hipMemsetAsync(sync, 0, LX_FLAGS, s));  // error word + flags: epochs restart at 0 each launch
+    hipLaunchKernelGGL(lstm_x3_kernel, dim3(grid), dim3(64 * LX_W), LX_PAD_LDS, s, pre, whh, hs, B, b0, nb, T, sp, hx,
+                       spin_max, err_host);
     M2S_HIP(hipGetLastError());
   }
 }

@@ -91,6 +91,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_IR_S2BAND")) ir_s2band_ = std::strcmp(e, "0") != 0;  // A/B and tests only
   if (const char* e = std::getenv("M2S_LSTM_PERSISTENT")) lstm_persistent_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_LSTM_MID")) lstm_mid_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_LSTM_X3")) lstm_x3_ = std::strcmp(e, "0") != 0;
   const std::string P = "cnn.backbone.";
   {  // stem: fold repeat(1,3,1,1) by summing the 3 input channels; then BN
     const float* w = need(sd, P + "conv_stem.weight", {EFF_STEM, 3, 3, 3}).data;
@@ -450,7 +451,7 @@ size_t Acoustic::workspace_bytes(int B, int T, int H, int W) const {
   ws.take<float>(BT * 8 * hidden_);
   ws.take<float>(2 * BT * hidden_);
   ws.take<float>((size_t)2 * B * hidden_);
-  ws.take<char>(std::max({lstm_persistent_sync_bytes(), lstm_small_sync_bytes(), lstm_mid_sync_bytes()}));
+  ws.take<char>(std::max({lstm_persistent_sync_bytes(), lstm_small_sync_bytes(), lstm_mid_sync_bytes(), lstm_x3_sync_bytes()}));
   return ws.used();
 }
 
@@ -723,13 +724,16 @@ void Acoustic::bilstm(const float* feats, int B, int T, float* y, float* mel_nor
   a.y = pre;
   a.M = (int)BT;
   run_conv<float>(a, lstm_ih_, s);
-  void* sync = ws.take<char>(std::max({lstm_persistent_sync_bytes(), lstm_small_sync_bytes(), lstm_mid_sync_bytes()}));
+  void* sync = ws.take<char>(std::max({lstm_persistent_sync_bytes(), lstm_small_sync_bytes(), lstm_mid_sync_bytes(), lstm_x3_sync_bytes()}));
   if (lstm_persistent_ && lstm_small_supported(B, H)) {
     ProfScope ps("lstm_small_kernel", 2.0 * 2 * B * 4.0 * H * H * (T - 1), 4.0 * 2 * 4 * H * H + 4.0 * BT * (8.0 * H + 2.0 * H), s);
     launch_lstm_small(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, lstm_spin_max_, err_dev_, s);
   } else if (lstm_persistent_ && lstm_mid_ && lstm_mid_supported(B, H)) {
     ProfScope ps("lstm_mid_kernel", 2.0 * 2 * B * 4.0 * H * H * (T - 1), 4.0 * 2 * 4 * H * H + 4.0 * BT * (8.0 * H + 2.0 * H), s);
     launch_lstm_mid(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, lstm_spin_max_, err_dev_, s);
+  } else if (lstm_persistent_ && lstm_x3_ && dtype_ != M2S_DT_F32 && lstm_persistent_supported(H)) {
+    ProfScope ps("lstm_x3_kernel", 3.0 * 2 * B * 4.0 * H * H * (T - 1), 4.0 * 2 * 4 * H * H + 4.0 * BT * (8.0 * H + 2.0 * H), s);
+    launch_lstm_x3(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, lstm_spin_max_, err_dev_, s);
   } else if (lstm_persistent_ && lstm_persistent_supported(H)) {
     // algorithmic bytes: W_hh of both directions once, gate pre-activations in, h out
     ProfScope ps("lstm_persistent_kernel", 2.0 * 2 * B * 4.0 * H * H * (T - 1),

@@ -15,8 +15,10 @@ from m2s import runtime as rt, synth  # noqa: E402
 
 DEV = torch.device("cuda", 0)
 g = np.load(os.path.join(os.path.dirname(__file__), "..", "tests", "golden", "acoustic.npz"), allow_pickle=False)
-eng = rt.AcousticEngine(synth.synth_acoustic_state(int(g["seed"])), dtype="fp32", device=DEV)
-# M2S_LSTM_MID=0 in the environment times the counter-barrier kernel at 4 < B <= 64 instead
+# M2S_LSTM_MID=0 in the environment times the counter-barrier kernel at 4 < B <= 64 instead; argv[1] = engine
+# dtype (fp32 default; bf16x3 / bf16 / fp8 run lstm_x3_kernel above 16 sequences unless M2S_LSTM_X3=0)
+eng = rt.AcousticEngine(synth.synth_acoustic_state(int(g["seed"])), dtype=sys.argv[1] if len(sys.argv) > 1 else "fp32",
+                        device=DEV)
 shapes = ((1, 1000), (1, 30), (8, 1000), (16, 200), (32, 100), (64, 30), (64, 200))
 for B, T in shapes:
     x = torch.randn(B, T, 208, device=DEV)
