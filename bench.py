@@ -53,24 +53,28 @@ FP32_TOL = {"mel_norm": 1e-4, "mel_log": 5e-4, "wav": 2e-4}  # tests/test_gpu_co
 LONG_TOL = {"mel_norm": 2e-4, "mel_log": 1e-3, "wav": 2e-4}
 PRECISION = {
     "bf16x3": "split fp32: bf16 hi+lo pairs (17-bit), 3 bf16 MFMA terms per product, fp32 accumulate; "
-              "BiLSTM/head/glue fp32 (exact products)",
+              "BiLSTM recurrence 3-term split products (lstm_x3, B > 4), input projection/head/glue fp32",
     "fp32": "exact f32 MFMA products (v_mfma_f32_16x16x4_f32), fp32 storage",
-    "bf16": "bf16 storage and operands, fp32 accumulate; BiLSTM/head/glue fp32",
+    "bf16": "bf16 storage and operands, fp32 accumulate; BiLSTM recurrence 3-term split products (B > 4), "
+            "input projection/head/glue fp32",
     "fp8": "e4m3 storage + block-scaled e4m3 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, per-output-channel "
            "weight scales) for the IR blocks' expanded maps and SE-gated conv_pwl GEMMs and the C=128/256 "
            "MRF convs; the other convs (stem, EdgeResidual, IR expand/depthwise, C=32/64 MRF, upsamplers) "
-           "bf16; BiLSTM/head/glue fp32",
+           "bf16; BiLSTM recurrence 3-term split products (B > 4), input projection/head/glue fp32",
 }
 
 MFMA_KERNELS = ("conv_gemm_kernel", "gemm128_kernel", "conv_halo_kernel", "conv1d_halo", "conv_igemm_kernel", "ir_pwdw",
-                "ir_ws_kernel", "se_ws_kernel", "lstm_persistent_kernel", "rb1_fused_kernel", "stem_b0_kernel", "se_excite_kernel",
+                "ir_ws_kernel", "se_ws_kernel", "lstm_persistent_kernel", "lstm_x3_kernel", "rb1_fused_kernel", "stem_b0_kernel", "se_excite_kernel",
                 "er_fused_kernel", "er2_fused_kernel", "ers2_fused_kernel", "er_sp_kernel", "ers2_sp_kernel")
 
 
 def kernel_arith(name: str, dtype: str) -> str:
-    """Arithmetic of a kernel in a run of `dtype`: the BiLSTM and its input projection are f32."""
+    """Arithmetic of a kernel in a run of `dtype`: the BiLSTM input projection is f32, its recurrence
+    split fp32 (three bf16 terms) in every non-fp32 engine."""
     if name.startswith("lstm_persistent") or name.startswith("lstm_step") or "<float" in name:
         return "fp32"
+    if name.startswith("lstm_x3"):  # the split recurrence of every non-fp32 engine
+        return "bf16x3"
     if dtype == "fp8":  # only the e4m3 kernels run fp8 MFMA; the rest of an fp8 engine is bf16
         e4m3 = name.startswith(("gemm128_kernel<0", "gemm128_kernel<1")) or (name.startswith("se_ws_kernel") and "true" in name)
         return "fp8" if e4m3 else "bf16"

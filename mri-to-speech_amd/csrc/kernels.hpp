@@ -196,7 +196,7 @@ void launch_lstm_mid(const float* pre, const float* whh, float* hs, int B, int T
                      unsigned* err_host, hipStream_t s);
 void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync,
                             unsigned spin_max, unsigned* err_host, hipStream_t s);
-// B > 16 in split fp32 (the bf16x3 / bf16 / fp8 engines): three bf16 MFMA terms over W_hh and h_t split
+// B > 4 in split fp32 (the bf16x3 / bf16 / fp8 engines): three bf16 MFMA terms over W_hh and h_t split
 // hi / lo, h_t published split by write-through stores behind per-workgroup flags (no fences).
 // `sync` = lstm_x3_sync_bytes() (flags reset by the launcher).
 size_t lstm_x3_sync_bytes();

@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(256, 1) lstm_persistent_kernel(const float* __
   }
 }
 
-// ---- wide batches in split fp32 (B > 16, up to 64 per launch; the bf16x3 / bf16 / fp8 engines) ---------
+// ---- split fp32 batches (B > 4, up to 64 per launch; the bf16x3 / bf16 / fp8 engines) -----------------
 // Measured against lstm_persistent_kernel's 24 us per step at B = 64 (gpurun_out lstm1), three changes:
 // * the recurrent products are three bf16 MFMA terms (W_hi h_lo + W_lo h_hi + W_hi h_hi, fp32
 //   accumulation; v_mfma_f32_32x32x16_bf16, K = 16 per instruction) over split operands: W_hh is split

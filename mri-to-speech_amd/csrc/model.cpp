@@ -728,12 +728,14 @@ void Acoustic::bilstm(const float* feats, int B, int T, float* y, float* mel_nor
   if (lstm_persistent_ && lstm_small_supported(B, H)) {
     ProfScope ps("lstm_small_kernel", 2.0 * 2 * B * 4.0 * H * H * (T - 1), 4.0 * 2 * 4 * H * H + 4.0 * BT * (8.0 * H + 2.0 * H), s);
     launch_lstm_small(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, lstm_spin_max_, err_dev_, s);
+  } else if (lstm_persistent_ && lstm_x3_ && dtype_ != M2S_DT_F32 && lstm_persistent_supported(H)) {
+    // split engines above the small-batch kernel: 4.1 / 5.2 / 9.9 us per step at B = 8 / 16 / 64 against
+    // lstm_mid's 7.2 / 11.9 and the f32 counter-barrier kernel's 24 (gpurun_out lstm2, lstm3_x3small)
+    ProfScope ps("lstm_x3_kernel", 3.0 * 2 * B * 4.0 * H * H * (T - 1), 4.0 * 2 * 4 * H * H + 4.0 * BT * (8.0 * H + 2.0 * H), s);
+    launch_lstm_x3(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, lstm_spin_max_, err_dev_, s);
   } else if (lstm_persistent_ && lstm_mid_ && lstm_mid_supported(B, H)) {
     ProfScope ps("lstm_mid_kernel", 2.0 * 2 * B * 4.0 * H * H * (T - 1), 4.0 * 2 * 4 * H * H + 4.0 * BT * (8.0 * H + 2.0 * H), s);
     launch_lstm_mid(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, lstm_spin_max_, err_dev_, s);
-  } else if (lstm_persistent_ && lstm_x3_ && dtype_ != M2S_DT_F32 && lstm_persistent_supported(H)) {
-    ProfScope ps("lstm_x3_kernel", 3.0 * 2 * B * 4.0 * H * H * (T - 1), 4.0 * 2 * 4 * H * H + 4.0 * BT * (8.0 * H + 2.0 * H), s);
-    launch_lstm_x3(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, lstm_spin_max_, err_dev_, s);
   } else if (lstm_persistent_ && lstm_persistent_supported(H)) {
     // algorithmic bytes: W_hh of both directions once, gate pre-activations in, h out
     ProfScope ps("lstm_persistent_kernel", 2.0 * 2 * B * 4.0 * H * H * (T - 1),

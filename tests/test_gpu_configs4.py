@@ -2,7 +2,7 @@
 
 configs[4] (BASELINE.json): "fp8 MFMA CNN encoder + HiFi-GAN MRF dilated-conv path, >=1000-frame clips".
 bench.py's ``configs4`` lines time 8 x 1000 frames (8 000 CNN frames over several CNN chunks, the
-8-sequence ``lstm_mid`` BiLSTM, the batched e4m3 MRF stages); these tests hold that exact batch to the
+8-sequence split ``lstm_x3`` BiLSTM, the batched e4m3 MRF stages); these tests hold that exact batch to the
 fp32 oracle (oracle/pipeline.py e2e, the no_grad section of scripts/run_mri_video_inference.py:218-242)
 on clips 0 and 7 (the first and last rows of every batched launch):
 

@@ -321,13 +321,14 @@ def test_bilstm_persistent_long_and_wide(rt, ac_state, monkeypatch, B, T):
     np.testing.assert_allclose(m.cpu().numpy(), acoustic.head(sd, torch.from_numpy(ref_y)).numpy(), atol=5 * tol, rtol=0)
 
 
-@pytest.mark.parametrize("B,T", [(17, 1), (20, 33), (64, 30), (64, 200), (70, 6), (40, 1000)])
+@pytest.mark.parametrize("B,T", [(5, 17), (8, 1000), (12, 33), (16, 200), (17, 1), (20, 33), (64, 30), (64, 200),
+                                 (70, 6), (40, 1000)])
 def test_bilstm_split_x3(rt, ac_state, monkeypatch, B, T):
-    """B > 16 in the split-fp32 engines (lstm_x3_kernel): three bf16 MFMA terms over W_hh and h split
+    """B > 4 in the split-fp32 engines (lstm_x3_kernel): three bf16 MFMA terms over W_hh and h split
     hi / lo, h_t handed over by write-through stores behind per-workgroup flags.  Against the oracle and
     the exact-product f32 kernel (M2S_LSTM_X3=0) in the same engine; the split costs ~2^-16 per product,
     so the bar is the split engines' 1e-4 (a 64-sequence full launch, a ragged 6-sequence second launch at
-    70, one-tile launches at 17 / 20, 1000 recurrent steps at 40)."""
+    70, one sequence half at 5-20, configs[4]'s 8 x 1000, 1000 recurrent steps at 40)."""
     sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
     x = torch.from_numpy(np.random.default_rng(B * 11 + T).normal(0, 0.5, (B, T, 208)).astype(np.float32))
     monkeypatch.setenv("M2S_LSTM_X3", "1")
@@ -364,12 +365,12 @@ def test_preprocess_vs_oracle_shapes_and_bgr(rt, shape):
 
 
 # ------------------------------------------------------------------------------ asynchronous failure report
-@pytest.mark.parametrize("B,dtype", [(1, "fp32"), (8, "fp32"), (12, "fp32"), (70, "fp32"), (70, "bf16x3")])
+@pytest.mark.parametrize("B,dtype", [(1, "fp32"), (8, "fp32"), (12, "fp32"), (70, "fp32"), (8, "bf16x3"), (70, "bf16x3")])
 def test_bilstm_barrier_timeout_is_reported(rt, ac_state, B, dtype):
     """A BiLSTM hand-off wait that times out (forced: spin limit 0 = the first wait fails) poisons the outputs and is
     reported: m2s_acoustic_status -> M2SError, and the next forward on the engine fails too.  B = 1:
     lstm_small_kernel, 8 / 12: lstm_mid_kernel with 4- / 8-sequence chunks (granule sweeps), 70: the counter
-    barrier (fp32) and the flag hand-off of lstm_x3_kernel (bf16x3)."""
+    barrier (fp32); 8 / 70 bf16x3: the flag hand-off of lstm_x3_kernel."""
     import ctypes
     from m2s import _native
     eng = rt.AcousticEngine(ac_state[1], dtype=dtype, device=DEV)
