@@ -55,7 +55,7 @@ struct StemB0Args {
   const float* b1;
   bf16_t* y;            // (N, OH, OW, 16) (SP: (N, OH, OW, [hi 16 | lo 16]))
   int N, H, W, OH, OW, pad_t, pad_l, kp0, kp1, tiles_x, tiles_y;
-  int per_xcd;  // tiles per XCD range (gridDim.x is a multiple of 8)
+  int per_xcd;  // strips (image, tile column) per XCD range (gridDim.x is a multiple of 8)
   unsigned long long* trace;  // diagnostic build (-DIRWS_TRACE): per-phase s_memtime stamps, else null
 };
 
@@ -68,14 +68,21 @@ __device__ __forceinline__ f32x4 mma3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl
 
 template <int TH, int SP>
 __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Args a) {
+  static_assert(TH == 16, "line buffer: 16 new S / A rows per tile");
+  // Plane index of S pixel / A position (row, col) = OFS + row * SB_SW + col: the pad makes A row 2 start
+  // on a 16-position subtile, so a strip's later tiles recompute exactly A rows 2..17 (20 subtiles).
+  constexpr int OFS = 8;
   constexpr int SH = TH + 4, AH = TH + 2;
-  constexpr int SPIX = SH * SB_SW, APIX = AH * SB_AW;
-  constexpr int APIX_PAD = (APIX + 15) / 16 * 16;
+  constexpr int SPIX = OFS + SH * SB_SW, APIX = OFS + AH * SB_AW;
+  static_assert(APIX % 16 == 0 && (OFS + 2 * SB_AW) % 16 == 0, "A subtiles");
   constexpr int SPLANE = (SPIX * 16 + 255) / 256 * 256;      // bytes per S plane (4 planes)
-  constexpr int APLANE = (APIX_PAD * 16 + 255) / 256 * 256;  // bytes per A plane (2 planes)
-  constexpr int ASUB = APIX_PAD / 16;                         // A position subtiles
-  constexpr int AMS = (ASUB + 3) / 4;                         // ... per wave, at most
+  constexpr int APLANE = (APIX * 16 + 255) / 256 * 256;      // bytes per A plane (2 planes)
+  constexpr int ASUB = APIX / 16;                             // A position subtiles of a strip's first tile
+  constexpr int ASUB0 = (OFS + 2 * SB_AW) / 16;               // first subtile of A row 2 (later tiles)
+  constexpr int AMS = (ASUB + 3) / 4;                         // subtiles per wave, at most
   constexpr int OMS = TH / 4;                                 // output subtiles (rows) per wave
+  constexpr int SHIFT = TH * SB_SW;                           // carried rows move up by TH rows
+  static_assert(SB_SW == SB_AW, "S and A share the pitch");
   constexpr int R = SP ? 2 : 1;  // plane sets: hi (+ lo)
   __shared__ __attribute__((aligned(16))) char sS[R * 4 * SPLANE + 256];  // + the overrun of columns 18-19
   __shared__ __attribute__((aligned(16))) char sA[R * 2 * APLANE];
@@ -84,43 +91,52 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
-  const int tpi = a.tiles_x * a.tiles_y, total = a.N * tpi;
-  // tiles of XCD x (= blockIdx % 8, where the hardware deals consecutive blocks round-robin):
-  // [x * per_xcd, (x + 1) * per_xcd); its gx workgroups take consecutive tiles of that range
+  // Strips = (image, 16-column tile column): a workgroup walks a strip's tiles top to bottom and keeps
+  // the rows the next tile shares (S rows 16..19 -> 0..3, A rows 16..17 -> 0..1: halo recompute 1.56x ->
+  // 1.25x of the stem, 1.44x -> 1.25x of blocks.0.0).  Strips of XCD x (= blockIdx % 8) are
+  // [x * per_xcd, (x + 1) * per_xcd) (neighbouring columns of the same frames share one L2).
+  const int nstrip = a.N * a.tiles_x;
   const int gx = gridDim.x / 8, xcd = blockIdx.x % 8;
-  const int t_end = min(total, (xcd + 1) * a.per_xcd);
-  auto tile_of = [&](int t, int& n, int& ty0, int& tx0) {
-    n = t / tpi;
-    const int tr = t - n * tpi;
-    ty0 = (tr / a.tiles_x) * TH;
-    tx0 = (tr - (tr / a.tiles_x) * a.tiles_x) * SB_TW;
-  };
+  const int s_end = min(nstrip, (xcd + 1) * a.per_xcd);
 
-  // ---- phase-1 inputs: threads [0, SPIX/2) take S pixels i and i + SPIX/2 ---------------------
-  static_assert(SPIX % 2 == 0 && SPIX / 2 <= 256, "stem tile");
-  const bool p1 = tid < SPIX / 2;
-  float in[2][9];
-  auto load_in = [&](int t) {
-    int n, ty0, tx0;
-    tile_of(t, n, ty0, tx0);
-    const float* fr = a.frames + (size_t)n * a.H * a.W;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int i = tid + h * (SPIX / 2);
-      const int sy = i / SB_SW, sx = i - (i / SB_SW) * SB_SW;
-      const int oy = ty0 - 2 + sy, ox = tx0 - 2 + sx;  // stem output pixel
-      const bool ok = oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW;
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int iy = oy * 2 - a.pad_t + ky, ix = ox * 2 - a.pad_l + kx;
-          in[h][ky * 3 + kx] = (ok && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) ? fr[(size_t)iy * a.W + ix] : 0.f;
-        }
-    }
+  // ---- phase-1 work of a tile: this thread's full pixel (32 channels) and its quarter pixels (the 8
+  // channels of group qg), both as S plane indices.  First tile of a strip: 400 pixels = 256 full + 144
+  // by quarters; later tiles: the 320 pixels of rows 4..19 = 256 full + 64 by quarters (40 channels a
+  // thread, balanced).  A wave's quarter lanes are 4 groups x 16 consecutive pixels: conflict-free stores.
+  // (t = the thread index, re-materialised per tile by the caller: addresses derived from it and hoisted
+  // out of the tile loop for both the first-tile and the later-tile variants spilled to scratch)
+  auto slot_px = [&](bool first, int k, int t) -> int {  // k = 0: full pixel; 1..3: quarter pixels (-1: none)
+    const int qoff = 16 * (t >> 6) + (t & 15);
+    if (k == 0) return first ? OFS + t : OFS + 4 * SB_SW + t;
+    const int m = k - 1;
+    if (first) return (m < 2 || qoff < 16) ? OFS + 256 + 64 * m + qoff : -1;
+    return m == 0 ? OFS + 4 * SB_SW + 256 + qoff : -1;
   };
-  int t = xcd * a.per_xcd + (int)blockIdx.x / 8;
-  if (p1 && t < t_end) load_in(t);
+  // frame values of slot k's 9 stem taps (zeros outside the frame / the map)
+  auto load9 = [&](float* x9, int st, int ty, int k, int t) {
+    const int n = st / a.tiles_x, tx0 = (st - n * a.tiles_x) * SB_TW, ty0 = ty * TH;
+    const float* fr = a.frames + (size_t)n * a.H * a.W;
+    const int px = slot_px(ty == 0, k, t);
+    const int i = px - OFS, sy = i / SB_SW, sx = i - (i / SB_SW) * SB_SW;
+    const int oy = ty0 - 2 + sy, ox = tx0 - 2 + sx;  // stem output pixel
+    const bool ok = px >= 0 && oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int iy = oy * 2 - a.pad_t + ky, ix = ox * 2 - a.pad_l + kx;
+        x9[ky * 3 + kx] = (ok && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) ? fr[(size_t)iy * a.W + ix] : 0.f;
+      }
+  };
+  // slots 0 and 1 of the next tile are prefetched into registers (they land while phases 2 and 3 run);
+  // a strip's first tile loads its two further quarter slots when it needs them
+  float in[2][9];
+  auto load_in = [&](int st, int ty, int t) {
+    load9(in[0], st, ty, 0, t);
+    load9(in[1], st, ty, 1, t);
+  };
+  int st = xcd * a.per_xcd + (int)blockIdx.x / 8, ty = 0;
+  if (st < s_end) load_in(st, 0, tid);
 
   // resident weights of both convs (A fragments)
   bf16x8 wf0[9], wf1[5], wl0[SP ? 9 : 1], wl1[SP ? 5 : 1];
@@ -136,18 +152,45 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
     wf1[k] = *reinterpret_cast<const bf16x8*>(w);
     if constexpr (SP) wl1[k] = *reinterpret_cast<const bf16x8*>(w + a.kp1);
   }
-  // the stem's weights and biases in LDS (uniform-address reads broadcast): read from global inside
-  // the tile loop they were vector loads (the loop's stores of y rule out scalar loads), each tile
-  // waiting on ~100 of them
-  // split: tap-major ([k][32 channels]), so the two channels of a packed FMA are adjacent (one ds_read_b64
-  // instead of two reads and the moves that pair them: 569 -> 394 v_mov in this variant); bf16 keeps
-  // [32][9] (tap-major there costs it VGPR spills at its 168-register bound)
+  // the stem's weights and biases in LDS, tap-major ([k][32 channels] + 32 biases): read from global
+  // inside the tile loop they were vector loads (the loop's stores of y rule out scalar loads)
   __shared__ __attribute__((aligned(16))) float sw9[288 + 32];
-  for (int i = tid; i < 320; i += 256)
-    sw9[i] = i < 288 ? (SP ? a.w9[(i % 32) * 9 + i / 32] : a.w9[i]) : a.b9[i - 288];
+  for (int i = tid; i < 320; i += 256) sw9[i] = i < 288 ? a.w9[(i % 32) * 9 + i / 32] : a.b9[i - 288];
   const float4 bb0 = *reinterpret_cast<const float4*>(a.b0 + 4 * g);
   const float4 bb1 = *reinterpret_cast<const float4*>(a.b1 + 4 * g);
   __syncthreads();
+
+  // 8 stem channels (group grp) of one S pixel from its 9 frame values -> S planes (hi, lo): eight
+  // independent FMA chains, the tap's 8 weights by two 16-byte LDS reads (tap-major [k][32 channels])
+  auto stem8 = [&](const float* x9, int grp, bool ok, int px) {
+    float acc[8];
+    {
+      const float4 b0 = *reinterpret_cast<const float4*>(&sw9[288 + grp * 8]);
+      const float4 b1 = *reinterpret_cast<const float4*>(&sw9[288 + grp * 8 + 4]);
+      acc[0] = b0.x; acc[1] = b0.y; acc[2] = b0.z; acc[3] = b0.w;
+      acc[4] = b1.x; acc[5] = b1.y; acc[6] = b1.z; acc[7] = b1.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const float4 w0 = *reinterpret_cast<const float4*>(&sw9[k * 32 + grp * 8]);
+      const float4 w1 = *reinterpret_cast<const float4*>(&sw9[k * 32 + grp * 8 + 4]);
+      acc[0] += w0.x * x9[k]; acc[1] += w0.y * x9[k]; acc[2] += w0.z * x9[k]; acc[3] += w0.w * x9[k];
+      acc[4] += w1.x * x9[k]; acc[5] += w1.y * x9[k]; acc[6] += w1.z * x9[k]; acc[7] += w1.w * x9[k];
+    }
+    uint32_t v[4], vl[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const float s0 = silu(acc[j]), s1 = silu(acc[j + 1]);
+      v[j / 2] = ok ? pack_bf16x2(s0, s1) : 0u;
+      if constexpr (SP)  // lo halves: v - hi
+        vl[j / 2] = ok ? pack_bf16x2(s0 - __uint_as_float(v[j / 2] << 16), s1 - __uint_as_float(v[j / 2] & 0xffff0000u)) : 0u;
+    }
+    *reinterpret_cast<uint4*>(sS + grp * SPLANE + px * 16) = make_uint4(v[0], v[1], v[2], v[3]);
+    if constexpr (SP) *reinterpret_cast<uint4*>(sS + SLO + grp * SPLANE + px * 16) = make_uint4(vl[0], vl[1], vl[2], vl[3]);
+  };
+  auto copy16 = [&](char* base, int from, int to) {  // one 16-byte LDS chunk, hi (and lo) planes
+    *reinterpret_cast<uint4*>(base + to) = *reinterpret_cast<const uint4*>(base + from);
+  };
 
   int it = 0;  // tile iteration (diagnostic stamps)
   auto TR = [&](int k) {
@@ -157,66 +200,48 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
     (void)k;
 #endif
   };
-  for (; t < t_end; t += gx, ++it) {
-    int n, ty0, tx0;
-    tile_of(t, n, ty0, tx0);
+  while (st < s_end) {
+    const int n = st / a.tiles_x, tx0 = (st - n * a.tiles_x) * SB_TW, ty0 = ty * TH;
+    const bool first = ty == 0;
+    int tl = tid;
+    asm volatile("" : "+v"(tl));
+    const int g = (tl & 63) >> 4, r16 = tl & 15, qg = (tl & 63) >> 4;
     TR(0);
     // ---- phase 1: stem (fp32 VALU) -> S -----------------------------------------------------
-    // (S is free: every wave passed this tile's predecessor's phase-2/3 barrier before reaching here.)
-    if (p1) {
-      bool ok[2];
-      int pix[2];
+    // (S is free: every wave passed the previous tile's phase-2 barrier before reaching here.)
+    {
+      // a later tile first moves the S rows it shares with the previous one (16..19 -> 0..3): each
+      // thread copies exactly the chunks it is about to overwrite, before it writes them
+      if (!first) {
+        const int fpx = slot_px(false, 0, tl), qpx = slot_px(false, 1, tl);
+        if (fpx >= OFS + SHIFT) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int i = tid + h * (SPIX / 2);
-        pix[h] = i;
-        const int sy = i / SB_SW, sx = i - (i / SB_SW) * SB_SW;
-        const int oy = ty0 - 2 + sy, ox = tx0 - 2 + sx;
-        ok[h] = oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW;
+          for (int p = 0; p < 4 * R; ++p) copy16(sS + p * SPLANE, fpx * 16, (fpx - SHIFT) * 16);
+        }
+        copy16(sS + qg * SPLANE, qpx * 16, (qpx - SHIFT) * 16);
+        if constexpr (SP) copy16(sS + SLO + qg * SPLANE, qpx * 16, (qpx - SHIFT) * 16);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint32_t v[2][4], vl[2][4];
+      for (int k = 0; k < 4; ++k) {
+        const int px = slot_px(first, k, tl);
+        if (px < 0) continue;
+        const int i = px - OFS, sy = i / SB_SW, sx = i - (i / SB_SW) * SB_SW;
+        const int oy = ty0 - 2 + sy, ox = tx0 - 2 + sx;
+        const bool ok = oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW;
+        if (k == 0) {
 #pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-          const float bj0 = sw9[288 + q * 8 + j], bj1 = sw9[288 + q * 8 + j + 1];
-          float a0 = bj0, a1 = bj1, c0 = bj0, c1 = bj1;
-#pragma unroll
-          for (int k = 0; k < 9; ++k) {
-            float w0, w1;
-            if constexpr (SP) {
-              const float2 w01 = *reinterpret_cast<const float2*>(&sw9[k * 32 + q * 8 + j]);
-              w0 = w01.x;
-              w1 = w01.y;
-            } else {
-              w0 = sw9[(q * 8 + j) * 9 + k];
-              w1 = sw9[(q * 8 + j + 1) * 9 + k];
-            }
-            a0 += w0 * in[0][k];
-            a1 += w1 * in[0][k];
-            c0 += w0 * in[1][k];
-            c1 += w1 * in[1][k];
-          }
-          const float s0 = silu(a0), s1 = silu(a1), t0 = silu(c0), t1 = silu(c1);
-          v[0][j / 2] = ok[0] ? pack_bf16x2(s0, s1) : 0u;
-          v[1][j / 2] = ok[1] ? pack_bf16x2(t0, t1) : 0u;
-          if constexpr (SP) {  // lo halves: v - hi
-            vl[0][j / 2] = ok[0] ? pack_bf16x2(s0 - __uint_as_float(v[0][j / 2] << 16),
-                                               s1 - __uint_as_float(v[0][j / 2] & 0xffff0000u)) : 0u;
-            vl[1][j / 2] = ok[1] ? pack_bf16x2(t0 - __uint_as_float(v[1][j / 2] << 16),
-                                               t1 - __uint_as_float(v[1][j / 2] & 0xffff0000u)) : 0u;
-          }
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          *reinterpret_cast<uint4*>(sS + q * SPLANE + pix[h] * 16) = make_uint4(v[h][0], v[h][1], v[h][2], v[h][3]);
-          if constexpr (SP)
-            *reinterpret_cast<uint4*>(sS + SLO + q * SPLANE + pix[h] * 16) =
-                make_uint4(vl[h][0], vl[h][1], vl[h][2], vl[h][3]);
+          for (int grp = 0; grp < 4; ++grp) stem8(in[0], grp, ok, px);
+        } else if (k == 1) {
+          stem8(in[1], qg, ok, px);
+        } else {
+          float x9[9];
+          load9(x9, st, ty, k, tl);
+          stem8(x9, qg, ok, px);
         }
       }
       // the next tile's frame pixels, in flight through phases 2 and 3
-      if (t + gx < t_end) load_in(t + gx);
+      const int nst = ty + 1 < a.tiles_y ? st : st + gx, nty = ty + 1 < a.tiles_y ? ty + 1 : 0;
+      if (nst < s_end) load_in(nst, nty, tl);
     }
     TR(1);
     __syncthreads();
@@ -224,10 +249,11 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
 
     // ---- phase 2: blocks.0.0 (32 -> 16) on MFMA -> A ------------------------------------------
     {
+      const int sub0 = first ? 0 : ASUB0;  // later tiles: A rows 2..17 (rows 0, 1 carried)
       int sbase[AMS];
 #pragma unroll
       for (int i = 0; i < AMS; ++i) {
-        const int pa = min(16 * (wave + 4 * i) + r16, APIX - 1);
+        const int pa = min(16 * (sub0 + wave + 4 * i) + r16, APIX - 1);
         sbase[i] = pa * 16 + g * SPLANE;  // (A and S share the pitch; the taps of columns 18-19 may read
                                           // into the next plane or the pad: ignored results)
       }
@@ -239,7 +265,7 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
         const int toff = ((k / 3) * SB_SW + (k % 3)) * 16;
 #pragma unroll
         for (int i = 0; i < AMS; ++i) {
-          if (wave + 4 * i < ASUB) {
+          if (sub0 + wave + 4 * i < ASUB) {
             const bf16x8 b = frag(sS + sbase[i] + toff);
             if constexpr (SP)
               acc[i] = mma3(wf0[k], wl0[k], b, frag(sS + SLO + sbase[i] + toff), acc[i]);
@@ -250,9 +276,9 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
       }
 #pragma unroll
       for (int i = 0; i < AMS; ++i) {
-        const int pa = 16 * (wave + 4 * i) + r16;
-        const int ay = pa / SB_AW, ax = pa - (pa / SB_AW) * SB_AW;
-        if (wave + 4 * i >= ASUB || pa >= APIX || ax >= SB_AV) continue;
+        const int pa = 16 * (sub0 + wave + 4 * i) + r16, ai = pa - OFS;
+        const int ay = ai / SB_AW, ax = ai - (ai / SB_AW) * SB_AW;
+        if (sub0 + wave + 4 * i >= ASUB || ai < 0 || ax >= SB_AV) continue;
         const int oy = ty0 - 1 + ay, ox = tx0 - 1 + ax;
         uint2 u = make_uint2(0u, 0u), ul = make_uint2(0u, 0u);
         if (oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW) {
@@ -265,8 +291,13 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
             u.y = pack_bf16x2(v[2], v[3]);
           }
         }
-        *reinterpret_cast<uint2*>(sA + (g >> 1) * APLANE + pa * 16 + (g & 1) * 8) = u;
-        if constexpr (SP) *reinterpret_cast<uint2*>(sA + ALO + (g >> 1) * APLANE + pa * 16 + (g & 1) * 8) = ul;
+        const int ao = (g >> 1) * APLANE + pa * 16 + (g & 1) * 8;
+        if (!first && pa >= OFS + SHIFT) {  // carry A rows 16, 17 -> 0, 1 before overwriting them
+          *reinterpret_cast<uint2*>(sA + ao - SHIFT * 16) = *reinterpret_cast<const uint2*>(sA + ao);
+          if constexpr (SP) *reinterpret_cast<uint2*>(sA + ALO + ao - SHIFT * 16) = *reinterpret_cast<const uint2*>(sA + ALO + ao);
+        }
+        *reinterpret_cast<uint2*>(sA + ao) = u;
+        if constexpr (SP) *reinterpret_cast<uint2*>(sA + ALO + ao) = ul;
       }
     }
     TR(3);
@@ -279,31 +310,31 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
       // 9 (zero weights) reads tap 0's pixel so the product stays finite
       int toff[5];
 #pragma unroll
-      for (int st = 0; st < 5; ++st) {
-        int k = 2 * st + (g >> 1);
+      for (int ks = 0; ks < 5; ++ks) {
+        int k = 2 * ks + (g >> 1);
         if (k > 8) k = 0;
-        toff[st] = ((k / 3) * SB_AW + (k % 3)) * 16 + (g & 1) * APLANE;
+        toff[ks] = ((k / 3) * SB_AW + (k % 3)) * 16 + (g & 1) * APLANE;
       }
       f32x4 acc[OMS];
 #pragma unroll
       for (int i = 0; i < OMS; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int st = 0; st < 5; ++st)
+      for (int ks = 0; ks < 5; ++ks)
 #pragma unroll
         for (int i = 0; i < OMS; ++i) {
           const int row = wave + 4 * i;  // output tile row = subtile
-          const char* p = sA + (row * SB_AW + r16) * 16 + toff[st];
+          const char* p = sA + (OFS + row * SB_AW + r16) * 16 + toff[ks];
           if constexpr (SP)
-            acc[i] = mma3(wf1[st], wl1[st], frag(p), frag(p + ALO), acc[i]);
+            acc[i] = mma3(wf1[ks], wl1[ks], frag(p), frag(p + ALO), acc[i]);
           else
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[st], frag(p), acc[i], 0, 0, 0);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[ks], frag(p), acc[i], 0, 0, 0);
         }
       const int ox = tx0 + r16;
 #pragma unroll
       for (int i = 0; i < OMS; ++i) {
         const int row = wave + 4 * i, oy = ty0 + row;
         if (oy >= a.OH || ox >= a.OW) continue;
-        const int soff = (g >> 1) * APLANE + ((row + 1) * SB_AW + r16 + 1) * 16 + (g & 1) * 8;
+        const int soff = (g >> 1) * APLANE + (OFS + (row + 1) * SB_AW + r16 + 1) * 16 + (g & 1) * 8;
         float r[4];
         unpack_bf16x4(*reinterpret_cast<const uint2*>(sA + soff), r);
         if constexpr (SP) {
@@ -326,6 +357,11 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
       }
     }
     TR(5);
+    ++it;
+    if (++ty == a.tiles_y) {
+      ty = 0;
+      st += gx;
+    }
   }
 }
 
@@ -369,8 +405,8 @@ void launch_stem_b0(const float* frames, int N, int H, int W, int OH, int OW, in
   // persistent grid: the resident workgroups of the device (two per CU split, three bf16), a multiple
   // of 8 (one equal share per XCD); small inputs take fewer
   const int cus = device_cus();
-  const int total = N * a.tiles_x * a.tiles_y;
-  a.per_xcd = ceil_div(total, 8);
+  const int nstrip = N * a.tiles_x;  // a workgroup walks whole strips (image, tile column) top to bottom
+  a.per_xcd = ceil_div(nstrip, 8);
   const int per_cu = split ? 2 : 3;
   const int grid = 8 * std::max(1, std::min(ceil_div(cus * per_cu, 8), a.per_xcd));
   if (split) {

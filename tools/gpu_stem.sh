@@ -1,16 +1,16 @@
 #!/bin/bash
-# stem_b0 iteration: parity tests that run it (every-block taps fp32 / bf16x3 / bf16, configs), then kernel
-# stats of the bench step in bf16x3 and bf16.  Usage: bash tools/gpu_stem.sh <tag>
+# stem_b0 iteration: its parity tests, the diagnostic per-phase stamps, the headline bench's kernel table.
 set -o pipefail
 OUT=gpurun_out/${1:-stem}
-ROOT=$(pwd)
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "effnet or config or smoke or bf16" > "$OUT/pytest.log" 2>&1 \
-  || { tail -30 "$OUT/pytest.log"; exit 1; }
-tail -1 "$OUT/pytest.log"
-for dt in bf16x3 bf16; do
-  (cd /tmp && export DTYPE=$dt && STEPS=3 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/$dt" -o run -- \
-     python3 "$ROOT/tools/profile_step.py" > "$ROOT/$OUT/$dt.log" 2>&1) || exit 1
-  echo "== $dt"; python3 tools/kstats.py "$OUT/$dt" 3 > "$OUT/$dt.txt"; grep -E "total|stem" "$OUT/$dt.txt"
-done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  -k "every_block or fused_kernels_vs_unfused or test_pipeline_bf16x3_end_to_end" > "$OUT/pytest.log" 2>&1 \
+  || { tail -40 "$OUT/pytest.log"; exit 1; }
+tail -2 "$OUT/pytest.log"
+M2S_IR_WS_TRACE=1 timeout -k 10 200 python -u tools/trace_ir_ws.py > "$OUT/trace.txt" 2>&1 || { tail -20 "$OUT/trace.txt"; exit 1; }
+grep -o "STEMTRACE.\{0,900\}" "$OUT/trace.txt" | head -1
+M2S_BENCH_KERNELS=1 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-compare --no-cpu-baseline --no-parity --no-long \
+  > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
+cut -c1-250 "$OUT/bench.json"
+grep "stem_b0\|lstm" "$OUT/bench.err"
