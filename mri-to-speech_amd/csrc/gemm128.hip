@@ -74,8 +74,9 @@ struct G128Args {
   const bf16_t* gate;   // SE: [M / P][cs_in] (SP: split [M / P][hi cs_in | lo cs_in])
   const bf16_t* res;    // [M][cs_out] or null (SP: split [M][hi cs_out | lo cs_out])
   bf16_t* y;            // [M][cs_out] bf16 or null (SP: split)
-  uint8_t* y8;          // C1D: [M][cs_out] e4m3 of lrelu(v, slope8) or null
+  uint8_t* y8;          // C1D: [M][cs_out] e4m3 of lrelu(v, slope8); F8 SE: [M][ld8] e4m3 of v; or null
   int M, P, cs_in, kp, cs_out, n_tiles, nimg;  // P: SE rows per image, C1D sequence length L
+  int ld8;                                      // F8 SE: y8 row bytes
   int dil, pad_left, accum;                     // C1D: tap dilation, causal left pad, MRF sum mode (0 / 1 / 2)
   float accum_div, slope8;
 };
@@ -384,6 +385,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) gemm128_kernel(const G128Args
         for (int j = 0; j < 4; ++j) v[j] = a.accum == 2 ? (p[j] + v[j]) / a.accum_div : p[j] + v[j];
       }
       if (SE || Y) *reinterpret_cast<uint2*>(Y + o) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      if (SE && a.y8) {  // the next IR block's e4m3 expand operand
+        const float l[8] = {v[0], v[1], v[2], v[3], 0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<uint32_t*>(a.y8 + (size_t)m * a.ld8 + n4) = e4m3x8(l).x;
+      }
       if (!SE && a.y8) {  // the next conv's operand: e4m3(lrelu(v))
         float l[8];
 #pragma unroll
@@ -429,9 +434,10 @@ bool se_gemm_f8_supported(int P, int cs_in, int cs_out) {
 
 void launch_se_gemm_f8(const void* x8, int M, int P, int cs_in, const void* w8, int kp, int n_pad, const float* wscale,
                        const float* bias, const void* gate, const void* res, void* y, int cs_out, hipStream_t s,
-                       double flops, double bytes) {
+                       double flops, double bytes, void* y8, int ld8) {
   M2S_CHECK(se_gemm_f8_supported(P, cs_in, cs_out) && kp % F8_ROW == 0 && kp >= cs_in && M % P == 0,
             "se_gemm_f8: unsupported shape");
+  M2S_CHECK(!y8 || (ld8 >= cs_out && ld8 % 16 == 0 && y8 != x8), "se_gemm_f8: e4m3 output rows");
   M2S_CHECK(x8 && w8 && wscale && bias && gate && y && y != res && y != x8, "se_gemm_f8: operand pointers");
   M2S_CHECK((double)M * cs_in < 4294967295.0, "se_gemm_f8: input too large");
   if (M <= 0) return;
@@ -443,6 +449,8 @@ void launch_se_gemm_f8(const void* x8, int M, int P, int cs_in, const void* w8, 
   a.gate = static_cast<const bf16_t*>(gate);
   a.res = static_cast<const bf16_t*>(res);
   a.y = static_cast<bf16_t*>(y);
+  a.y8 = static_cast<uint8_t*>(y8);
+  a.ld8 = ld8;
   a.M = M;
   a.P = P;
   a.cs_in = cs_in;

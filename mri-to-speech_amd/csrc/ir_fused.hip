@@ -32,6 +32,8 @@
 namespace m2s {
 namespace {
 
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
 constexpr int SL = 32;         // expanded channels per slice
 constexpr int MROW = SL + 8;   // bf16 LDS row stride in bf16 (80 B)
 constexpr int MROWF = SL + 4;  // fp32 (SP) LDS row stride in floats (144 B)
@@ -60,9 +62,12 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
                                                          const float* __restrict__ bdw, int N, int OH, int OW,
                                                          int cs_mid, bf16_t* __restrict__ y,
                                                          bf16_t* __restrict__ se_mean, int SOH, int SOW, int pad_t,
-                                                         int pad_l) {
+                                                         int pad_l, const float* __restrict__ wsc = nullptr) {
   constexpr bool SP = SPM == 1;  // split fp32
-  constexpr bool F8 = SPM == 2;  // bf16 compute, e4m3 depthwise output (fp8 engines: the e4m3 SE GEMM's operand)
+  constexpr bool F8 = SPM >= 2;  // e4m3 depthwise output (fp8 engines: the e4m3 SE GEMM's operand)
+  // SPM = 3: the expand on e4m3 too: x = e4m3 rows of kp bytes (launch_se_*_f8 y8), wpw = e4m3 [rows][kp] with
+  // per-channel scales wsc (pack_gemm_f8), one v_mfma_scale_f32_16x16x128_f8f6f4 per 128 k
+  constexpr bool F8I = SPM == 3;
   // the haloed tile: dynamic LDS sized for this launch's G images (ir_tile_bytes)
   extern __shared__ __attribute__((aligned(16))) char tile_raw[];
   bf16_t* tile = reinterpret_cast<bf16_t*>(tile_raw);
@@ -192,7 +197,31 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
         __builtin_amdgcn_sched_barrier(0);
       }
     };
-    if (kp == 128 && cs_in == 128) {
+    if constexpr (F8I) {
+      const uint8_t* x8 = reinterpret_cast<const uint8_t*>(x) + (size_t)n0 * P * kp;
+      const uint8_t* w8 = reinterpret_cast<const uint8_t*>(wpw);
+      for (int k0 = 0; k0 < kp; k0 += 128) {  // lane (r16, g16): 32 consecutive k bytes 32 g16 .. of its row
+        i32x8 af[NT], bx[MT];
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni) {
+          const uint4* wp = reinterpret_cast<const uint4*>(w8 + (size_t)(c0 + ni * 16 + r16) * kp + k0 + 32 * g16);
+          const uint4 u0 = wp[0], u1 = wp[1];
+          af[ni] = i32x8{(int)u0.x, (int)u0.y, (int)u0.z, (int)u0.w, (int)u1.x, (int)u1.y, (int)u1.z, (int)u1.w};
+        }
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi) {  // positions past MP read a clamped row: their columns are discarded
+          const uint4* xp = reinterpret_cast<const uint4*>(x8 + (size_t)min(mw + mi * 16 + r16, MP - 1) * kp + k0 + 32 * g16);
+          const uint4 u0 = xp[0], u1 = xp[1];
+          bx[mi] = i32x8{(int)u0.x, (int)u0.y, (int)u0.z, (int)u0.w, (int)u1.x, (int)u1.y, (int)u1.z, (int)u1.w};
+        }
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+          for (int mi = 0; mi < MT; ++mi)
+            acc[ni][mi] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[ni], bx[mi], acc[ni][mi], 0, 0, 0,
+                                                                           0x7f7f7f7f, 0, 0x7f7f7f7f);
+      }
+    } else if (kp == 128 && cs_in == 128) {
       unrolled(std::integral_constant<int, 4>());
     } else if (kp == 224 && cs_in == 224) {
       unrolled(std::integral_constant<int, 7>());
@@ -212,6 +241,16 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
     for (int ni = 0; ni < NT; ++ni) {
       const int cl = ni * 16 + 4 * g16;  // slice-local channel of acc[ni][.][0]
       const float4 bb = *reinterpret_cast<const float4*>(bpw + c0 + cl);
+      if constexpr (F8I) {  // the e4m3 weights' per-channel scales
+        const float4 sc = *reinterpret_cast<const float4*>(wsc + c0 + cl);
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi) {
+          acc[ni][mi][0] *= sc.x;
+          acc[ni][mi][1] *= sc.y;
+          acc[ni][mi][2] *= sc.z;
+          acc[ni][mi][3] *= sc.w;
+        }
+      }
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi) {
         const int m = mw + mi * 16 + r16;
@@ -364,8 +403,9 @@ template <int MT, int G, int SP>
 __global__ void __launch_bounds__(256, SP == 1 ? (MT >= 4 ? 3 : 4) : 4)
     ir_pwdw_kernel(const bf16_t* __restrict__ x, int cs_in, int kp, const bf16_t* __restrict__ wpw,
                    const float* __restrict__ bpw, const uint32_t* __restrict__ wdw2, const float* __restrict__ bdw, int N,
-                   int OH, int OW, int cs_mid, bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean) {
-  ir_pwdw_body<MT, G, 1, SP>(x, cs_in, kp, wpw, bpw, wdw2, bdw, N, OH, OW, cs_mid, y, se_mean, OH, OW, 1, 1);
+                   int OH, int OW, int cs_mid, bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean,
+                   const float* __restrict__ wsc) {
+  ir_pwdw_body<MT, G, 1, SP>(x, cs_in, kp, wpw, bpw, wdw2, bdw, N, OH, OW, cs_mid, y, se_mean, OH, OW, 1, 1, wsc);
 }
 
 template <int SP>
@@ -399,11 +439,18 @@ bool ir_fused_supported(int OH, int OW, int cs_in, int cs_mid, bool split) {
 
 void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, const float* bpw, const void* wdw,
                     const float* bdw, int OH, int OW, int cs_mid, void* y, void* se_mean, bool split, double flops,
-                    double bytes, hipStream_t s, bool f8_out) {
+                    double bytes, hipStream_t s, bool f8_out, const void* x8, const void* w8, const float* wsc, int kp8) {
   M2S_CHECK(ir_fused_supported(OH, OW, cs_in, cs_mid, split), "ir_pwdw: unsupported shape");
   M2S_CHECK(!(split && f8_out), "ir_pwdw: e4m3 output is a bf16-path variant");
-  const int mode = split ? 1 : f8_out ? 2 : 0;
+  const bool f8_in = x8 != nullptr;
+  M2S_CHECK(!f8_in || (f8_out && w8 && wsc && kp8 % 128 == 0 && kp8 >= cs_in), "ir_pwdw: e4m3 expand operands");
+  const int mode = split ? 1 : f8_in ? 3 : f8_out ? 2 : 0;
   M2S_CHECK(kp % 32 == 0 && kp >= cs_in, "ir_pwdw: kp");
+  if (f8_in) {  // the e4m3 operands replace the bf16 ones
+    x = x8;
+    wpw = w8;
+    kp = kp8;
+  }
   const int G = ir_group(OH, OW, split), pos = G * OH * OW;
   const dim3 grid(ceil_div(cs_mid, SL) * ceil_div(N, G));
   const bf16_t* xb = static_cast<const bf16_t*>(x);
@@ -417,7 +464,7 @@ void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, co
   if (pos <= 64 * MT_ && G == G_ && mode == SP_) {                                                 \
     ProfScope ps("ir_pwdw_kernel<" #MT_ ", " #G_ ", " #SP_ ">", flops, bytes, s);                       \
     hipLaunchKernelGGL((ir_pwdw_kernel<MT_, G_, SP_>), grid, dim3(256), ir_tile_bytes(OH, OW, G, split), s, xb, cs_in, \
-                       kp, wb, bpw, wd, bdw, N, OH, OW, cs_mid, yb, mb);                                 \
+                       kp, wb, bpw, wd, bdw, N, OH, OW, cs_mid, yb, mb, wsc);                            \
     M2S_HIP(hipGetLastError());                                                                          \
     return;                                                                                              \
   }
@@ -428,8 +475,33 @@ void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, co
   M2S_IRF(2, 1, 1) M2S_IRF(2, 2, 1) M2S_IRF(2, 4, 1)
   M2S_IRF(4, 1, 1) M2S_IRF(4, 2, 1) M2S_IRF(4, 4, 1)
   M2S_IRF(4, 1, 2) M2S_IRF(4, 2, 2) M2S_IRF(4, 4, 2)
+  M2S_IRF(4, 1, 3) M2S_IRF(4, 2, 3) M2S_IRF(4, 4, 3)
 #undef M2S_IRF
   M2S_CHECK(false, "ir_pwdw: no variant for this shape");
+}
+
+__global__ void rows_e4m3_kernel(const uint4* __restrict__ x, long rows, int cs8, uint2* __restrict__ y8, int ld8_8) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one 8-byte group of one row
+  if (i >= rows * ld8_8) return;
+  const long r = i / ld8_8;
+  const int c = (int)(i - r * ld8_8);
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < cs8) {
+    const uint4 u = x[r * cs8 + c];
+    unpack_bf16x4(make_uint2(u.x, u.y), v);
+    unpack_bf16x4(make_uint2(u.z, u.w), v + 4);
+  }
+  y8[i] = e4m3x8(v);
+}
+
+void launch_rows_e4m3(const void* x, long rows, int cs, void* y8, int ld8, hipStream_t s) {
+  M2S_CHECK(cs % 8 == 0 && ld8 % 8 == 0 && ld8 >= cs && rows >= 0, "rows_e4m3: shape");
+  const long n = rows * (ld8 / 8);
+  if (n == 0) return;
+  ProfScope ps("rows_e4m3_kernel", 0.0, (double)rows * (2.0 * cs + ld8), s);
+  hipLaunchKernelGGL(rows_e4m3_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, static_cast<const uint4*>(x), rows,
+                     cs / 8, static_cast<uint2*>(y8), ld8 / 8);
+  M2S_HIP(hipGetLastError());
 }
 
 bool ir_fused_s2_supported(int IH, int IW, int cs_in, int cs_mid, bool split) {

@@ -33,18 +33,26 @@ void launch_se_mean(const float* psum, int N, int npb, int cs, float inv_count, 
 bool ir_fused_supported(int OH, int OW, int cs_in, int cs_mid, bool split);
 void launch_ir_pwdw(const void* x, int N, int cs_in, int kp, const void* wpw, const float* bpw, const void* wdw,
                     const float* bdw, int OH, int OW, int cs_mid, void* y, void* se_mean, bool split, double flops,
-                    double bytes, hipStream_t s, bool f8_out = false);
+                    double bytes, hipStream_t s, bool f8_out = false, const void* x8 = nullptr,
+                    const void* w8 = nullptr, const float* wsc = nullptr, int kp8 = 0);
 // f8_out (bf16 inputs and weights): the depthwise output y is stored as OCP e4m3 bytes [N][P][cs_mid]
 // (saturated to +-448), the operand of launch_se_gemm_f8; the SE means stay bf16 (exact sums).
+// x8 (with f8_out): the expand runs on e4m3 too: x8 = the block input as e4m3 rows of kp8 bytes (kp8 = cs_in
+// rounded up to 128, zero past cs_in; launch_se_*_f8 y8 / launch_rows_e4m3), w8 = e4m3 [rows][kp8] with
+// per-channel scales wsc (pack_gemm_f8), one block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 per 128 k.
+// bf16 (N*P, cs) rows -> e4m3 rows of ld8 bytes (zeros past cs): an e4m3 expand operand for a block input
+// no e4m3 producer wrote.
+void launch_rows_e4m3(const void* x, long rows, int cs, void* y8, int ld8, hipStream_t s);
 
 // fp8 engines: the SE-gated conv_pwl (+ bn3 + skip) of a stride-1 IR block on v_mfma_scale_f32_16x16x128_f8f6f4:
 // y (M, cs_out) bf16 = wscale[n] * sum_k w8[n][k] e4m3(gate[m / P][k] x8[m][k]) + bias[n] (+ res (M, cs_out) bf16).
 // x8: e4m3 (M, cs_in) (launch_ir_pwdw f8_out); w8: e4m3 [n_pad][kp], kp = cs_in rounded up to 128, zero
 // padded (pack_gemm_f8); gate: bf16 (M / P, cs_in).  P % 64 == 0, cs_out <= 224.  (gemm128.hip)
+// y8 (optional): an e4m3 copy of y, rows of ld8 bytes (the next IR block's expand operand).
 bool se_gemm_f8_supported(int P, int cs_in, int cs_out);
 void launch_se_gemm_f8(const void* x8, int M, int P, int cs_in, const void* w8, int kp, int n_pad, const float* wscale,
                        const float* bias, const void* gate, const void* res, void* y, int cs_out, hipStream_t s,
-                       double flops, double bytes);
+                       double flops, double bytes, void* y8 = nullptr, int ld8 = 0);
 
 // bf16x3 engines: the same SE-gated conv_pwl (+ bn3 + skip) in split fp32 on gemm128.hip: x interleaved split
 // (M, cs_in / 32, [hi 32 | lo 32]) (il_st8), w split rows [hi cs_in | lo cs_in] (conv_gemm packing, n_pad rows),
@@ -64,9 +72,10 @@ void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_p
 // fp8 engines: launch_se_gemm_f8's operation (e4m3 x8 / w8, bf16 gate / res / y) on the same warp-specialised
 // flag ring.  (se_ws.hip)
 bool se_ws_f8_supported(int P, int cs_in, int cs_out);
+// y8 (optional): an e4m3 copy of y, rows of ld8 bytes (the next IR block's e4m3 expand operand, launch_ir_pwdw x8)
 void launch_se_ws_f8(const void* x8, int M, int P, int cs_in, const void* w8, int kp, int n_pad, const float* wscale,
                      const float* bias, const void* gate, const void* res, void* y, int cs_out, hipStream_t s, double flops,
-                     double bytes);
+                     double bytes, void* y8 = nullptr, int ld8 = 0);
 
 // The same for a stride-2 depthwise (TF-SAME, top / left pads pad_t / pad_l) on an IH x IW <= 256-pixel
 // conv_pw map: y (N, OH*OW, cs_mid), se_mean over the OH x OW output.  (ir_fused.hip)

@@ -83,6 +83,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_IR_FUSED")) ir_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_IR_WS")) ir_ws_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_F8_EXPAND")) f8_expand_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_FUSED")) se_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER_FUSED")) er_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_SP")) se_sp_ = std::strcmp(e, "0") != 0;  // A/B only
@@ -300,6 +301,15 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
         const int m = b.mid, cs = chan_stride(m);
         max_mid_cs_ = std::max(max_mid_cs_, cs);
         conv1x1(b.c1, q + "conv_pw.weight", cin, m, fold_bn(sd, q + "bn1", m));
+        if (dtype == M2S_DT_FP8 && b.stride == 1 && chan_stride(cin) <= 256) {  // the e4m3 expand (ir_pwdw x8)
+          const float* wq = need(sd, q + "conv_pw.weight", {m, cin, 1, 1}).data;
+          const BN bn1 = fold_bn(sd, q + "bn1", m);
+          size_t boff = 0;
+          b.f8x_kp = round_up(chan_stride(cin), 128);
+          pack_gemm_f8(arena_, cin, m, round_up(cs, 32), b.f8x_kp, [&](int n, int c) { return wq[(size_t)n * cin + c] * bn1.a[n]; },
+                       [&](int n) { return bn1.b[n]; }, &b.f8x_w, &b.f8x_s, &boff);
+          b.f8_pw = true;
+        }
         const float* wd = need(sd, q + "conv_dw.weight", {m, 1, k, k}).data;
         BN bn2 = fold_bn(sd, q + "bn2", m);
         std::vector<float> w9((size_t)cs * 9, 0.f), bd(cs, 0.f);
@@ -426,6 +436,23 @@ void Acoustic::effnet_dims(int H, int W, size_t* io, size_t* mid, size_t* se) co
   *se = mse;
 }
 
+size_t Acoustic::effnet_x8(int H, int W) const {
+  if (dtype_ != M2S_DT_FP8 || !f8_expand_) return 0;
+  int oh, ow, ph, pw;
+  same_pad(H, 3, 2, &oh, &ph);
+  same_pad(W, 3, 2, &ow, &pw);
+  size_t mx = 0;
+  for (const Block& b : blocks_) {
+    int nh, nw;
+    same_pad(oh, 3, b.stride, &nh, &ph);
+    same_pad(ow, 3, b.stride, &nw, &pw);
+    if (b.f8_pw) mx = std::max(mx, (size_t)nh * nw * b.f8x_kp);  // stride 1: the block input's map
+    oh = nh;
+    ow = nw;
+  }
+  return round_up((int)mx, 256);
+}
+
 size_t Acoustic::effnet_ws(int N, int H, int W) const {
   size_t io, mid, se;
   effnet_dims(H, W, &io, &mid, &se);
@@ -440,6 +467,8 @@ size_t Acoustic::effnet_ws(int N, int H, int W) const {
   ws.take<char>(nc * max_mid_cs_ * es);   // SE means
   ws.take<char>(nc * SE_RD_MAX * es);     // SE hidden (rd <= 64)
   ws.take<char>(nc * max_mid_cs_ * es);   // SE gates
+  ws.take<char>(nc * effnet_x8(H, W));    // fp8: e4m3 expand operands, two buffers
+  ws.take<char>(nc * effnet_x8(H, W));
   return ws.used();
 }
 
@@ -481,6 +510,14 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
   T* se_mean = ws.take<T>((size_t)nc_max * max_mid_cs_ * R);
   T* se_hid = ws.take<T>((size_t)nc_max * SE_RD_MAX * R);
   T* scale = ws.take<T>((size_t)nc_max * max_mid_cs_ * R);
+  // fp8: e4m3 copies of IR block inputs (the e4m3 expand's operand), written by the previous block's SE GEMM
+  // (y8) or converted; zeroed once so the pad bytes past cs_in (never written) stay finite
+  const size_t x8b = effnet_x8(H, W);
+  uint8_t* X8[2] = {x8b ? ws.take<uint8_t>((size_t)nc_max * x8b) : nullptr, x8b ? ws.take<uint8_t>((size_t)nc_max * x8b) : nullptr};
+  if (x8b) {
+    M2S_HIP(hipMemsetAsync(X8[0], 0, (size_t)nc_max * x8b, s));
+    M2S_HIP(hipMemsetAsync(X8[1], 0, (size_t)nc_max * x8b, s));
+  }
 
   for (int n0 = 0; n0 < N; n0 += nc_max) {
     const int nc = std::min(nc_max, N - n0);
@@ -525,8 +562,12 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
     };
     if (tap(bi)) continue;  // bi = 0, or 2 after the fused front
     bool stopped = false;
+    uint8_t* cur8 = nullptr;  // fp8: the e4m3 copy of cur in X8[0] / X8[1], when one was written
     for (size_t k = front ? 2 : 0; k < blocks_.size(); ++k) {
       const Block& b = blocks_[k];
+      uint8_t* next8 = nullptr;  // the e4m3 copy of this block's output, if its SE GEMM wrote one
+      // the next block takes an e4m3 expand operand (fp8 engines, stride-1 IR blocks)
+      const bool want8 = X8[0] && k + 1 < blocks_.size() && blocks_[k + 1].f8_pw && blocks_[k + 1].stride == 1;
       int nh, nw, qt, ql;
       same_pad(oh, 3, b.stride, &nh, &qt);
       same_pad(ow, 3, b.stride, &nw, &ql);
@@ -606,9 +647,16 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         } else if (FUSABLE && b.stride == 1 && ir_fused_ && ir_fused_supported(nh, nw, b.c1.cs_in, cs, SPL)) {
           const double P = (double)nh * nw, es = SPL ? 4.0 : 2.0;
           f8 = b.f8_pwl && se_gemm_f8_supported(nh * nw, cs, chan_stride(b.cout));
+          const bool f8x = f8 && b.f8_pw && X8[0];  // the expand on e4m3 (x8 of the block input)
+          if (f8x && !cur8) {  // no e4m3 producer wrote this input: convert it
+            cur8 = X8[0];
+            launch_rows_e4m3(cur, (long)nc * nh * nw, b.c1.cs_in, cur8, b.f8x_kp, s);
+          }
           launch_ir_pwdw(cur, nc, b.c1.cs_in, b.c1.kp, b.c1.w, b.c1.b, wdw, static_cast<const float*>(arena_.ptr(b.dw_b)),
                          nh, nw, cs, M2, se_mean, SPL, 2.0 * nc * P * b.mid * (b.c1.cin + 9),
-                         nc * P * (es * b.c1.cs_in + (f8 ? 1.0 : es) * cs), s, f8);
+                         nc * P * ((f8x ? 1.0 : es) * b.c1.cs_in + (f8 ? 1.0 : es) * cs), s, f8, f8x ? cur8 : nullptr,
+                         f8x ? arena_.ptr(b.f8x_w) : nullptr, f8x ? static_cast<const float*>(arena_.ptr(b.f8x_s)) : nullptr,
+                         b.f8x_kp);
         } else if (FUSABLE && b.stride == 2 && ir_fused_ && ir_fused_s2_supported(oh, ow, b.c1.cs_in, cs, SPL) &&
                    nh * nw <= 64) {
           const double Pi = (double)oh * ow, Po = (double)nh * nw, es = SPL ? 4.0 : 2.0;
@@ -660,19 +708,25 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         r2.act = ACT_SIGMOID;
         run_conv<T>(r2, b.se2, s);
         }
+        // fp8: an e4m3 copy of the output for the next block's expand, into the buffer cur8 does not hold
+        const int ld8 = want8 ? blocks_[k + 1].f8x_kp : 0;
+        if (f8 && want8) next8 = cur8 == X8[0] ? X8[1] : X8[0];
         if (f8 && se_ws_ && se_ws_f8_supported(nh * nw, cs, chan_stride(b.cout))) {
           const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
           launch_se_ws_f8(M2, nc * nh * nw, nh * nw, cs, arena_.ptr(b.f8_w), b.f8_kp, b.f8_npad,
                           static_cast<const float*>(arena_.ptr(b.f8_s)), static_cast<const float*>(arena_.ptr(b.f8_b)),
                           scale, b.skip ? cur : nullptr, nxt, chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
-                          rows * cs + 2.0 * rows * co * (b.skip ? 2.0 : 1.0) + (double)b.f8_npad * b.f8_kp + 2.0 * nc * cs);
+                          rows * cs + 2.0 * rows * co * (b.skip ? 2.0 : 1.0) + (double)b.f8_npad * b.f8_kp + 2.0 * nc * cs +
+                              (next8 ? rows * ld8 : 0.0),
+                          next8, ld8);
         } else if (f8) {
           const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
           launch_se_gemm_f8(M2, nc * nh * nw, nh * nw, cs, arena_.ptr(b.f8_w), b.f8_kp, b.f8_npad,
                             static_cast<const float*>(arena_.ptr(b.f8_s)), static_cast<const float*>(arena_.ptr(b.f8_b)),
                             scale, b.skip ? cur : nullptr, nxt, chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
                             rows * cs + 2.0 * rows * co * (b.skip ? 2.0 : 1.0) + (double)b.f8_npad * b.f8_kp +
-                                2.0 * nc * cs);
+                                2.0 * nc * cs + (next8 ? rows * ld8 : 0.0),
+                            next8, ld8);
         } else if (SPL && se_ws_ && se_ws_supported(nh * nw, cs, chan_stride(b.cout))) {
           const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
           launch_se_ws(M2, nc * nh * nw, nh * nw, cs, b.c2.w, b.c2.n_pad, b.c2.b, scale, b.skip ? cur : nullptr, nxt,
@@ -697,6 +751,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         }
       }
       std::swap(cur, nxt);
+      cur8 = next8;
       oh = nh;
       ow = nw;
       cc = b.cout;

@@ -94,6 +94,7 @@ class Acoustic {
   bool ir_fused_ = true;  // bf16: fused conv_pw + conv_dw + SE squeeze (env M2S_IR_FUSED=0 disables)
   bool ir_ws_ = true;     // split fp32: the persistent warp-specialised form of it (env M2S_IR_WS=0 disables)
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
+  bool f8_expand_ = false;       // fp8: the stride-1 IR expand on e4m3 (env M2S_F8_EXPAND=1; off: bf16 expand)
   bool se_fused_ = true;    // bf16: SE excitation in one kernel (env M2S_SE_FUSED=0: two GEMMs)
   bool er_fused_ = true;    // bf16: EdgeResidual 32->128->32 in one kernel (env M2S_ER_FUSED=0 disables)
   bool se_sp_ = false;      // split: SE-gated conv_pwl on gemm128.hip (env M2S_SE_SP=1; default conv_gemm's in-LDS
@@ -132,11 +133,16 @@ class Acoustic {
     size_t f8_w = 0, f8_s = 0, f8_b = 0;
     int f8_kp = 0, f8_npad = 0;
     bool f8_pwl = false;
+    // fp8 engines, ir conv_pw (stride 1): e4m3 bytes [round_up(cs_mid, 32)][f8x_kp] of W / scale, scales
+    size_t f8x_w = 0, f8x_s = 0;
+    int f8x_kp = 0;
+    bool f8_pw = false;
   };
   template <typename T>
   void effnet_t(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe, int* probe_dims,
                 Workspace& ws, hipStream_t s);
   size_t effnet_ws(int N, int H, int W) const;
+  size_t effnet_x8(int H, int W) const;  // fp8 engines: bytes per image of an e4m3 expand-operand buffer
   void effnet_dims(int H, int W, size_t* io_elems, size_t* mid_elems, size_t* se_elems) const;
 
   int dtype_, device_, n_mels_, hidden_;

@@ -75,7 +75,9 @@ struct SeWsArgs {
   const uint8_t* gate;    // split gates; F8: bf16 [M / P][cs_in]
   const bf16_t* res;      // split skip or null; F8: bf16 [M][cs_out]
   bf16_t* y;              // split output; F8: bf16 [M][cs_out]
+  uint8_t* y8;            // F8: e4m3 copy of y (the next IR block's expand operand, rows of ld8 bytes) or null
   int M, P, cs_in, cs_out, n_tiles_m, kp;  // kp: F8 weight row bytes (cs_in rounded up to 128)
+  int ld8;
 };
 
 constexpr int E8M0_ONE = 0x7f7f7f7f;  // 2^0 block scale in every byte
@@ -367,6 +369,10 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
                               fmaf(acc[ni][mi][2], ws.z, bb.z) + r[2], fmaf(acc[ni][mi][3], ws.w, bb.w) + r[3]};
           *reinterpret_cast<uint2*>(a.y + (size_t)m * a.cs_out + n4) =
               make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+          if (a.y8) {
+            const float l[8] = {v[0], v[1], v[2], v[3], 0.f, 0.f, 0.f, 0.f};
+            *reinterpret_cast<uint32_t*>(a.y8 + (size_t)m * a.ld8 + n4) = e4m3x8(l).x;
+          }
         }
       }
       continue;
@@ -495,9 +501,10 @@ bool se_ws_f8_supported(int P, int cs_in, int cs_out) {
 
 void launch_se_ws_f8(const void* x8, int M, int P, int cs_in, const void* w8, int kp, int n_pad, const float* wscale,
                      const float* bias, const void* gate, const void* res, void* y, int cs_out, hipStream_t s, double flops,
-                     double bytes) {
+                     double bytes, void* y8, int ld8) {
   M2S_CHECK(se_ws_f8_supported(P, cs_in, cs_out) && kp % 128 == 0 && kp >= cs_in && M % P == 0 && cs_out % 4 == 0,
             "se_ws_f8: unsupported shape");
+  M2S_CHECK(!y8 || (ld8 >= cs_out && ld8 % 16 == 0 && y8 != x8), "se_ws_f8: e4m3 output rows");
   M2S_CHECK(x8 && w8 && wscale && bias && gate && y && y != res && y != x8, "se_ws_f8: operand pointers");
   M2S_CHECK((double)M * cs_in < 2147483647.0, "se_ws_f8: input too large");
   if (M <= 0) return;
@@ -515,6 +522,8 @@ void launch_se_ws_f8(const void* x8, int M, int P, int cs_in, const void* w8, in
   a.cs_in = cs_in;
   a.cs_out = cs_out;
   a.kp = kp;
+  a.y8 = static_cast<uint8_t*>(y8);
+  a.ld8 = ld8;
   if (cs_out <= 128) {
     M2S_CHECK(n_pad >= 128, "se_ws_f8: weight rows");
     // 128 x 128 (half a 16x16 image), 4 consumers + 4 loaders, 4 slots: the 8-consumer 256-row tile of the

@@ -228,3 +228,4 @@ def test_se_ws_matches_barrier_ring(rt, ac_state, monkeypatch, n):
         sd = {k: torch.from_numpy(v) for k, v in ac_state.items()}
         ref = effnet.effnet_gap(sd, fr.cpu()).numpy()
         assert _rel(ws.effnet(fr).cpu().numpy(), ref) <= 1e-4
+

@@ -166,3 +166,31 @@ def test_se_ws_f8_matches_gemm128(rt, monkeypatch, n):
         ref = effnet.effnet_gap(sd, fr.cpu()).numpy()
         f = ws.effnet(fr).cpu().numpy()
         assert min(_cos(f[i], ref[i]) for i in range(n)) >= 0.999
+
+
+@pytest.mark.parametrize("n", [5, 300])
+def test_fp8_e4m3_expand(rt, monkeypatch, n):
+    """The fp8 engine's stride-1 IR expand (conv_pw + bn1) on e4m3 (ir_pwdw mode 3: the block input as e4m3
+    rows written by the previous block's SE GEMM epilogue or converted, per-channel-scaled e4m3 weights,
+    v_mfma_scale_f32_16x16x128_f8f6f4) against the bf16 expand (M2S_F8_EXPAND=0) and the fp32 oracle.  One
+    more e4m3 rounding per IR block, so the bars are cosines: every probed tap >= 0.995 against the bf16
+    expand, pooled features per frame >= 0.995 against the oracle (0.99 end to end)."""
+    st = synth.synth_acoustic_state(8)
+    fr = torch.from_numpy(synth.synth_frames(1, n, seed=45)[0]).to(DEV)
+    monkeypatch.setenv("M2S_F8_EXPAND", "1")
+    e8 = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    monkeypatch.setenv("M2S_F8_EXPAND", "0")
+    eb = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    for i in (10, 13, 18, 20, 28):  # after blocks 3.1, 4.0, 4.5, 5.1, 5.9
+        a, b = e8.probe(fr, i).cpu().numpy(), eb.probe(fr, i).cpu().numpy()
+        assert np.isfinite(a).all()
+        c = _cos(a.ravel(), b.ravel())
+        print(f"tap {i}: cos(e4m3 expand, bf16 expand) {c:.6f}")
+        assert c >= 0.995, (i, c)
+    if n == 5:
+        sd = {k: torch.from_numpy(v) for k, v in st.items()}
+        ref = effnet.effnet_gap(sd, fr.cpu()).numpy()
+        f = e8.effnet(fr).cpu().numpy()
+        cmin = min(_cos(f[i], ref[i]) for i in range(n))
+        print(f"features vs oracle: min per-frame cos {cmin:.6f}")
+        assert cmin >= 0.995
