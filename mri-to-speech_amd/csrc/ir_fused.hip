@@ -208,10 +208,13 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
           const uint4 u0 = wp[0], u1 = wp[1];
           af[ni] = i32x8{(int)u0.x, (int)u0.y, (int)u0.z, (int)u0.w, (int)u1.x, (int)u1.y, (int)u1.z, (int)u1.w};
         }
+        // the row bytes past cs_in are not read: the buffer's rows are laid out per stage (128 / 256 bytes), so
+        // a 256-byte row's pad can hold an earlier stage's bytes, NaN included (0 x NaN would leak it)
+        const bool kin = k0 + 32 * g16 < cs_in;
 #pragma unroll
         for (int mi = 0; mi < MT; ++mi) {  // positions past MP read a clamped row: their columns are discarded
           const uint4* xp = reinterpret_cast<const uint4*>(x8 + (size_t)min(mw + mi * 16 + r16, MP - 1) * kp + k0 + 32 * g16);
-          const uint4 u0 = xp[0], u1 = xp[1];
+          const uint4 u0 = kin ? xp[0] : make_uint4(0u, 0u, 0u, 0u), u1 = kin ? xp[1] : make_uint4(0u, 0u, 0u, 0u);
           bx[mi] = i32x8{(int)u0.x, (int)u0.y, (int)u0.z, (int)u0.w, (int)u1.x, (int)u1.y, (int)u1.z, (int)u1.w};
         }
 #pragma unroll

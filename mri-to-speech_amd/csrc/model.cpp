@@ -511,13 +511,9 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
   T* se_hid = ws.take<T>((size_t)nc_max * SE_RD_MAX * R);
   T* scale = ws.take<T>((size_t)nc_max * max_mid_cs_ * R);
   // fp8: e4m3 copies of IR block inputs (the e4m3 expand's operand), written by the previous block's SE GEMM
-  // (y8) or converted; zeroed once so the pad bytes past cs_in (never written) stay finite
+  // (y8) or converted (the expand reads no byte past cs_in of a row)
   const size_t x8b = effnet_x8(H, W);
   uint8_t* X8[2] = {x8b ? ws.take<uint8_t>((size_t)nc_max * x8b) : nullptr, x8b ? ws.take<uint8_t>((size_t)nc_max * x8b) : nullptr};
-  if (x8b) {
-    M2S_HIP(hipMemsetAsync(X8[0], 0, (size_t)nc_max * x8b, s));
-    M2S_HIP(hipMemsetAsync(X8[1], 0, (size_t)nc_max * x8b, s));
-  }
 
   for (int n0 = 0; n0 < N; n0 += nc_max) {
     const int nc = std::min(nc_max, N - n0);

@@ -94,7 +94,7 @@ class Acoustic {
   bool ir_fused_ = true;  // bf16: fused conv_pw + conv_dw + SE squeeze (env M2S_IR_FUSED=0 disables)
   bool ir_ws_ = true;     // split fp32: the persistent warp-specialised form of it (env M2S_IR_WS=0 disables)
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
-  bool f8_expand_ = false;       // fp8: the stride-1 IR expand on e4m3 (env M2S_F8_EXPAND=1; off: bf16 expand)
+  bool f8_expand_ = true;        // fp8: the stride-1 IR expand on e4m3 (env M2S_F8_EXPAND=0: bf16 expand)
   bool se_fused_ = true;    // bf16: SE excitation in one kernel (env M2S_SE_FUSED=0: two GEMMs)
   bool er_fused_ = true;    // bf16: EdgeResidual 32->128->32 in one kernel (env M2S_ER_FUSED=0 disables)
   bool se_sp_ = false;      // split: SE-gated conv_pwl on gemm128.hip (env M2S_SE_SP=1; default conv_gemm's in-LDS
