@@ -58,8 +58,8 @@ PRECISION = {
     "bf16": "bf16 storage and operands, fp32 accumulate; BiLSTM recurrence 3-term split products (B > 4), "
             "input projection/head/glue fp32",
     "fp8": "e4m3 storage + block-scaled e4m3 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, per-output-channel "
-           "weight scales) for the IR blocks' expanded maps and SE-gated conv_pwl GEMMs and the C=128/256 "
-           "MRF convs; the other convs (stem, EdgeResidual, IR expand/depthwise, C=32/64 MRF, upsamplers) "
+           "weight scales) for the stride-1 IR blocks' expand, expanded maps and SE-gated conv_pwl GEMMs and the "
+           "C=128/256 MRF convs; the other convs (stem, EdgeResidual, IR depthwise, C=32/64 MRF, upsamplers) "
            "bf16; BiLSTM recurrence 3-term split products (B > 4), input projection/head/glue fp32",
 }
 
@@ -76,7 +76,8 @@ def kernel_arith(name: str, dtype: str) -> str:
     if name.startswith("lstm_x3"):  # the split recurrence of every non-fp32 engine
         return "bf16x3"
     if dtype == "fp8":  # only the e4m3 kernels run fp8 MFMA; the rest of an fp8 engine is bf16
-        e4m3 = name.startswith(("gemm128_kernel<0", "gemm128_kernel<1")) or (name.startswith("se_ws_kernel") and "true" in name)
+        e4m3 = (name.startswith(("gemm128_kernel<0", "gemm128_kernel<1")) or (name.startswith("se_ws_kernel") and "true" in name)
+                or (name.startswith("ir_pwdw_kernel<") and name.rstrip(">").endswith(", 3")))  # the e4m3 expand
         return "fp8" if e4m3 else "bf16"
     return dtype
 
