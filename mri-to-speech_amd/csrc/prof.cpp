@@ -27,9 +27,9 @@ struct Prof {
       pool.pop_back();
       return e;
     }
-    // timing-only events: no system-scope fence when recorded (a default event writes back and invalidates
-    // the caches around every launch it brackets: the bench's event table then read ~11 % above rocprofv3's
-    // kernel durations, profiles/r04fin1_bench.json vs r04fin1_rocprof_kernel_stats.csv)
+    // timing-only events: no system-scope fence when recorded (no cache write-back / invalidate around the
+    // launches they bracket; the durations agree with rocprofv3's trace of the same steps either way,
+    // tools/step_kstats.py)
     hipEvent_t e;
     if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) M2S_HIP(hipEventCreate(&e));
     return e;
