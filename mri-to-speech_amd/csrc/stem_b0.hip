@@ -76,7 +76,13 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
   constexpr int SPIX = OFS + SH * SB_SW, APIX = OFS + AH * SB_AW;
   static_assert(APIX % 16 == 0 && (OFS + 2 * SB_AW) % 16 == 0, "A subtiles");
   constexpr int SPLANE = (SPIX * 16 + 255) / 256 * 256;      // bytes per S plane (4 planes)
-  constexpr int APLANE = (APIX * 16 + 255) / 256 * 256;      // bytes per A plane (2 planes)
+  // A: four planes of 4 channels (8 bytes a position) per set, plane p at a4(p): blocks.0.0's epilogue
+  // stores a 16-lane group's 16 positions as 128 contiguous bytes (with 8-channel planes the two halves
+  // of a position interleaved and every store was 2-way bank-conflicted: 0.29 conflict cycles per LDS
+  // instruction, profiles/r04ev2_sq_mfma.txt), and the plane offsets are 0 / 128 / 128 / 0 mod 256 bytes so
+  // the paired 8-byte reads of blocks.0.1 (planes 0 + 2, 1 + 3) and of the skip (0 + 1, 2 + 3) land on
+  // disjoint banks
+  constexpr int A4 = (APIX * 8 + 255) / 256 * 256;           // bytes per 4-channel A plane, a multiple of 256
   constexpr int ASUB = APIX / 16;                             // A position subtiles of a strip's first tile
   constexpr int ASUB0 = (OFS + 2 * SB_AW) / 16;               // first subtile of A row 2 (later tiles)
   constexpr int AMS = (ASUB + 3) / 4;                         // subtiles per wave, at most
@@ -85,8 +91,10 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
   static_assert(SB_SW == SB_AW, "S and A share the pitch");
   constexpr int R = SP ? 2 : 1;  // plane sets: hi (+ lo)
   __shared__ __attribute__((aligned(16))) char sS[R * 4 * SPLANE + 256];  // + the overrun of columns 18-19
-  __shared__ __attribute__((aligned(16))) char sA[R * 2 * APLANE];
-  constexpr int SLO = 4 * SPLANE, ALO = 2 * APLANE;  // offset of the lo plane set
+  constexpr int ALO = 4 * A4 + 256;                           // offset of the lo plane set
+  __shared__ __attribute__((aligned(16))) char sA[R * ALO];
+  constexpr int SLO = 4 * SPLANE;  // offset of the lo S plane set
+  auto a4 = [](int p) { return p * A4 + ((p == 1 || p == 2) ? 128 : 0); };
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -291,10 +299,10 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
             u.y = pack_bf16x2(v[2], v[3]);
           }
         }
-        const int ao = (g >> 1) * APLANE + pa * 16 + (g & 1) * 8;
+        const int ao = a4(g) + pa * 8;
         if (!first && pa >= OFS + SHIFT) {  // carry A rows 16, 17 -> 0, 1 before overwriting them
-          *reinterpret_cast<uint2*>(sA + ao - SHIFT * 16) = *reinterpret_cast<const uint2*>(sA + ao);
-          if constexpr (SP) *reinterpret_cast<uint2*>(sA + ALO + ao - SHIFT * 16) = *reinterpret_cast<const uint2*>(sA + ALO + ao);
+          *reinterpret_cast<uint2*>(sA + ao - SHIFT * 8) = *reinterpret_cast<const uint2*>(sA + ao);
+          if constexpr (SP) *reinterpret_cast<uint2*>(sA + ALO + ao - SHIFT * 8) = *reinterpret_cast<const uint2*>(sA + ALO + ao);
         }
         *reinterpret_cast<uint2*>(sA + ao) = u;
         if constexpr (SP) *reinterpret_cast<uint2*>(sA + ALO + ao) = ul;
@@ -308,13 +316,19 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
     {
       // K step st covers taps 2st (lanes g < 2) and 2st + 1 (g >= 2), 16 channels each; the pad tap
       // 9 (zero weights) reads tap 0's pixel so the product stays finite
+      // a lane's 8 channels 8 (g & 1) .. of its tap are planes 2 (g & 1) and 2 (g & 1) + 1: two 8-byte reads
       int toff[5];
 #pragma unroll
       for (int ks = 0; ks < 5; ++ks) {
         int k = 2 * ks + (g >> 1);
         if (k > 8) k = 0;
-        toff[ks] = ((k / 3) * SB_AW + (k % 3)) * 16 + (g & 1) * APLANE;
+        toff[ks] = ((k / 3) * SB_AW + (k % 3)) * 8 + a4(2 * (g & 1));
       }
+      const int pdel = a4(2 * (g & 1) + 1) - a4(2 * (g & 1));  // second plane of the pair
+      auto afrag = [&](const char* p) {
+        const uint2 lo = *reinterpret_cast<const uint2*>(p), hi = *reinterpret_cast<const uint2*>(p + pdel);
+        return __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      };
       f32x4 acc[OMS];
 #pragma unroll
       for (int i = 0; i < OMS; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -323,18 +337,18 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
 #pragma unroll
         for (int i = 0; i < OMS; ++i) {
           const int row = wave + 4 * i;  // output tile row = subtile
-          const char* p = sA + (OFS + row * SB_AW + r16) * 16 + toff[ks];
+          const char* p = sA + (OFS + row * SB_AW + r16) * 8 + toff[ks];
           if constexpr (SP)
-            acc[i] = mma3(wf1[ks], wl1[ks], frag(p), frag(p + ALO), acc[i]);
+            acc[i] = mma3(wf1[ks], wl1[ks], afrag(p), afrag(p + ALO), acc[i]);
           else
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[ks], frag(p), acc[i], 0, 0, 0);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[ks], afrag(p), acc[i], 0, 0, 0);
         }
       const int ox = tx0 + r16;
 #pragma unroll
       for (int i = 0; i < OMS; ++i) {
         const int row = wave + 4 * i, oy = ty0 + row;
         if (oy >= a.OH || ox >= a.OW) continue;
-        const int soff = (g >> 1) * APLANE + (OFS + (row + 1) * SB_AW + r16 + 1) * 16 + (g & 1) * 8;
+        const int soff = a4(g) + (OFS + (row + 1) * SB_AW + r16 + 1) * 8;
         float r[4];
         unpack_bf16x4(*reinterpret_cast<const uint2*>(sA + soff), r);
         if constexpr (SP) {
