@@ -1,0 +1,296 @@
+// Fused EdgeResidual block of the fp8 engines on e4m3 operands, stride 1 with skip, 32 -> 128 -> 32
+// channels (timm EdgeResidual conv_exp 3x3 + bn1 + SiLU -> conv_pwl 1x1 + bn2 -> + shortcut:
+// tf_efficientnetv2_b2 blocks.1.1/.2 at 64x64, built by mri_acoustic_model.py:28-34).
+//
+// er_fused.hip's dataflow (the 128-channel map never leaves the registers) on the block-scaled
+// v_mfma_scale_f32_16x16x128_f8f6f4 (unit E8M0 scales; K = 128 per instruction, 2x the bf16 rate):
+//   conv_exp: K = (tap, input channel) in groups of four taps, 3 MFMAs per (16 channels, 16 pixels)
+//     (taps 0-3, 4-7, 8 + three zero taps) instead of 9 bf16 ones.  A lane's 32 B of a B fragment are one
+//     tap's 32 input channels of one pixel: lane (r16, g) reads pixel (row + ky, r16 + kx) of tap 4q + g
+//     from an e4m3 copy of the haloed tile (two 16-channel planes, 16 B per pixel: a fragment read of 16
+//     consecutive pixels is bank-conflict free), or a zero slot for the padding taps.
+//   weights: e4m3 of W / s with s = amax / 448 per output channel (host), the epilogues multiply by s.
+//   conv_exp -> conv_pwl: a lane's accumulators hold channels 16 nt + 4 g + e (nt < 8, e < 4) of its
+//     pixel; after scale + bias + SiLU their 32 e4m3 bytes, in (nt, e) order, are the lane's B fragment of
+//     conv_pwl's single K = 128 step, with the host packing conv_pwl's K in the same permuted order
+//     (k-slot 32 g + 4 nt + e = mid channel 16 nt + 4 g + e).
+// Persistent workgroups (one per CU, 8 waves, wave w = output rows 2w, 2w + 1 of a 16 x 16 tile): the
+// e4m3 conv_exp fragments (48 KB) are DMA'd into LDS once; each tile's bf16 halo (18 x 18 x 32) lands by
+// LDS-DMA in one of two buffers while the previous tile computes, is converted once to the e4m3 planes,
+// and keeps serving the bf16 shortcut.  All LDS reads are inline asm consumed behind counted lgkmcnt waits
+// (a plain ds_read after an LDS-DMA makes hipcc drain the DMA in flight: the next tile's halo), the
+// conv_exp weight fragments three deep.
+#include <algorithm>
+
+#include "kernels.hpp"
+#include "prof.hpp"
+
+namespace m2s {
+namespace {
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int E8M0_ONE = 0x7f7f7f7f;
+
+__device__ __attribute__((aligned(16))) uint4 g_er8_zero[4];  // DMA source for padding pixels
+
+constexpr int E8_TW = 16, E8_HW = 18, E8_HPIX = E8_HW * E8_HW;  // tile width, halo width, 324 halo pixels
+constexpr int E8_PLANE = 384 * 16;                               // bf16 halo: 6 DMA pieces per 8-channel plane
+constexpr int E8_BUF = 4 * E8_PLANE;                             // 4 planes (24 KB)
+constexpr int E8_WEXP = 3 * 8 * 2 * 1024;                        // conv_exp fragments [q][nt][half][lane][16 B]
+constexpr int E8_P8 = 336 * 16;                                  // e4m3 plane: 16 channels x 324 pixels (+ pad)
+constexpr int E8_ZS = 2 * E8_P8;                                 // zero slot (32 B) after the two planes
+constexpr int E8_H8 = E8_ZS + 64;
+constexpr int E8_LDS = E8_WEXP + 2 * E8_BUF + E8_H8 + 2 * 128 * 4;  // + conv_exp scales and biases
+
+struct Er8Args {
+  const bf16_t* x;       // (N, H, W, 32)
+  const uint8_t* wexp;   // e4m3 [3][8][2][64][16]
+  const float* sexp;     // [128] conv_exp per-channel scales
+  const float* bexp;     // [128] bn1 bias
+  const uint8_t* wpwl;   // e4m3 [2][2][64][16] (permuted K)
+  const float* spwl;     // [32]
+  const float* bpwl;     // [32]
+  bf16_t* y;             // (N, H, W, 32)
+  int N, H, W, tiles_x, tiles_y;
+};
+
+__device__ __forceinline__ void dma16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, lds_wave_base, 16, 0, 0);
+}
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ i32x8 cat8(u32x4 a, u32x4 b) {
+  return i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+}
+
+__global__ void __launch_bounds__(512, 1) er8_fused_kernel(const Er8Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* wl = smem;                        // conv_exp fragments
+  char* hbuf = smem + E8_WEXP;            // two bf16 halo buffers
+  char* h8 = hbuf + 2 * E8_BUF;           // e4m3 halo planes + zero slot
+  float* sb = reinterpret_cast<float*>(h8 + E8_H8);  // [128] scales, [128] biases
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int tpi = a.tiles_x * a.tiles_y, ntiles = a.N * tpi;
+
+  // this wave's 3 halo pieces per tile: plane c, 64-pixel block pb (er_fused.hip's layout)
+  auto issue_halo = [&](int tile, char* buf) {
+    const int n = tile / tpi, tr = tile - n * tpi;
+    const int ty0 = (tr / a.tiles_x) * E8_TW - 1, tx0 = (tr - (tr / a.tiles_x) * a.tiles_x) * E8_TW - 1;
+    const bf16_t* xi = a.x + (size_t)n * a.H * a.W * 32;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int piece = wave * 3 + j, c = piece / 6, pb = piece - c * 6;
+      const int p = pb * 64 + lane, hy = p / E8_HW, hx = p - hy * E8_HW;
+      const int iy = ty0 + hy, ix = tx0 + hx;
+      const void* src = g_er8_zero;
+      if (p < E8_HPIX && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) src = xi + ((size_t)iy * a.W + ix) * 32 + c * 8;
+      dma16(src, buf + c * E8_PLANE + pb * 1024);
+    }
+  };
+
+  // ---- once: conv_exp fragments -> LDS (6 pieces per wave); conv_pwl fragments, its scales and biases ->
+  // VGPRs; conv_exp scales and biases -> LDS; the zero slot
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const int piece = wave * 6 + j;
+    dma16(a.wexp + (size_t)piece * 1024 + lane * 16, wl + piece * 1024);
+  }
+  i32x8 wp[2];
+#pragma unroll
+  for (int on = 0; on < 2; ++on) {
+    const u32x4 h0 = *reinterpret_cast<const u32x4*>(a.wpwl + ((size_t)(on * 2 + 0) * 64 + lane) * 16);
+    const u32x4 h1 = *reinterpret_cast<const u32x4*>(a.wpwl + ((size_t)(on * 2 + 1) * 64 + lane) * 16);
+    wp[on] = cat8(h0, h1);
+  }
+  float4 sp[2], bp[2];
+#pragma unroll
+  for (int on = 0; on < 2; ++on) {
+    sp[on] = *reinterpret_cast<const float4*>(a.spwl + on * 16 + 4 * g);
+    bp[on] = *reinterpret_cast<const float4*>(a.bpwl + on * 16 + 4 * g);
+  }
+  if (tid < 128) sb[tid] = a.sexp[tid];
+  else if (tid < 256) sb[tid] = a.bexp[tid - 128];
+  else if (tid < 260) *reinterpret_cast<uint4*>(h8 + E8_ZS + (tid - 256) * 16) = make_uint4(0u, 0u, 0u, 0u);
+  if ((int)blockIdx.x < ntiles) issue_halo(blockIdx.x, hbuf);
+  wait_vm<0>();
+  __syncthreads();
+
+  const uint32_t wl0 = lds_off(wl) + lane * 16, h80 = lds_off(h8), sb0 = lds_off(sb);
+  for (int it = 0, tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
+    char* hb = hbuf + (it & 1) * E8_BUF;
+    const uint32_t hb0 = lds_off(hb);
+    if (it > 0) {
+      wait_vm<4>();  // this tile's halo landed (the 4 younger ops are the last tile's stores)
+      __builtin_amdgcn_s_barrier();  // ... for every wave; every wave is done with h8 and the other buffer
+      asm volatile("" ::: "memory");
+    }
+    if (tile + (int)gridDim.x < ntiles) issue_halo(tile + gridDim.x, hbuf + ((it + 1) & 1) * E8_BUF);
+
+    // ---- the haloed tile as e4m3: item = (pixel, 16-channel plane), two bf16 planes -> 16 bytes --------
+    for (int w = tid; w < 2 * E8_HPIX; w += 512) {
+      const int px = w >> 1, pl = w & 1;
+      u32x4 u0, u1;
+      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(u0), "=&v"(u1)
+                   : "v"(hb0 + (2 * pl) * E8_PLANE + px * 16), "v"(hb0 + (2 * pl + 1) * E8_PLANE + px * 16)
+                   : "memory");
+      float f[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f[2 * j] = __uint_as_float(u0[j] << 16);
+        f[2 * j + 1] = __uint_as_float(u0[j] & 0xffff0000u);
+        f[8 + 2 * j] = __uint_as_float(u1[j] << 16);
+        f[8 + 2 * j + 1] = __uint_as_float(u1[j] & 0xffff0000u);
+      }
+      const uint2 q0 = e4m3x8(f), q1 = e4m3x8(f + 8);
+      const u32x4 q = {q0.x, q0.y, q1.x, q1.y};
+      asm volatile("ds_write_b128 %0, %1" ::"v"(h80 + pl * E8_P8 + px * 16), "v"(q) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    // ---- conv_exp: 2 rows x 16 pixels x 128 channels per wave; B fragments of all 3 tap groups first,
+    // then the 24 (q, nt) weight fragments three deep
+    u32x4 b0[2][3], b1[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int tap = 4 * q + g, ky = tap / 3, kx = tap - (tap / 3) * 3;
+        const int pix = (2 * wave + i + ky) * E8_HW + r16 + kx;
+        const uint32_t o0 = tap < 9 ? pix * 16 : E8_ZS, o1 = tap < 9 ? E8_P8 + pix * 16 : E8_ZS + 16;
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3"
+                     : "=&v"(b0[i][q]), "=&v"(b1[i][q])
+                     : "v"(h80 + o0), "v"(h80 + o1)
+                     : "memory");
+      }
+    u32x4 a0[3], a1[3];
+    auto read_a = [&](int f) {
+      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024"
+                   : "=&v"(a0[f % 3]), "=&v"(a1[f % 3])
+                   : "v"(wl0 + f * 2048)
+                   : "memory");
+    };
+    read_a(0);
+    read_a(1);
+    f32x4 acc[2][8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt) acc[i][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    i32x8 bx[2][3];
+#pragma unroll
+    for (int f = 0; f < 24; ++f) {
+      const int q = f / 8, nt = f % 8;
+      if (f + 2 < 24) read_a(f + 2);
+      // reads younger than A(f): A(f + 1), A(f + 2) (2 each, while issued)
+      if (f + 2 < 24) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(a0[f % 3]), "+v"(a1[f % 3]));
+      else if (f + 1 < 24) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(a0[f % 3]), "+v"(a1[f % 3]));
+      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0[f % 3]), "+v"(a1[f % 3]));
+      if (nt == 0) {  // the B reads were issued before every A read
+        asm volatile("" : "+v"(b0[0][q]), "+v"(b1[0][q]), "+v"(b0[1][q]), "+v"(b1[1][q]));
+        bx[0][q] = cat8(b0[0][q], b1[0][q]);
+        bx[1][q] = cat8(b0[1][q], b1[1][q]);
+      }
+      const i32x8 af = cat8(a0[f % 3], a1[f % 3]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        acc[i][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bx[i][q], acc[i][nt], 0, 0, 0, E8M0_ONE, 0,
+                                                                      E8M0_ONE);
+    }
+
+    // ---- scale + bias + SiLU -> e4m3 B fragment of conv_pwl (dword nt = channels 16 nt + 4 g + e) ----------
+    i32x8 mid[2];
+#pragma unroll
+    for (int nt = 0; nt < 8; nt += 2) {
+      u32x4 s0, s1, c0, c1;
+      asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:512\n\t"
+                   "ds_read_b128 %3, %4 offset:576\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(s0), "=&v"(s1), "=&v"(c0), "=&v"(c1)
+                   : "v"(sb0 + (nt * 16 + 4 * g) * 4)
+                   : "memory");
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = silu_e4m3(acc[i][nt][e] * __uint_as_float(s0[e]) + __uint_as_float(c0[e]));
+          v[4 + e] = silu_e4m3(acc[i][nt + 1][e] * __uint_as_float(s1[e]) + __uint_as_float(c1[e]));
+        }
+        const uint2 m = e4m3x8_nosat(v);
+        mid[i][nt] = (int)m.x;
+        mid[i][nt + 1] = (int)m.y;
+      }
+    }
+
+    // ---- conv_pwl (one K = 128 MFMA per 16 output channels) + scale + bn2 bias + shortcut ------------------
+    const int n = tile / tpi, tr = tile - n * tpi;
+    const int oy0 = (tr / a.tiles_x) * E8_TW, ox = (tr - (tr / a.tiles_x) * a.tiles_x) * E8_TW + r16;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ry = 2 * wave + i, oy = oy0 + ry;
+#pragma unroll
+      for (int on = 0; on < 2; ++on) {
+        const f32x4 o = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wp[on], mid[i], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0,
+                                                                         0, E8M0_ONE, 0, E8M0_ONE);
+        const int c4 = on * 16 + 4 * g;
+        uint2 r;
+        asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(r)
+                     : "v"(hb0 + (c4 >> 3) * E8_PLANE + ((ry + 1) * E8_HW + r16 + 1) * 16 + (c4 & 7) * 2)
+                     : "memory");
+        const float v0 = o[0] * sp[on].x + bp[on].x + __uint_as_float(r.x << 16);
+        const float v1 = o[1] * sp[on].y + bp[on].y + __uint_as_float(r.x & 0xffff0000u);
+        const float v2 = o[2] * sp[on].z + bp[on].z + __uint_as_float(r.y << 16);
+        const float v3 = o[3] * sp[on].w + bp[on].w + __uint_as_float(r.y & 0xffff0000u);
+        // every tile is whole (H, W multiples of 16): exactly 4 stores per wave per tile, which the counted
+        // wait at the top of the loop relies on
+        *reinterpret_cast<uint2*>(a.y + (((size_t)n * a.H + oy) * a.W + ox) * 32 + c4) =
+            make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+      }
+    }
+  }
+  wait_vm<0>();
+}
+
+}  // namespace
+
+bool er8_fused_supported(int H, int W, int cin, int mid, int cout) {
+  return cin == 32 && mid == 128 && cout == 32 && H % E8_TW == 0 && W % E8_TW == 0 && H > 0 && W > 0;
+}
+
+void launch_er8_fused(const bf16_t* x, int N, int H, int W, const uint8_t* wexp, const float* sexp, const float* bexp,
+                      const uint8_t* wpwl, const float* spwl, const float* bpwl, bf16_t* y, double flops, double bytes,
+                      hipStream_t s) {
+  M2S_CHECK(er8_fused_supported(H, W, 32, 128, 32) && N > 0, "er8_fused: unsupported shape");
+  Er8Args a;
+  a.x = x;
+  a.wexp = wexp;
+  a.sexp = sexp;
+  a.bexp = bexp;
+  a.wpwl = wpwl;
+  a.spwl = spwl;
+  a.bpwl = bpwl;
+  a.y = y;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.tiles_x = W / E8_TW;
+  a.tiles_y = H / E8_TW;
+  allow_lds(reinterpret_cast<const void*>(&er8_fused_kernel));
+  const int grid = std::min(N * a.tiles_x * a.tiles_y, device_cus());
+  ProfScope ps("er8_fused_kernel", flops, bytes, s);
+  hipLaunchKernelGGL(er8_fused_kernel, dim3(grid), dim3(512), E8_LDS, s, a);
+  M2S_HIP(hipGetLastError());
+}
+
+}  // namespace m2s

@@ -137,6 +137,14 @@ bool er_fused_supported(int H, int W, int cin, int mid, int cout, int kp_exp, in
 void launch_er_fused(const bf16_t* x, int N, int H, int W, const bf16_t* wexp, const float* bexp, const bf16_t* wpwl,
                      const float* bpwl, bf16_t* y, double flops, double bytes, hipStream_t s);
 
+// fp8 engines: er_fused's block on e4m3 operands (v_mfma_scale_f32_16x16x128_f8f6f4): wexp e4m3 [3][8][2][64][16]
+// (tap groups of four, per-channel scales sexp), wpwl e4m3 [2][2][64][16] (permuted K, scales spwl); x, y bf16
+// (N,H,W,32).  (er8_fused.hip)
+bool er8_fused_supported(int H, int W, int cin, int mid, int cout);
+void launch_er8_fused(const bf16_t* x, int N, int H, int W, const uint8_t* wexp, const float* sexp, const float* bexp,
+                      const uint8_t* wpwl, const float* spwl, const float* bpwl, bf16_t* y, double flops, double bytes,
+                      hipStream_t s);
+
 // bf16 EdgeResidual (stride 1, skip) 56 -> 224 -> 56 (channel strides 64 / 224 / 64): same fusion with the
 // weights streamed through an LDS ring; wst = er2_stage_elems() bf16 in the kernel's stage order.
 // (er2_fused.hip)

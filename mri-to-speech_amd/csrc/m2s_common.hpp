@@ -202,6 +202,17 @@ __device__ __forceinline__ uint2 e4m3x8(const float* v) {
   return make_uint2((uint32_t)q[0], (uint32_t)q[1]);
 }
 
+// 8 values already within +-448 (or NaN: kept) -> 8 e4m3
+__device__ __forceinline__ uint2 e4m3x8_nosat(const float* v) {
+  int q[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * h], v[4 * h + 1], 0, false);
+    q[h] = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * h + 2], v[4 * h + 3], r, true);
+  }
+  return make_uint2((uint32_t)q[0], (uint32_t)q[1]);
+}
+
 // bf16-path activations: one v_exp_f32 + one v_rcp_f32 (1 ulp) instead of an IEEE divide and
 // __expf's denormal-range fix-up (a compare + select + multiply per value); e^-x underflowing to
 // 0 or overflowing to inf gives silu = x or -0 as the exact function does.  These run in every
@@ -209,6 +220,9 @@ __device__ __forceinline__ uint2 e4m3x8(const float* v) {
 __device__ __forceinline__ float exp_neg(float x) { return __builtin_amdgcn_exp2f(x * -1.4426950408889634f); }
 __device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + exp_neg(x)); }
 __device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + exp_neg(x)); }
+// SiLU saturated for e4m3 (SiLU >= -0.28, so only the top needs the clamp): min(x, 448) * sigmoid(x), where a
+// NaN x still yields NaN through the sigmoid factor, so e4m3x8_nosat needs no NaN test (sat_e4m3's two ops)
+__device__ __forceinline__ float silu_e4m3(float x) { return fminf(x, 448.f) * __builtin_amdgcn_rcpf(1.0f + exp_neg(x)); }
 
 // Exact-libm variants used by the fp32 parity path (the reference runs fp32 libm on CPU).
 __device__ __forceinline__ float silu_exact(float x) { return x / (1.0f + expf(-x)); }

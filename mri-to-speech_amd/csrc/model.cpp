@@ -84,6 +84,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_IR_WS")) ir_ws_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_EXPAND")) f8_expand_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_F8_ER")) f8_er_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_FUSED")) se_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER_FUSED")) er_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_SP")) se_sp_ = std::strcmp(e, "0") != 0;  // A/B only
@@ -237,6 +238,48 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
           b.er_wexp = arena_.add_vec(fe);
           b.er_wpwl = arena_.add_vec(fp);
           b.er_frag = true;
+          if (dtype == M2S_DT_FP8) {
+            // er8_fused.hip: conv_exp [q][nt][half][lane][16 B], byte 16 half + j of lane (r16, g) = tap 4q + g
+            // (zero past tap 8), input channel 16 half + j of output channel 16 nt + r16; conv_pwl
+            // [on][half][lane][16 B], byte b = 4 nt + e of lane (r16, g) = mid channel 16 nt + 4 g + e
+            std::vector<float> s1(128, 1.f), s2(32, 1.f);
+            auto wexp_at = [&](int n, int c, int t) { return we[((size_t)n * cin + c) * 9 + t] * e1.a[n]; };
+            for (int n = 0; n < 128; ++n) {
+              float amax = 0.f;
+              for (int c = 0; c < 32; ++c)
+                for (int t = 0; t < 9; ++t) amax = std::max(amax, std::fabs(wexp_at(n, c, t)));
+              if (amax > 0.f) s1[n] = amax / 448.f;
+            }
+            for (int o = 0; o < 32; ++o) {
+              float amax = 0.f;
+              for (int c = 0; c < 128; ++c) amax = std::max(amax, std::fabs(wq[(size_t)o * b.mid + c] * e2.a[o]));
+              if (amax > 0.f) s2[o] = amax / 448.f;
+            }
+            std::vector<uint8_t> f8e((size_t)3 * 8 * 2 * 64 * 16, 0), f8p((size_t)2 * 2 * 64 * 16, 0);
+            for (int q4 = 0; q4 < 3; ++q4)
+              for (int nt = 0; nt < 8; ++nt)
+                for (int h = 0; h < 2; ++h)
+                  for (int ln = 0; ln < 64; ++ln)
+                    for (int j = 0; j < 16; ++j) {
+                      const int t = 4 * q4 + (ln >> 4), n = nt * 16 + (ln & 15), c = 16 * h + j;
+                      if (t < 9)
+                        f8e[((((size_t)q4 * 8 + nt) * 2 + h) * 64 + ln) * 16 + j] =
+                            e4m3_bits_host(e4m3_host(wexp_at(n, c, t) / s1[n]));
+                    }
+            for (int on = 0; on < 2; ++on)
+              for (int h = 0; h < 2; ++h)
+                for (int ln = 0; ln < 64; ++ln)
+                  for (int j = 0; j < 16; ++j) {
+                    const int o = on * 16 + (ln & 15), bb = 16 * h + j, c = 16 * (bb >> 2) + 4 * (ln >> 4) + (bb & 3);
+                    f8p[(((size_t)on * 2 + h) * 64 + ln) * 16 + j] =
+                        e4m3_bits_host(e4m3_host(wq[(size_t)o * b.mid + c] * e2.a[o] / s2[o]));
+                  }
+            b.er8_wexp = arena_.add_vec(f8e);
+            b.er8_sexp = arena_.add_vec(s1);
+            b.er8_wpwl = arena_.add_vec(f8p);
+            b.er8_spwl = arena_.add_vec(s2);
+            b.er8 = true;
+          }
         } else if (pdt == M2S_DT_BF16 && b.stride == 1 && b.skip && k == 3 &&
                    er2_fused_supported(32, 32, b.c1.cs_in, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
           // er2_fused.hip stage stream [20][16 pieces][lane][8]: stages 0..17 = conv_exp k-step s (tap
@@ -596,6 +639,14 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         launch_ers2_sp(cur, nc, oh, ow, nh, nw, qt, ql, b.c1.cs_in, b.mid, chan_stride(b.cout), arena_.ptr(b.er_wexp),
                        b.c1.b, arena_.ptr(b.er_wpwl), b.c2.b, nxt, 2.0 * px * b.mid * (9.0 * b.cin + b.cout),
                        4.0 * ((double)nc * oh * ow * b.c1.cs_in + px * chan_stride(b.cout)), s);
+      } else if (b.type == 1 && std::is_same<T, bf16_t>::value && er_fused_ && f8_er_ && b.er8 &&
+                 er8_fused_supported(nh, nw, b.cin, b.mid, b.cout)) {
+        const double px = (double)nc * nh * nw;
+        launch_er8_fused(reinterpret_cast<const bf16_t*>(cur), nc, nh, nw, static_cast<const uint8_t*>(arena_.ptr(b.er8_wexp)),
+                         static_cast<const float*>(arena_.ptr(b.er8_sexp)), b.c1.b,
+                         static_cast<const uint8_t*>(arena_.ptr(b.er8_wpwl)), static_cast<const float*>(arena_.ptr(b.er8_spwl)),
+                         b.c2.b, reinterpret_cast<bf16_t*>(nxt), 2.0 * px * b.mid * (9.0 * b.cin + b.cout),
+                         2.0 * px * (2.0 * b.cin) + (3.0 * 8 * 2048 + 2 * 2048), s);
       } else if (b.type == 1 && std::is_same<T, bf16_t>::value && er_fused_ && b.er_frag &&
                  er_fused_supported(nh, nw, b.cin, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
         const double px = (double)nc * nh * nw;

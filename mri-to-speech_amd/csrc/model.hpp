@@ -94,6 +94,7 @@ class Acoustic {
   bool ir_fused_ = true;  // bf16: fused conv_pw + conv_dw + SE squeeze (env M2S_IR_FUSED=0 disables)
   bool ir_ws_ = true;     // split fp32: the persistent warp-specialised form of it (env M2S_IR_WS=0 disables)
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
+  bool f8_er_ = true;            // fp8: EdgeResidual blocks.1.1/.2 on e4m3 (env M2S_F8_ER=0: bf16 er_fused)
   bool f8_expand_ = true;        // fp8: the stride-1 IR expand on e4m3 (env M2S_F8_EXPAND=0: bf16 expand)
   bool se_fused_ = true;    // bf16: SE excitation in one kernel (env M2S_SE_FUSED=0: two GEMMs)
   bool er_fused_ = true;    // bf16: EdgeResidual 32->128->32 in one kernel (env M2S_ER_FUSED=0 disables)
@@ -126,6 +127,9 @@ class Acoustic {
     PConv se1, se2;             // ir SE: conv_reduce (mid -> rd, SiLU), conv_expand (rd -> mid, sigmoid)
     size_t er_wexp = 0, er_wpwl = 0;  // bf16 er 32 -> 128 -> 32 stride 1: fused-kernel fragment orders
     bool er_frag = false;
+    // fp8 engines, er 32 -> 128 -> 32 stride 1 on e4m3 (er8_fused.hip): fragments, per-channel scales
+    size_t er8_wexp = 0, er8_sexp = 0, er8_wpwl = 0, er8_spwl = 0;
+    bool er8 = false;
     size_t er_sp_w = 0;  // split fp32 er stride 1: er_sp_fused.hip stage stream
     bool er_sp = false;
     bool ers_sp = false;  // split fp32 er stride 2 (blocks.1.0): er_wexp / er_wpwl in [hi/lo] fragment order

@@ -194,3 +194,32 @@ def test_fp8_e4m3_expand(rt, monkeypatch, n):
         cmin = min(_cos(f[i], ref[i]) for i in range(n))
         print(f"features vs oracle: min per-frame cos {cmin:.6f}")
         assert cmin >= 0.995
+
+
+@pytest.mark.parametrize("n", [5, 300])
+def test_fp8_e4m3_edge_residual(rt, monkeypatch, n):
+    """The fp8 engine's EdgeResidual blocks.1.1/.2 on e4m3 (er8_fused.hip: conv_exp 3x3 in tap groups of four
+    and conv_pwl on v_mfma_scale_f32_16x16x128_f8f6f4, per-channel-scaled e4m3 weights, the halo and the
+    128-channel map as e4m3) against the bf16 er_fused (M2S_F8_ER=0) and the fp32 oracle.  Two more e4m3
+    roundings per block, so the bars are cosines: the blocks' own outputs >= 0.995 and every later probed tap
+    >= 0.99 against the bf16 blocks, pooled features per frame >= 0.995 against the oracle (SURVEY.md §8(c):
+    0.99 end to end).  300 frames = 4800 tiles: the persistent loop's halo double buffer over many tiles."""
+    st = synth.synth_acoustic_state(8)
+    fr = torch.from_numpy(synth.synth_frames(1, n, seed=46)[0]).to(DEV)
+    monkeypatch.setenv("M2S_F8_ER", "1")
+    e8 = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    monkeypatch.setenv("M2S_F8_ER", "0")
+    eb = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    for i, bar in ((4, 0.995), (5, 0.995), (8, 0.99), (18, 0.99), (28, 0.99)):  # after 1.1, 1.2, 2.2, 4.5, 5.9
+        a, b = e8.probe(fr, i).cpu().numpy(), eb.probe(fr, i).cpu().numpy()
+        assert np.isfinite(a).all()
+        c = _cos(a.ravel(), b.ravel())
+        print(f"tap {i}: cos(e4m3 er, bf16 er) {c:.6f}")
+        assert c >= bar, (i, c)
+    if n == 5:
+        sd = {k: torch.from_numpy(v) for k, v in st.items()}
+        ref = effnet.effnet_gap(sd, fr.cpu()).numpy()
+        f = e8.effnet(fr).cpu().numpy()
+        cmin = min(_cos(f[i], ref[i]) for i in range(n))
+        print(f"features vs oracle: min per-frame cos {cmin:.6f}")
+        assert cmin >= 0.995
