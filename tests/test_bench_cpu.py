@@ -36,6 +36,8 @@ def test_roofline_picks_the_dominant_kernel_and_its_arithmetic():
     assert bench.kernel_arith("lstm_x3_kernel", "fp8") == "bf16x3"
     assert bench.kernel_arith("ir_pwdw_kernel<4, 1, 3>", "fp8") == "fp8"  # the e4m3 expand
     assert bench.kernel_arith("ir_pwdw_kernel<4, 1, 2>", "fp8") == "bf16"
+    assert bench.kernel_arith("er8_fused_kernel", "fp8") == "fp8"  # the e4m3 EdgeResidual
+    assert bench.kernel_arith("er_fused_kernel", "fp8") == "bf16"
     assert bench.kernel_arith("conv_igemm_kernel<float, 2, 4, 3>", "bf16") == "fp32"
     assert bench.PEAK_TFLOPS[bench.kernel_arith("conv_gemm_kernel<1>", "bf16x3")] == pytest.approx(2500.0 / 3)
     # fp8 engines: only the block-scaled e4m3 kernels (gemm128 KIND 0 / 1) are priced at the fp8 peak
