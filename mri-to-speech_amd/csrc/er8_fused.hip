@@ -50,7 +50,12 @@ constexpr int E8_WP8 = 4 * E8_HW * 16;                      // a wave's e4m3 pla
 constexpr int E8_W8 = 2 * E8_WP8;                           // two 16-channel planes per wave (2304 B)
 constexpr int E8_ZS = 8 * E8_W8;                            // zero slot (32 B) after the 8 waves' rows
 constexpr int E8_H8 = E8_ZS + 64;
-constexpr int E8_LDS = E8_WEXP + 4 * E8_BUF + E8_H8 + 2 * 128 * 4;  // + conv_exp scales and biases
+// with an e4m3 input from the producer (x8): [half][2] e4m3 halo buffers of two 16-channel planes instead
+constexpr int E8_P8 = 192 * 16;                             // e4m3 plane: 3 DMA pieces of 64 pixels
+constexpr int E8_XBUF = 2 * E8_P8;
+constexpr int E8_ZSX = 4 * E8_XBUF;
+constexpr int E8_H8X = E8_ZSX + 64;
+constexpr int e8_lds(bool x8) { return E8_WEXP + 4 * E8_BUF + (x8 ? E8_H8X : E8_H8) + 2 * 128 * 4; }  // + scales, biases
 
 struct Er8Args {
   const bf16_t* x;       // (N, H, W, 32)
@@ -61,6 +66,8 @@ struct Er8Args {
   const float* spwl;     // [32]
   const float* bpwl;     // [32]
   bf16_t* y;             // (N, H, W, 32)
+  const uint8_t* x8;     // X8: the input as e4m3 bytes (N, H, W, 32), written by the producer block
+  uint8_t* y8;           // Y8: e4m3 of the stored y (the next er8 block's x8)
   int N, H, W, tiles_x, tiles_y;  // 8 x 16 tiles
 };
 
@@ -78,12 +85,14 @@ __device__ __forceinline__ i32x8 cat8(u32x4 a, u32x4 b) {
   return i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
 }
 
+template <bool X8, bool Y8>
 __global__ void __launch_bounds__(512, 1) er8_fused_kernel(const Er8Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* wl = smem;                        // conv_exp fragments
   char* hbuf = smem + E8_WEXP;            // [half][2] bf16 halo buffers
-  char* h8 = hbuf + 4 * E8_BUF;           // per-wave e4m3 halo rows + zero slot
-  float* sb = reinterpret_cast<float*>(h8 + E8_H8);  // [128] scales, [128] biases
+  char* h8 = hbuf + 4 * E8_BUF;           // per-wave e4m3 halo rows (X8: [half][2] e4m3 halos) + zero slot
+  float* sb = reinterpret_cast<float*>(h8 + (X8 ? E8_H8X : E8_H8));  // [128] scales, [128] biases
+  constexpr int ZS = X8 ? E8_ZSX : E8_ZS;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int half = wave >> 2, lw = wave & 3;  // lw: output rows 2 lw, 2 lw + 1 of the half's tile
@@ -113,6 +122,21 @@ __global__ void __launch_bounds__(512, 1) er8_fused_kernel(const Er8Args a) {
     }
   };
   char* hb_half = hbuf + half * 2 * E8_BUF;
+  // X8: this wave's pieces (lw, lw + 4 < 6) of tile T's e4m3 halo: plane pl, 64-pixel block pb
+  auto issue_halo8 = [&](int T, char* buf) {
+    const int n = T / tpi, tr = T - n * tpi;
+    const int ty0 = (tr / a.tiles_x) * E8_TH - 1, tx0 = (tr - (tr / a.tiles_x) * a.tiles_x) * E8_TW - 1;
+    const uint8_t* xi = a.x8 + (size_t)n * a.H * a.W * 32;
+    for (int piece = lw; piece < 6; piece += 4) {
+      const int pl = piece / 3, pb = piece - pl * 3;
+      const int p = pb * 64 + lane, hy = p / E8_HW, hx = p - hy * E8_HW;
+      const int iy = ty0 + hy, ix = tx0 + hx;
+      const void* src = g_er8_zero;
+      if (p < E8_HPIX && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) src = xi + ((size_t)iy * a.W + ix) * 32 + pl * 16;
+      dma16(src, buf + pl * E8_P8 + pb * 1024);
+    }
+  };
+  char* x8_half = h8 + half * 2 * E8_XBUF;
 
   // ---- once: conv_exp fragments -> LDS (6 pieces per wave); conv_pwl fragments, its scales and biases ->
   // VGPRs; conv_exp scales and biases -> LDS; the zero slot; both halves' first halo
@@ -136,13 +160,14 @@ __global__ void __launch_bounds__(512, 1) er8_fused_kernel(const Er8Args a) {
   }
   if (tid < 128) sb[tid] = a.sexp[tid];
   else if (tid < 256) sb[tid] = a.bexp[tid - 128];
-  else if (tid < 260) *reinterpret_cast<uint4*>(h8 + E8_ZS + (tid - 256) * 16) = make_uint4(0u, 0u, 0u, 0u);
+  else if (tid < 260) *reinterpret_cast<uint4*>(h8 + ZS + (tid - 256) * 16) = make_uint4(0u, 0u, 0u, 0u);
   if (J > 0) issue_halo(tile_of(half, 0), hb_half);
+  if (X8 && J > 0) issue_halo8(tile_of(half, 0), x8_half);
   wait_vm<0>();
   __syncthreads();
 
   const uint32_t wl0 = lds_off(wl) + lane * 16, sb0 = lds_off(sb);
-  const uint32_t w80 = lds_off(h8) + wave * E8_W8, zs0 = lds_off(h8) + E8_ZS;
+  const uint32_t w80 = lds_off(h8) + wave * E8_W8, zs0 = lds_off(h8) + ZS;
   f32x4 acc[2][8];
   // phases: half 0 conv_exp(j) at 2 j, epilogue(j) at 2 j + 1; half 1 one phase later; J0 >= J (half 1)
   const int nphase = 2 * J0 + 1;
@@ -154,9 +179,11 @@ __global__ void __launch_bounds__(512, 1) er8_fused_kernel(const Er8Args a) {
       const uint32_t hb0 = lds_off(hb_half + (j & 1) * E8_BUF);
       if (j + 1 < J) issue_halo(tile_of(half, j + 1), hb_half + ((j + 1) & 1) * E8_BUF);  // its epilogue read
       // buffer (j + 1) & 1 last in phase p - 1
+      if (X8 && j + 1 < J) issue_halo8(tile_of(half, j + 1), x8_half + ((j + 1) & 1) * E8_XBUF);  // read in p - 2
+      const uint32_t xb0 = lds_off(x8_half + (j & 1) * E8_XBUF);
 
-      // this wave's halo rows 2 lw .. 2 lw + 3 as e4m3: item = (row, pixel, 16-channel plane)
-      for (int w = lane; w < 4 * E8_HW * 2; w += 64) {
+      // without x8: this wave's halo rows 2 lw .. 2 lw + 3 as e4m3: item = (row, pixel, 16-channel plane)
+      for (int w = lane; w < (X8 ? 0 : 4 * E8_HW * 2); w += 64) {
         const int pl = w & 1, rp = w >> 1;  // rp = local row * 18 + pixel
         const int hp = 2 * lw * E8_HW + rp;  // halo pixel
         u32x4 u0, u1;
@@ -185,8 +212,9 @@ __global__ void __launch_bounds__(512, 1) er8_fused_kernel(const Er8Args a) {
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
           const int tap = 4 * q + g, ky = tap / 3, kx = tap - (tap / 3) * 3;
-          const int rp = (i + ky) * E8_HW + r16 + kx;
-          const uint32_t o0 = tap < 9 ? w80 + rp * 16 : zs0, o1 = tap < 9 ? w80 + E8_WP8 + rp * 16 : zs0 + 16;
+          const int rp = (i + ky) * E8_HW + r16 + kx, hp = 2 * lw * E8_HW + rp;
+          const uint32_t b = X8 ? xb0 + hp * 16 : w80 + rp * 16, pl1 = X8 ? E8_P8 : E8_WP8;
+          const uint32_t o0 = tap < 9 ? b : zs0, o1 = tap < 9 ? b + pl1 : zs0 + 16;
           asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3" : "=&v"(b0[i][q]), "=&v"(b1[i][q]) : "v"(o0), "v"(o1) : "memory");
         }
       u32x4 a0[3], a1[3];
@@ -269,14 +297,17 @@ __global__ void __launch_bounds__(512, 1) er8_fused_kernel(const Er8Args a) {
           const float v1 = o[1] * sp[on].y + bp[on].y + __uint_as_float(r.x & 0xffff0000u);
           const float v2 = o[2] * sp[on].z + bp[on].z + __uint_as_float(r.y << 16);
           const float v3 = o[3] * sp[on].w + bp[on].w + __uint_as_float(r.y & 0xffff0000u);
-          // every tile is whole (H a multiple of 8, W of 16): exactly 4 stores per wave per tile
-          *reinterpret_cast<uint2*>(a.y + (((size_t)n * a.H + oy) * a.W + ox) * 32 + c4) =
-              make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+          // every tile is whole (H a multiple of 8, W of 16): exactly 4 stores (8 with y8) per wave per tile
+          const size_t px = ((size_t)n * a.H + oy) * a.W + ox;
+          const uint2 yb = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+          *reinterpret_cast<uint2*>(a.y + px * 32 + c4) = yb;
+          if (Y8) *reinterpret_cast<uint32_t*>(a.y8 + px * 32 + c4) = e4m3x4_bf16(yb);
         }
       }
-      // the next tile's halo (issued in the conv_exp phase of tile j, before these 4 stores) must have landed
+      // the next tile's halo (issued in the conv_exp phase of tile j, before these stores) must have landed
       // for every wave of the half by the next phase: the barrier below follows each wave's own wait
-      wait_vm<4>();
+      if (Y8) wait_vm<8>();
+      else wait_vm<4>();
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -292,7 +323,7 @@ bool er8_fused_supported(int H, int W, int cin, int mid, int cout) {
 
 void launch_er8_fused(const bf16_t* x, int N, int H, int W, const uint8_t* wexp, const float* sexp, const float* bexp,
                       const uint8_t* wpwl, const float* spwl, const float* bpwl, bf16_t* y, double flops, double bytes,
-                      hipStream_t s) {
+                      hipStream_t s, const uint8_t* x8, uint8_t* y8) {
   M2S_CHECK(er8_fused_supported(H, W, 32, 128, 32) && N > 0, "er8_fused: unsupported shape");
   Er8Args a;
   a.x = x;
@@ -303,16 +334,20 @@ void launch_er8_fused(const bf16_t* x, int N, int H, int W, const uint8_t* wexp,
   a.spwl = spwl;
   a.bpwl = bpwl;
   a.y = y;
+  a.x8 = x8;
+  a.y8 = y8;
   a.N = N;
   a.H = H;
   a.W = W;
   a.tiles_x = W / E8_TW;
   a.tiles_y = H / E8_TH;
-  allow_lds(reinterpret_cast<const void*>(&er8_fused_kernel));
+  M2S_CHECK(x8 || !y8, "er8_fused: an e4m3 output needs the e4m3 input path");
+  auto k = x8 ? (y8 ? er8_fused_kernel<true, true> : er8_fused_kernel<true, false>) : er8_fused_kernel<false, false>;
+  allow_lds(reinterpret_cast<const void*>(k));
   // two tiles per workgroup in flight (one per half)
   const int grid = std::min((N * a.tiles_x * a.tiles_y + 1) / 2, device_cus());
-  ProfScope ps("er8_fused_kernel", flops, bytes, s);
-  hipLaunchKernelGGL(er8_fused_kernel, dim3(grid), dim3(512), E8_LDS, s, a);
+  ProfScope ps("er8_fused_kernel", flops, bytes + (x8 ? N * (double)H * W * 32 : 0.0) + (y8 ? N * (double)H * W * 32 : 0.0), s);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(512), e8_lds(x8 != nullptr), s, a);
   M2S_HIP(hipGetLastError());
 }
 

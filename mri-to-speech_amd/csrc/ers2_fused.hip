@@ -36,6 +36,8 @@ struct Es2Args {
   const bf16_t* wpwl;  // [CO / 16][MID / 32][64][8], permuted K
   const float* bpwl;   // [CO] (zero past cout)
   bf16_t* y;           // (N, OH, OW, CO)
+  uint8_t* y8;         // bf16 kernel, fp8 engines: e4m3 of the stored y, (N, OH, OW, CO) bytes (the next
+                       // block's er8_fused operand), or null
   int N, H, W, OH, OW, pad_t, pad_l, tiles_x, tiles_y;
 };
 
@@ -102,7 +104,8 @@ __global__ void __launch_bounds__(512, (CIN == 16 ? 2 : 1)) ers2_fused_kernel(co
   for (int it = 0, tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
     char* hb = hbuf + (it & 1) * BUF;
     if (it > 0) {
-      wait_vm<ON>();  // this tile's halo landed (the ON younger ops are the last tile's stores)
+      if (a.y8) wait_vm<2 * ON>();  // this tile's halo landed (the younger ops are the last tile's stores)
+      else wait_vm<ON>();
       __builtin_amdgcn_s_barrier();  // ... for every wave; every wave is done with the other buffer
       asm volatile("" ::: "memory");  // (a raw barrier: __syncthreads would also wait for the stores)
     }
@@ -145,14 +148,16 @@ __global__ void __launch_bounds__(512, (CIN == 16 ? 2 : 1)) ers2_fused_kernel(co
     }
     const int n = tile / tpi, tr = tile - n * tpi, ty = tr / a.tiles_x, tx = tr - ty * a.tiles_x;
     const int oy = ty * ES_TH + wave, ox = tx * ES_TW + r16;
-    // every tile is whole (OH % 8 == 0, OW % 16 == 0): exactly ON stores per wave per tile, which
-    // the counted wait at the top of the loop relies on
+    // every tile is whole (OH % 8 == 0, OW % 16 == 0): exactly ON stores (2 ON with y8) per wave per
+    // tile, which the counted wait at the top of the loop relies on
 #pragma unroll
     for (int on = 0; on < ON; ++on) {
       const int c4 = on * 16 + 4 * g;
-      *reinterpret_cast<uint2*>(a.y + (((size_t)n * a.OH + oy) * a.OW + ox) * CO + c4) =
-          make_uint2(pack_bf16x2(o[on][0] + bp[on].x, o[on][1] + bp[on].y),
-                     pack_bf16x2(o[on][2] + bp[on].z, o[on][3] + bp[on].w));
+      const size_t px = ((size_t)n * a.OH + oy) * a.OW + ox;
+      const uint2 yb = make_uint2(pack_bf16x2(o[on][0] + bp[on].x, o[on][1] + bp[on].y),
+                                  pack_bf16x2(o[on][2] + bp[on].z, o[on][3] + bp[on].w));
+      *reinterpret_cast<uint2*>(a.y + px * CO + c4) = yb;
+      if (a.y8) *reinterpret_cast<uint32_t*>(a.y8 + px * CO + c4) = e4m3x4_bf16(yb);
     }
   }
   wait_vm<0>();
@@ -344,6 +349,7 @@ void launch_ers2_sp(const void* x, int N, int H, int W, int OH, int OW, int pad_
   a.wpwl = static_cast<const bf16_t*>(wpwl);
   a.bpwl = bpwl;
   a.y = static_cast<bf16_t*>(y);
+  a.y8 = nullptr;
   a.N = N;
   a.H = H;
   a.W = W;
@@ -358,7 +364,7 @@ void launch_ers2_sp(const void* x, int N, int H, int W, int OH, int OW, int pad_
 
 void launch_ers2_fused(const bf16_t* x, int N, int H, int W, int OH, int OW, int pad_t, int pad_l, int cs_in, int mid,
                        int cs_out, const bf16_t* wexp, const float* bexp, const bf16_t* wpwl, const float* bpwl,
-                       bf16_t* y, double flops, double bytes, hipStream_t s) {
+                       bf16_t* y, double flops, double bytes, hipStream_t s, uint8_t* y8) {
   M2S_CHECK(N > 0 && ers2_fused_supported(OH, OW, cs_in, mid, cs_out, 9 * cs_in, mid), "ers2_fused: unsupported shape");
   Es2Args a;
   a.x = x;
@@ -367,6 +373,7 @@ void launch_ers2_fused(const bf16_t* x, int N, int H, int W, int OH, int OW, int
   a.wpwl = wpwl;
   a.bpwl = bpwl;
   a.y = y;
+  a.y8 = y8;
   a.N = N;
   a.H = H;
   a.W = W;

@@ -139,11 +139,12 @@ void launch_er_fused(const bf16_t* x, int N, int H, int W, const bf16_t* wexp, c
 
 // fp8 engines: er_fused's block on e4m3 operands (v_mfma_scale_f32_16x16x128_f8f6f4): wexp e4m3 [3][8][2][64][16]
 // (tap groups of four, per-channel scales sexp), wpwl e4m3 [2][2][64][16] (permuted K, scales spwl); x, y bf16
-// (N,H,W,32).  (er8_fused.hip)
+// (N,H,W,32); x8 (optional): the input as e4m3 bytes (N,H,W,32) from the producer (ers2_fused / er8_fused y8),
+// y8 (optional, needs x8): e4m3 bytes of y for the next er8 block.  (er8_fused.hip)
 bool er8_fused_supported(int H, int W, int cin, int mid, int cout);
 void launch_er8_fused(const bf16_t* x, int N, int H, int W, const uint8_t* wexp, const float* sexp, const float* bexp,
                       const uint8_t* wpwl, const float* spwl, const float* bpwl, bf16_t* y, double flops, double bytes,
-                      hipStream_t s);
+                      hipStream_t s, const uint8_t* x8 = nullptr, uint8_t* y8 = nullptr);
 
 // bf16 EdgeResidual (stride 1, skip) 56 -> 224 -> 56 (channel strides 64 / 224 / 64): same fusion with the
 // weights streamed through an LDS ring; wst = er2_stage_elems() bf16 in the kernel's stage order.
@@ -176,7 +177,7 @@ void launch_ers2_sp(const void* x, int N, int H, int W, int OH, int OW, int pad_
                     double flops, double bytes, hipStream_t s);
 void launch_ers2_fused(const bf16_t* x, int N, int H, int W, int OH, int OW, int pad_t, int pad_l, int cs_in, int mid,
                        int cs_out, const bf16_t* wexp, const float* bexp, const bf16_t* wpwl, const float* bpwl,
-                       bf16_t* y, double flops, double bytes, hipStream_t s);
+                       bf16_t* y, double flops, double bytes, hipStream_t s, uint8_t* y8 = nullptr);
 
 // Decoded frames -> model input: uint8 (N,H,W) grey or (N,H,W,3) BGR -> fp32 (N,H,W) in [0, 1]
 // (_preprocess_frame, run_mri_video_inference.py:34-54, minus the host-side resize).  (preprocess.hip)

@@ -213,6 +213,15 @@ __device__ __forceinline__ uint2 e4m3x8_nosat(const float* v) {
   return make_uint2((uint32_t)q[0], (uint32_t)q[1]);
 }
 
+// 4 bf16 (a uint2 as stored) -> 4 e4m3 (saturated as sat_e4m3: NaN kept), the same bytes er8_fused's own
+// conversion of a bf16 operand gives
+__device__ __forceinline__ uint32_t e4m3x4_bf16(uint2 u) {
+  const int r = __builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(__uint_as_float(u.x << 16)),
+                                                sat_e4m3(__uint_as_float(u.x & 0xffff0000u)), 0, false);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(__uint_as_float(u.y << 16)),
+                                                   sat_e4m3(__uint_as_float(u.y & 0xffff0000u)), r, true);
+}
+
 // bf16-path activations: one v_exp_f32 + one v_rcp_f32 (1 ulp) instead of an IEEE divide and
 // __expf's denormal-range fix-up (a compare + select + multiply per value); e^-x underflowing to
 // 0 or overflowing to inf gives silu = x or -0 as the exact function does.  These run in every

@@ -85,6 +85,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_EXPAND")) f8_expand_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_ER")) f8_er_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_ER8_X8")) er8_x8_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_FUSED")) se_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER_FUSED")) er_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_SP")) se_sp_ = std::strcmp(e, "0") != 0;  // A/B only
@@ -480,7 +481,7 @@ void Acoustic::effnet_dims(int H, int W, size_t* io, size_t* mid, size_t* se) co
 }
 
 size_t Acoustic::effnet_x8(int H, int W) const {
-  if (dtype_ != M2S_DT_FP8 || !f8_expand_) return 0;
+  if (dtype_ != M2S_DT_FP8 || (!f8_expand_ && !f8_er_)) return 0;
   int oh, ow, ph, pw;
   same_pad(H, 3, 2, &oh, &ph);
   same_pad(W, 3, 2, &ow, &pw);
@@ -489,7 +490,8 @@ size_t Acoustic::effnet_x8(int H, int W) const {
     int nh, nw;
     same_pad(oh, 3, b.stride, &nh, &ph);
     same_pad(ow, 3, b.stride, &nw, &pw);
-    if (b.f8_pw) mx = std::max(mx, (size_t)nh * nw * b.f8x_kp);  // stride 1: the block input's map
+    if (b.f8_pw && f8_expand_) mx = std::max(mx, (size_t)nh * nw * b.f8x_kp);  // stride 1: the block input's map
+    if (b.er8 && f8_er_) mx = std::max(mx, (size_t)nh * nw * 32);              // er8_fused x8 / y8 (N, H, W, 32)
     oh = nh;
     ow = nw;
   }
@@ -606,7 +608,10 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
       const Block& b = blocks_[k];
       uint8_t* next8 = nullptr;  // the e4m3 copy of this block's output, if its SE GEMM wrote one
       // the next block takes an e4m3 expand operand (fp8 engines, stride-1 IR blocks)
-      const bool want8 = X8[0] && k + 1 < blocks_.size() && blocks_[k + 1].f8_pw && blocks_[k + 1].stride == 1;
+      const bool want8 = X8[0] && f8_expand_ && k + 1 < blocks_.size() && blocks_[k + 1].f8_pw && blocks_[k + 1].stride == 1;
+      // the next block is an e4m3 EdgeResidual (er8_fused): this block also stores its output as e4m3 bytes
+      uint8_t* const er8_next = X8[0] && f8_er_ && er8_x8_ && k + 1 < blocks_.size() && blocks_[k + 1].er8 ? (cur8 == X8[0] ? X8[1] : X8[0])
+                                                                                              : nullptr;
       int nh, nw, qt, ql;
       same_pad(oh, 3, b.stride, &nh, &qt);
       same_pad(ow, 3, b.stride, &nw, &ql);
@@ -642,11 +647,13 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
       } else if (b.type == 1 && std::is_same<T, bf16_t>::value && er_fused_ && f8_er_ && b.er8 &&
                  er8_fused_supported(nh, nw, b.cin, b.mid, b.cout)) {
         const double px = (double)nc * nh * nw;
+        uint8_t* y8 = cur8 && er8_next && er8_fused_supported(nh, nw, b.cout, b.mid, b.cout) ? er8_next : nullptr;
         launch_er8_fused(reinterpret_cast<const bf16_t*>(cur), nc, nh, nw, static_cast<const uint8_t*>(arena_.ptr(b.er8_wexp)),
                          static_cast<const float*>(arena_.ptr(b.er8_sexp)), b.c1.b,
                          static_cast<const uint8_t*>(arena_.ptr(b.er8_wpwl)), static_cast<const float*>(arena_.ptr(b.er8_spwl)),
                          b.c2.b, reinterpret_cast<bf16_t*>(nxt), 2.0 * px * b.mid * (9.0 * b.cin + b.cout),
-                         2.0 * px * (2.0 * b.cin) + (3.0 * 8 * 2048 + 2 * 2048), s);
+                         2.0 * px * (2.0 * b.cin) + (3.0 * 8 * 2048 + 2 * 2048), s, cur8, y8);
+        next8 = y8;
       } else if (b.type == 1 && std::is_same<T, bf16_t>::value && er_fused_ && b.er_frag &&
                  er_fused_supported(nh, nw, b.cin, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
         const double px = (double)nc * nh * nw;
@@ -663,11 +670,14 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
       } else if (b.type == 1 && std::is_same<T, bf16_t>::value && er_fused_ && b.er_frag && b.stride == 2 &&
                  ers2_fused_supported(nh, nw, b.c1.cs_in, b.mid, chan_stride(b.cout), b.c1.kp, b.c2.kp)) {
         const double px = (double)nc * nh * nw;
+        // fp8: an e4m3 copy of the output for an er8_fused next block (the copy is (N, OH, OW, cs_out) bytes)
+        uint8_t* y8 = er8_next && chan_stride(b.cout) == 32 && er8_fused_supported(nh, nw, 32, 128, 32) ? er8_next : nullptr;
         launch_ers2_fused(reinterpret_cast<const bf16_t*>(cur), nc, oh, ow, nh, nw, qt, ql, b.c1.cs_in, b.mid,
                           chan_stride(b.cout), static_cast<const bf16_t*>(arena_.ptr(b.er_wexp)), b.c1.b,
                           static_cast<const bf16_t*>(arena_.ptr(b.er_wpwl)), b.c2.b, reinterpret_cast<bf16_t*>(nxt),
                           2.0 * px * b.mid * (9.0 * b.cin + b.cout),
-                          2.0 * ((double)nc * oh * ow * b.c1.cs_in + px * chan_stride(b.cout)), s);
+                          2.0 * ((double)nc * oh * ow * b.c1.cs_in + px * chan_stride(b.cout)) + (y8 ? px * 32 : 0.0), s, y8);
+        next8 = y8;
       } else if (b.type == 1) {
         ConvArgs a = a2d(b.c1, cur, M);
         a.act = ACT_SILU;
@@ -694,7 +704,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         } else if (FUSABLE && b.stride == 1 && ir_fused_ && ir_fused_supported(nh, nw, b.c1.cs_in, cs, SPL)) {
           const double P = (double)nh * nw, es = SPL ? 4.0 : 2.0;
           f8 = b.f8_pwl && se_gemm_f8_supported(nh * nw, cs, chan_stride(b.cout));
-          const bool f8x = f8 && b.f8_pw && X8[0];  // the expand on e4m3 (x8 of the block input)
+          const bool f8x = f8 && f8_expand_ && b.f8_pw && X8[0];  // the expand on e4m3 (x8 of the block input)
           if (f8x && !cur8) {  // no e4m3 producer wrote this input: convert it
             cur8 = X8[0];
             launch_rows_e4m3(cur, (long)nc * nh * nw, b.c1.cs_in, cur8, b.f8x_kp, s);

@@ -95,6 +95,8 @@ class Acoustic {
   bool ir_ws_ = true;     // split fp32: the persistent warp-specialised form of it (env M2S_IR_WS=0 disables)
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
   bool f8_er_ = true;            // fp8: EdgeResidual blocks.1.1/.2 on e4m3 (env M2S_F8_ER=0: bf16 er_fused)
+  bool er8_x8_ = true;           // ... their input as e4m3 bytes from the producer (env M2S_ER8_X8=0: converted
+                                 // in er8_fused; the same bytes, test_fp8_er8_e4m3_handoff_is_exact)
   bool f8_expand_ = true;        // fp8: the stride-1 IR expand on e4m3 (env M2S_F8_EXPAND=0: bf16 expand)
   bool se_fused_ = true;    // bf16: SE excitation in one kernel (env M2S_SE_FUSED=0: two GEMMs)
   bool er_fused_ = true;    // bf16: EdgeResidual 32->128->32 in one kernel (env M2S_ER_FUSED=0 disables)

@@ -223,3 +223,18 @@ def test_fp8_e4m3_edge_residual(rt, monkeypatch, n):
         cmin = min(_cos(f[i], ref[i]) for i in range(n))
         print(f"features vs oracle: min per-frame cos {cmin:.6f}")
         assert cmin >= 0.995
+
+
+def test_fp8_er8_e4m3_handoff_is_exact(rt, monkeypatch):
+    """blocks.1.0 (ers2_fused) and blocks.1.1 (er8_fused) store their outputs' e4m3 bytes for the next er8 block
+    (y8 -> x8), which then DMAs them instead of converting its bf16 input in the kernel (M2S_ER8_X8=0): the
+    same bytes (e4m3 of the stored bf16 values, NaN kept), so the two paths agree bit for bit."""
+    st = synth.synth_acoustic_state(8)
+    fr = torch.from_numpy(synth.synth_frames(1, 37, seed=47)[0]).to(DEV)
+    monkeypatch.setenv("M2S_ER8_X8", "1")
+    ex = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    monkeypatch.setenv("M2S_ER8_X8", "0")
+    ec = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    for i in (4, 5, 8):
+        assert torch.equal(ex.probe(fr, i), ec.probe(fr, i)), i
+    assert torch.equal(ex.effnet(fr), ec.effnet(fr))
