@@ -484,7 +484,11 @@ void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_p
       case 1: return launch_cfg<4, 2, 4, 2, 3, 1>(a, s, flops, bytes);  // 256 x 128, 3 slots, 1 step in flight
       case 2: return launch_cfg<2, 2, 4, 4, 4, 2>(a, s, flops, bytes);  // 128 x 128, 4 slots, 2 in flight
       case 3: return launch_cfg<2, 2, 4, 4, 4, 1>(a, s, flops, bytes);  // 128 x 128, 4 slots, 1 in flight
-      default: return launch_cfg<4, 2, 4, 4, 3, 2>(a, s, flops, bytes);  // 256 x 128 (one 16x16 image), 3 slots
+      case 4: return launch_cfg<4, 2, 4, 4, 3, 2>(a, s, flops, bytes);  // 256 x 128, 8 consumers 64 x 64 each
+      // 256 x 128 (one 16x16 image), 3 slots, 4 consumers of 64 rows x all 128 columns: each activation
+      // fragment is gated and re-split by one wave instead of two (the 8-consumer 64 x 64 form above):
+      // 408 -> 389 us per launch, same-box per-process A/B (profiles/r04_se_ws_wn1_kstats.txt)
+      default: return launch_cfg<4, 1, 8, 4, 3, 2>(a, s, flops, bytes);
     }
   } else {
     M2S_CHECK(n_pad >= 224, "se_ws: weight rows");

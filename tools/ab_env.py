@@ -32,7 +32,7 @@ def timed(fn, n=10):
 
 for dt in dtypes:
     engs = {}
-    for v in ("1", "0"):
+    for v in os.environ.get("AB_VALUES", "1,0").split(","):  # e.g. AB_VALUES=4,0 for a config switch
         os.environ[var] = v
         engs[v] = rt.AcousticEngine(st, dtype=dt, device=dev)
     for rnd in range(2):
