@@ -131,6 +131,13 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) er_sp_kernel(const E
 #pragma unroll
   for (int on = 0; on < ON; ++on) bp[on] = *reinterpret_cast<const float4*>(a.bpwl + on * 16 + 4 * g);
 
+#ifndef ERSP_PRIO
+#define ERSP_PRIO 1
+#endif
+  // the second-dispatched half of the waves loses every VALU issue arbitration to the first by age; one
+  // static priority for it evens the halves' segments out (MI355X_MICROARCH.md, two waves per SIMD, item 4):
+  // same-box A/B -1.7 % on the 16-row blocks.1 form, neutral on blocks.2 (profiles/r04_prio_kstats.txt)
+  if (ERSP_PRIO && NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
   int q = 0;  // global stage counter: ring slot = q % 3
   if ((int)blockIdx.x < ntiles) {
     stage_dma(0, 0);

@@ -184,6 +184,11 @@ __global__ void __launch_bounds__(512, 1) ers2_sp_kernel(const Es2Args a) {
   char* hbuf = smem + WEXP;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifndef ERS2_PRIO
+#define ERS2_PRIO 1
+#endif
+  // the younger half at static priority (er_sp_fused.hip): same-box A/B -2 %
+  if (ERS2_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int g = lane >> 4, r16 = lane & 15;
   const int tpi = a.tiles_x * a.tiles_y, ntiles = a.N * tpi;
 

@@ -244,6 +244,11 @@ __global__ void __launch_bounds__(RB_NW * 64) rb1_fused_kernel(const RbArgs a) {
   char* bufT = bufA + HR * NPL * PLANE;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifndef RB1_PRIO
+#define RB1_PRIO 1
+#endif
+  // the younger half at static priority (er_sp_fused.hip): same-box A/B -3 % / -1 % at k = 11 / 7, +7 % at k = 3
+  if (RB1_PRIO && RB_NW == 8 && K >= 7 && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int g = lane >> 4, r16 = lane & 15;
   const int clip = blockIdx.x / a.tiles, tile = blockIdx.x - clip * a.tiles;
   const int t0 = tile * TOUT - a.H;  // time of row 0
