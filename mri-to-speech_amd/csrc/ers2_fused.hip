@@ -65,6 +65,12 @@ __global__ void __launch_bounds__(512, (CIN == 16 ? 2 : 1)) ers2_fused_kernel(co
   char* hbuf = smem + WEXP;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifndef ERB_PRIO
+#define ERB_PRIO 1
+#endif
+  // the younger half at static priority (er_sp_fused.hip): configs[4] bf16 A/B -4 % (CIN 16) / -1 % (CIN 32);
+  // er_fused / er2_fused measured -0.4 % / +1 % that way and do not take it (profiles/r04_prio_kstats.txt)
+  if (ERB_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int g = lane >> 4, r16 = lane & 15;
   const int tpi = a.tiles_x * a.tiles_y, ntiles = a.N * tpi;
 

@@ -8,7 +8,7 @@ export TMPDIR=/tmp AB_SHAPE=8x1000
 mkdir -p "gpurun_out/$TAG"
 for dt in "$@"; do
   (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$ROOT/gpurun_out/$TAG/$dt" -o run -- \
-    python3 "$ROOT/tools/ab_step.py" --child mri-to-speech_amd "$dt") > "gpurun_out/$TAG/$dt.log" 2>&1 || exit $?
+    python3 "$ROOT/tools/ab_step.py" --child "${PKG:-mri-to-speech_amd}" "$dt") > "gpurun_out/$TAG/$dt.log" 2>&1 || exit $?
   f=$(find "gpurun_out/$TAG/$dt" -name run_kernel_trace.csv)
   python3 tools/trace_sum.py "$f" 4 > "gpurun_out/$TAG/$dt.sum.txt" || exit $?
   rm -f "$f"
