@@ -39,10 +39,13 @@
 extern "C" {
 #endif
 
-#define M2S_ABI_VERSION 4
+#define M2S_ABI_VERSION 5
 
 enum m2s_status { M2S_OK = 0, M2S_E_ARG = 1, M2S_E_HIP = 2, M2S_E_STATE = 3, M2S_E_NODEV = 4, M2S_E_INTERNAL = 5 };
-/* compute dtype of the convolution stacks (BiLSTM, head and glue always run in fp32):
+/* compute dtype of the convolution stacks.  The BiLSTM input projection, head and glue run in fp32 in every
+ * dtype; the BiLSTM recurrence runs exact-f32 products in M2S_DT_F32 and for B <= 4 (lstm_small_kernel), and
+ * split three-term bf16x3 products (W_hh and h_t as hi + lo bf16 pairs, fp32 cell state and gates;
+ * lstm_x3_kernel) for B > 4 in the BF16, BF16X3 and FP8 engines:
  *   M2S_DT_F32    exact f32 MFMA products (v_mfma_f32_16x16x4_f32), fp32 storage
  *   M2S_DT_BF16   bf16 storage and operands, fp32 accumulation
  *   M2S_DT_BF16X3 split fp32: every activation / weight is a bf16 pair hi + lo (17 significant
@@ -204,6 +207,19 @@ typedef struct m2s_prof_stat {
 int m2s_prof_enable(int on);
 /* Synchronises on the recorded events, writes up to `max` stats, clears the record. */
 int m2s_prof_collect(m2s_prof_stat* out, int max, int* n_out);
+/* One recorded launch, in launch order: its kernel name, the stage of the path it belongs to
+ * ("cnn", "bilstm", "head", "glue", "voc_pre", "ups_c<C>", "mrf_c<C>", "voc_post"; bench.py's
+ * roofline.stages), event time, algorithmic FLOPs and bytes. */
+typedef struct m2s_prof_launch {
+  char name[96];
+  char stage[24];
+  double ms;
+  double flops;
+  double bytes;
+} m2s_prof_launch;
+/* Synchronises on the recorded events, writes up to `max` launches in launch order (*n_out = all of
+ * them), clears the record.  out == NULL: *n_out = the number recorded, the record stays. */
+int m2s_prof_launches(m2s_prof_launch* out, int max, int* n_out);
 
 #ifdef __cplusplus
 }

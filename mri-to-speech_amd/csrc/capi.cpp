@@ -19,6 +19,7 @@ struct m2s_cam {
 
 extern "C" int m2s_prof_enable_impl(int on);
 extern "C" int m2s_prof_collect_impl(m2s_prof_stat* out, int max, int* n_out);
+extern "C" int m2s_prof_launches_impl(m2s_prof_launch* out, int max, int* n_out);
 
 namespace {
 
@@ -357,3 +358,7 @@ int m2s_prof_collect(m2s_prof_stat* out, int max, int* n_out) {
 }
 
 }  // extern "C"
+
+int m2s_prof_launches(m2s_prof_launch* out, int max, int* n_out) {
+  return guarded([&] { m2s_prof_launches_impl(out, max, n_out); });
+}

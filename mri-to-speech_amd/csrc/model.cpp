@@ -531,6 +531,7 @@ size_t Acoustic::workspace_bytes(int B, int T, int H, int W) const {
 
 void Acoustic::effnet(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe,
                       int* probe_dims, Workspace& ws, hipStream_t s) {
+  StageTag tag("cnn");
   if (dtype_ == M2S_DT_BF16 || dtype_ == M2S_DT_FP8)
     effnet_t<bf16_t>(frames, N, H, W, feats, stop_after, probe, probe_dims, ws, s);
   else if (dtype_ == M2S_DT_BF16X3)
@@ -700,7 +701,9 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
           const double P = (double)nh * nw;
           launch_ir_ws(cur, nc, nh, nw, b.c1.cs_in, b.c1.kp, cs, b.c1.w, b.c1.b, static_cast<const float*>(arena_.ptr(b.dw_w)),
                        static_cast<const float*>(arena_.ptr(b.dw_b)), M2, se_mean, 2.0 * nc * P * b.mid * (b.c1.cin + 9),
-                       4.0 * nc * P * (b.c1.cs_in + cs), s);
+                       // algorithmic bytes on the real channel counts (split fp32: 4 B an element): the block input,
+                       // the depthwise output, the split expand weights, taps and biases
+                       4.0 * nc * P * (b.c1.cin + b.mid) + 4.0 * b.mid * (b.c1.cin + 11.0), s);
         } else if (FUSABLE && b.stride == 1 && ir_fused_ && ir_fused_supported(nh, nw, b.c1.cs_in, cs, SPL)) {
           const double P = (double)nh * nw, es = SPL ? 4.0 : 2.0;
           f8 = b.f8_pwl && se_gemm_f8_supported(nh * nw, cs, chan_stride(b.cout));
@@ -711,7 +714,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
           }
           launch_ir_pwdw(cur, nc, b.c1.cs_in, b.c1.kp, b.c1.w, b.c1.b, wdw, static_cast<const float*>(arena_.ptr(b.dw_b)),
                          nh, nw, cs, M2, se_mean, SPL, 2.0 * nc * P * b.mid * (b.c1.cin + 9),
-                         nc * P * ((f8x ? 1.0 : es) * b.c1.cs_in + (f8 ? 1.0 : es) * cs), s, f8, f8x ? cur8 : nullptr,
+                         nc * P * ((f8x ? 1.0 : es) * b.c1.cin + (f8 ? 1.0 : es) * b.mid), s, f8, f8x ? cur8 : nullptr,
                          f8x ? arena_.ptr(b.f8x_w) : nullptr, f8x ? static_cast<const float*>(arena_.ptr(b.f8x_s)) : nullptr,
                          b.f8x_kp);
         } else if (FUSABLE && b.stride == 2 && ir_fused_ && ir_fused_s2_supported(oh, ow, b.c1.cs_in, cs, SPL) &&
@@ -769,12 +772,12 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         const int ld8 = want8 ? blocks_[k + 1].f8x_kp : 0;
         if (f8 && want8) next8 = cur8 == X8[0] ? X8[1] : X8[0];
         if (f8 && se_ws_ && se_ws_f8_supported(nh * nw, cs, chan_stride(b.cout))) {
-          const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
+          const double rows = (double)nc * nh * nw;
           launch_se_ws_f8(M2, nc * nh * nw, nh * nw, cs, arena_.ptr(b.f8_w), b.f8_kp, b.f8_npad,
                           static_cast<const float*>(arena_.ptr(b.f8_s)), static_cast<const float*>(arena_.ptr(b.f8_b)),
                           scale, b.skip ? cur : nullptr, nxt, chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
-                          rows * cs + 2.0 * rows * co * (b.skip ? 2.0 : 1.0) + (double)b.f8_npad * b.f8_kp + 2.0 * nc * cs +
-                              (next8 ? rows * ld8 : 0.0),
+                          rows * b.mid + 2.0 * rows * b.cout * (b.skip ? 2.0 : 1.0) + (double)b.cout * b.mid + 2.0 * nc * b.mid +
+                              (next8 ? rows * b.cout : 0.0),
                           next8, ld8);
         } else if (f8) {
           const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
@@ -785,10 +788,10 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                                 2.0 * nc * cs + (next8 ? rows * ld8 : 0.0),
                             next8, ld8);
         } else if (SPL && se_ws_ && se_ws_supported(nh * nw, cs, chan_stride(b.cout))) {
-          const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
+          const double rows = (double)nc * nh * nw;
           launch_se_ws(M2, nc * nh * nw, nh * nw, cs, b.c2.w, b.c2.n_pad, b.c2.b, scale, b.skip ? cur : nullptr, nxt,
                        chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
-                       4.0 * rows * cs + 4.0 * rows * co * (b.skip ? 2.0 : 1.0) + 4.0 * b.c2.n_pad * b.c2.kp + 4.0 * nc * cs);
+                       4.0 * rows * b.mid + 4.0 * rows * b.cout * (b.skip ? 2.0 : 1.0) + 4.0 * b.cout * b.mid + 4.0 * nc * b.mid);
         } else if (SPL && se_sp_ && se_gemm_sp_supported(nh * nw, cs, chan_stride(b.cout))) {
           const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
           launch_se_gemm_sp(M2, nc * nh * nw, nh * nw, cs, b.c2.w, b.c2.n_pad, b.c2.b, scale, b.skip ? cur : nullptr, nxt,
@@ -831,6 +834,7 @@ void Acoustic::bilstm(const float* feats, int B, int T, float* y, float* mel_nor
   float* pre = ws.take<float>(BT * 8 * H);
   float* hs = ws.take<float>(2 * BT * H);
   float* cst = ws.take<float>((size_t)2 * B * H);
+  StageTag tag("bilstm");
   ConvArgs a = conv_args(lstm_ih_);
   a.x = feats;
   a.y = pre;
@@ -861,6 +865,7 @@ void Acoustic::bilstm(const float* feats, int B, int T, float* y, float* mel_nor
     }
   }
   if (mel_norm) {
+    StageTag head("head");
     ProfScope ps("mel_head_kernel", 2.0 * BT * H * n_mels_, 4.0 * BT * (2 * H + n_mels_), s);
     launch_mel_head(hs, (int)BT, H, static_cast<const float*>(arena_.ptr(head_wt_)),
                     static_cast<const float*>(arena_.ptr(head_b_)), n_mels_, mel_norm, s);
@@ -1121,6 +1126,7 @@ void Vocoder::forward_from_norm(const float* mel_norm, const float* mean, const 
   M2S_CHECK(B > 0 && T > 0, "vocoder: empty input");
   const int nm = h_.num_mels, cs = chan_stride(nm);
   ws.take<char>((size_t)B * T * cs * act_bytes(dtype_));  // same carve as forward()
+  StageTag tag("glue");
   if (dtype_ == M2S_DT_BF16 || dtype_ == M2S_DT_FP8) {
     ProfScope ps("mel_glue_kernel<unsigned short>", 0.0, 4.0 * B * T * nm * 4, s);
     launch_mel_glue<bf16_t>(mel_norm, B * T, nm, mean, std_, mel_db, mel_log, static_cast<bf16_t*>(ln_buf), cs, s);
@@ -1252,6 +1258,7 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
   // upsampler does not re-apply LeakyReLU to its operand fragments every K step
   bool s_act = SPL;
   {
+    StageTag tag("voc_pre");
     ConvArgs a = conv_args(pre_);
     a.x = mel_nlc;
     a.y = S;
@@ -1267,6 +1274,7 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
   for (int i = 0; i < h_.n_up; ++i) {
     const PConv& up = ups_[i];
     const bool batched = is_batched(i);
+    StageTag tag("ups_c" + std::to_string(up.cout));
     ConvArgs a = conv_args(up);
     a.x = S;
     a.y = X;
@@ -1283,6 +1291,7 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
     }
     run_conv<T>(a, up, s);
     L *= up.ct_u;
+    StageTag mrf("mrf_c" + std::to_string(up.cout));  // the stage's MRF (ResBlocks + sum), models.py:119-125
     if (batched) {
       // the last accumulation stores lrelu(S) when the next consumer is an upsampler (conv_post
       // takes F.leaky_relu's default slope 0.01 on the raw S)
@@ -1394,6 +1403,7 @@ void Vocoder::run_t(const void* mel_nlc, int B, int Tn, float* wav, Workspace& w
       }
     }
   }
+  StageTag tag("voc_post");
   ProfScope ps(tname<T>(post_c_ <= 64 ? "conv_post_tile_kernel" : "conv_post_kernel"), 2.0 * B * L * post_c_ * 7, (sizeof(T) * Elem<T>::R) * (double)B * L * post_c_ + 4.0 * B * L, s);
   launch_conv_post<T>(S, B, L, post_c_, chan_stride(post_c_), static_cast<const float*>(arena_.ptr(post_w_)), post_b_,
                       wav, s);

@@ -10,8 +10,10 @@
 namespace m2s {
 namespace {
 
+thread_local std::string g_stage = "other";
+
 struct Rec {
-  std::string name;
+  std::string name, stage;
   double flops, bytes;
   hipEvent_t a, b;
 };
@@ -45,11 +47,14 @@ Prof& P() {
 
 bool prof_on() { return P().on; }
 
+StageTag::StageTag(const std::string& stage) : prev_(g_stage) { g_stage = stage; }
+StageTag::~StageTag() { g_stage = prev_; }
+
 ProfScope::ProfScope(const std::string& name, double flops, double bytes, hipStream_t s) : s_(s) {
   Prof& p = P();
   if (!p.on) return;
   std::lock_guard<std::mutex> g(p.mu);
-  Rec r{name, flops, bytes, p.get(), p.get()};
+  Rec r{name, g_stage, flops, bytes, p.get(), p.get()};
   M2S_HIP(hipEventRecord(r.a, s));
   slot_ = (int)p.recs.size();
   p.recs.push_back(r);
@@ -94,6 +99,36 @@ extern "C" int m2s_prof_collect_impl(m2s_prof_stat* out, int max, int* n_out) {
     if (n < max && out) out[n] = kv.second;
     ++n;
   }
+  if (n_out) *n_out = n;
+  return 0;
+}
+
+extern "C" int m2s_prof_launches_impl(m2s_prof_launch* out, int max, int* n_out) {
+  Prof& p = P();
+  std::lock_guard<std::mutex> g(p.mu);
+  if (!out) {  // count only: the record stays
+    if (n_out) *n_out = (int)p.recs.size();
+    return 0;
+  }
+  int n = 0;
+  for (auto& r : p.recs) {
+    M2S_HIP(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    M2S_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+    if (n < max && out) {
+      m2s_prof_launch& l = out[n];
+      std::memset(&l, 0, sizeof(l));
+      std::strncpy(l.name, r.name.c_str(), sizeof(l.name) - 1);
+      std::strncpy(l.stage, r.stage.c_str(), sizeof(l.stage) - 1);
+      l.ms = ms;
+      l.flops = r.flops;
+      l.bytes = r.bytes;
+    }
+    ++n;
+    p.pool.push_back(r.a);
+    p.pool.push_back(r.b);
+  }
+  p.recs.clear();
   if (n_out) *n_out = n;
   return 0;
 }

@@ -9,6 +9,18 @@ namespace m2s {
 
 bool prof_on();
 // Brackets one kernel launch with HIP events on `s` when profiling is enabled.
+// Stage label (e.g. "cnn", "bilstm", "mrf_c128") of the launches recorded while a StageTag lives on this
+// thread; nested tags restore the outer one.  bench.py's roofline.stages and tools/evidence.py's per-stage PMC
+// records group launches by it (m2s_prof_launches).
+class StageTag {
+ public:
+  explicit StageTag(const std::string& stage);
+  ~StageTag();
+
+ private:
+  std::string prev_;
+};
+
 class ProfScope {
  public:
   ProfScope(const std::string& name, double flops, double bytes, hipStream_t s);

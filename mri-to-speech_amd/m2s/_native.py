@@ -20,7 +20,7 @@ F32, BF16, BF16X3, FP8 = 0, 1, 2, 3
 DTYPES = {"fp32": F32, "float32": F32, "f32": F32, "bf16": BF16, "bfloat16": BF16, "bf16x3": BF16X3,
           "fp8": FP8, "e4m3": FP8}
 ELEM_F32, ELEM_I64 = 0, 1
-ABI_VERSION = 4  # include/m2s.h M2S_ABI_VERSION
+ABI_VERSION = 5  # include/m2s.h M2S_ABI_VERSION
 
 
 class M2SError(RuntimeError):
@@ -41,6 +41,11 @@ class HifiganH(C.Structure):
 
 class ProfStat(C.Structure):
     _fields_ = [("name", C.c_char * 96), ("launches", C.c_int64), ("ms", C.c_double), ("flops", C.c_double),
+                ("bytes", C.c_double)]
+
+
+class ProfLaunch(C.Structure):
+    _fields_ = [("name", C.c_char * 96), ("stage", C.c_char * 24), ("ms", C.c_double), ("flops", C.c_double),
                 ("bytes", C.c_double)]
 
 
@@ -94,6 +99,7 @@ def lib():
         "m2s_gap_backward": (i, [fp, C.c_int64, i, fp, vp]),
         "m2s_prof_enable": (i, [i]),
         "m2s_prof_collect": (i, [C.POINTER(ProfStat), i, C.POINTER(i)]),
+        "m2s_prof_launches": (i, [C.POINTER(ProfLaunch), i, C.POINTER(i)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -122,7 +128,7 @@ def exported_symbols() -> List[str]:
                         "m2s_cam_bn_channels", "m2s_cam_workspace_bytes", "m2s_cam_backbone",
                         "m2s_bilstm_train_workspace_bytes", "m2s_bilstm_train_forward", "m2s_bilstm_train_backward",
                         "m2s_linear_forward", "m2s_linear_backward", "m2s_gap_forward", "m2s_gap_backward",
-                        "m2s_prof_enable", "m2s_prof_collect")]
+                        "m2s_prof_enable", "m2s_prof_collect", "m2s_prof_launches")]
 
 
 def tensor_array(state: Dict[str, "np.ndarray"]) -> Tuple[C.Array, list]:
@@ -174,9 +180,29 @@ def prof_enable(on: bool) -> None:
     check(lib().m2s_prof_enable(1 if on else 0))
 
 
-def prof_collect() -> List[dict]:
+def prof_launches() -> List[dict]:
+    """Every launch recorded since prof_enable(True), in launch order: name, stage, ms, flops, bytes
+    (m2s_prof_launches); clears the record."""
     n = C.c_int(0)
-    buf = (ProfStat * 256)()
-    check(lib().m2s_prof_collect(buf, 256, C.byref(n)))
-    return [dict(name=buf[i].name.decode(), launches=buf[i].launches, ms=buf[i].ms, flops=buf[i].flops,
-                 bytes=buf[i].bytes) for i in range(min(n.value, 256))]
+    check(lib().m2s_prof_launches(None, 0, C.byref(n)))  # count only (records kept)
+    cap = max(n.value, 1)
+    buf = (ProfLaunch * cap)()
+    check(lib().m2s_prof_launches(buf, cap, C.byref(n)))
+    return [dict(name=buf[i].name.decode(), stage=buf[i].stage.decode(), ms=buf[i].ms, flops=buf[i].flops,
+                 bytes=buf[i].bytes) for i in range(min(n.value, cap))]
+
+
+def aggregate(launches: List[dict], key: str = "name") -> List[dict]:
+    """Per-kernel (key="name") or per-stage (key="stage") sums of prof_launches() records."""
+    agg: Dict[str, dict] = {}
+    for r in launches:
+        a = agg.setdefault(r[key], dict(name=r[key], launches=0, ms=0.0, flops=0.0, bytes=0.0))
+        a["launches"] += 1
+        for f in ("ms", "flops", "bytes"):
+            a[f] += r[f]
+    return list(agg.values())
+
+
+def prof_collect() -> List[dict]:
+    """Per-kernel sums of the recorded launches (name, launches, ms, flops, bytes); clears the record."""
+    return aggregate(prof_launches(), "name")

@@ -115,13 +115,44 @@ def export_mels(args: argparse.Namespace) -> list:
     if not torch.cuda.is_available():
         raise SystemExit("m2s needs an MI355X (HIP) device; none is visible")
     world, rank, local = init_distributed()
+    try:
+        return _export(args, out_dir, mean, std, world, rank, local)
+    finally:  # leave the group on every path, errors included, so no peer waits on this rank
+        if world > 1:
+            import torch.distributed as dist
+            if dist.is_initialized():
+                dist.destroy_process_group()
+
+
+def agree(ok: bool, device, world: int) -> bool:
+    """True on every rank iff every rank passed ``ok`` (one all-reduce MIN); world 1: ``ok``."""
+    if world == 1:
+        return ok
+    import torch.distributed as dist
+    comm = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=comm)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def _export(args, out_dir, mean, std, world, rank, local) -> list:
     # one GPU per rank; more ranks than GPUs wrap round (a gloo rehearsal on a one-GPU box)
     device = torch.device("cuda", local % torch.cuda.device_count()) if world > 1 else torch.device("cuda")
     ckpt = Path(args.mri_checkpoint).resolve()
-    # rank 0 reads the checkpoint; the other ranks build the same module tree and receive its weights
-    model = drivers.build_acoustic(ckpt if rank == 0 else None, device, code_dir=args.mri_code_dir,
-                                   n_mels=mean.numel(), dtype=args.dtype,
-                                   log=print if rank == 0 else (lambda *a: None))
+    # rank 0 reads the checkpoint; the other ranks build the same module tree and receive its weights.  A rank
+    # that fails to build (rank 0: a missing or unreadable checkpoint) makes every rank stop before the
+    # broadcast instead of leaving its peers blocked in it until the collective timeout.
+    err = None
+    try:
+        model = drivers.build_acoustic(ckpt if rank == 0 else None, device, code_dir=args.mri_code_dir,
+                                       n_mels=mean.numel(), dtype=args.dtype,
+                                       log=print if rank == 0 else (lambda *a: None))
+    except Exception as e:  # noqa: BLE001 - re-raised below on this rank, reported as a failure on the others
+        err = e
+    if not agree(err is None, device, world):
+        if err is not None:
+            raise err
+        raise SystemExit(f"[rank {rank}] another rank failed to build the acoustic model (see rank 0's error)")
     if world > 1:
         broadcast_model_state(model, device)
     mean, std = mean.to(device), std.to(device)

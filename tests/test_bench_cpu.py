@@ -22,13 +22,25 @@ def test_parse_defaults_are_the_headline_workload():
     assert a.steps * 0.04 >= 3.0  # a timed region of about three seconds or more at ~42 ms per step
 
 
+def _launches(stats):
+    """prof_launches()-style records (one per launch, in order, with a stage) from per-kernel totals."""
+    out = []
+    for s in stats:
+        n = s["launches"]
+        out += [dict(name=s["name"], stage=s["stage"], ms=s["ms"] / n, flops=s["flops"] / n, bytes=s["bytes"] / n)
+                for _ in range(n)]
+    return out
+
+
 def test_roofline_picks_the_dominant_kernel_and_its_arithmetic():
     stats = [
-        {"name": "dwconv_kernel<m2s::sp_t, 1>", "launches": 36, "ms": 20.0, "flops": 4e9 * 36, "bytes": 1.8e9 * 36},
-        {"name": "lstm_persistent_kernel", "launches": 2, "ms": 1.2, "flops": 2e10, "bytes": 1e8},
-        {"name": "conv_gemm_kernel<128, 128, 4, 4, 2, 3, 0, 1>", "launches": 40, "ms": 10.0, "flops": 1e12, "bytes": 1e10},
+        {"name": "dwconv_kernel<m2s::sp_t, 1>", "launches": 36, "ms": 20.0, "flops": 4e9 * 36, "bytes": 1.8e9 * 36,
+         "stage": "cnn"},
+        {"name": "lstm_persistent_kernel", "launches": 2, "ms": 1.2, "flops": 2e10, "bytes": 1e8, "stage": "bilstm"},
+        {"name": "conv_gemm_kernel<128, 128, 4, 4, 2, 3, 0, 1>", "launches": 40, "ms": 10.0, "flops": 1e12, "bytes": 1e10,
+         "stage": "mrf_c128"},
     ]
-    r = bench.roofline(stats, "bf16x3", steps=2, fps=30000.0, frames_per_step=1920)
+    r = bench.roofline(_launches(stats), "bf16x3", steps=2, fps=30000.0, frames_per_step=1920, stages=True)
     assert r["kernel"].startswith("dwconv") and r["bound"] == "hbm" and r["unit"] == "GB/s"
     assert abs(r["achieved"] - 1.8e9 * 36 / 20e-3 / 1e9) < 1e-6 * r["achieved"]
     assert r["launches_per_step"] == 18
@@ -48,6 +60,12 @@ def test_roofline_picks_the_dominant_kernel_and_its_arithmetic():
                                                                        "ir_ws_kernel<16, 4>", "conv1d_halo_sp_kernel<64>", "ers2_sp_kernel<16>"))
     fl = (4e9 * 36 + 2e10 + 1e12) / (2 * 1920)
     assert r["plan_gflop_per_frame"] == pytest.approx(fl / 1e9, rel=1e-3)
+    # roofline.stages: per stage event time per step and algorithmic rates, in path order
+    st = r["stages"]
+    assert list(st) == ["cnn", "bilstm", "mrf_c128"]
+    assert st["cnn"]["ms_per_step"] == pytest.approx(10.0) and st["cnn"]["launches_per_step"] == 18
+    assert st["mrf_c128"]["algorithmic_GBs"] == pytest.approx(1e10 / 2 / 5e-3 / 1e9, rel=1e-3)
+    assert "stages_source" in r
 
 
 def _free_port():

@@ -156,3 +156,35 @@ def test_export_pending_samples_reads_lengths_only(tmp_path):
     assert [(j.stem, j.length, j.array is None) for j in jobs[:2]] == [("a", 4, True), ("b", 11, True)]
     assert jobs[2].error is not None
     assert mod.load_frames(jobs[1]).array.shape == (11, 8, 8)
+
+
+def _agree_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import importlib.util
+        repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        spec = importlib.util.spec_from_file_location(
+            "m2s_export_mels", os.path.join(repo, "mri-to-speech_amd", "scripts", "export_predicted_mels.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        dev = torch.device("cpu")
+        q.put((rank, mod.agree(True, dev, world), mod.agree(rank != 0, dev, world)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_export_ranks_agree_on_a_failed_build_gloo():
+    """export_predicted_mels.py's torchrun mode: when rank 0 cannot build the model (a bad checkpoint) every rank
+    learns it from one all-reduce and stops, instead of waiting in the state broadcast until the timeout."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    msgs = sorted(q.get(timeout=180) for _ in range(3))
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert msgs == [(0, True, False), (1, True, False), (2, True, False)]

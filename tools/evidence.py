@@ -37,6 +37,88 @@ def counters(d):
     return agg, {k: len(v) for k, v in disp.items()}
 
 
+def _base(name):
+    return re.sub(r"[<(].*$", "", short(name)).strip()
+
+
+def dispatch_stages(d):
+    """{Dispatch_Id: stage} for a PMC pass directory: its dispatches in order, aligned with the launch sequence
+    tools/profile_step.py logged (<d>.launches.json: libm2s's launches with their stage tags) by kernel name; a
+    dispatch no launch matches (runtime fills, torch kernels) gets no stage.  Returns (map, steps, matched, n)."""
+    log = d.rstrip("/") + ".launches.json"
+    if not os.path.exists(log):
+        return None, 0, 0, 0
+    with open(log) as fh:
+        rec = json.load(fh)
+    launches = rec["launches"]
+    names = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                names[int(r["Dispatch_Id"])] = r["Kernel_Name"]
+    disp = sorted(names)
+    out, j, matched = {}, 0, 0
+    i = 0
+    while i < len(disp) and j < len(launches):
+        want = _base(launches[j][0])
+        # the next dispatch of this kernel within a short window (a launch may be preceded by fills / copies)
+        hit = next((q for q in range(i, min(i + 8, len(disp))) if _base(names[disp[q]]) == want), None)
+        if hit is None:  # this launch was not traced as named: skip it
+            j += 1
+            continue
+        out[disp[hit]] = launches[j][1]
+        matched += 1
+        i, j = hit + 1, j + 1
+    return out, rec["steps"], matched, len(launches)
+
+
+def stage_counters(d, st_map):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                st = st_map.get(int(r["Dispatch_Id"]))
+                if st is not None:
+                    agg[st][r["Counter_Name"]] += float(r["Counter_Value"] or 0)
+    return agg
+
+
+def stages(src, sha, prefix):
+    """<prefix>_stages.json: per stage of the path (libm2s's StageTag labels: cnn, bilstm, mrf_c<C>, ...), HBM
+    bytes per step (FETCH_SIZE x2 + WRITE_SIZE, KiB -> bytes), MFMA utilisation and VALU per MFMA."""
+    res = collections.defaultdict(dict)
+    notes = {}
+    for pas in ("fetch", "write", "mfma", "valu"):
+        d = os.path.join(src, pas)
+        st_map, steps, matched, n = dispatch_stages(d)
+        if st_map is None:
+            return None
+        notes[pas] = f"{matched} of {n} launches aligned to dispatches over {steps} steps"
+        for st, c in stage_counters(d, st_map).items():
+            r = res[st]
+            if pas == "fetch":
+                r["fetch_bytes_per_step"] = 2.0 * c["FETCH_SIZE"] * 1024 / steps
+            elif pas == "write":
+                r["write_bytes_per_step"] = c["WRITE_SIZE"] * 1024 / steps
+            elif pas == "mfma":
+                g = c.get("GRBM_GUI_ACTIVE", 0.0)
+                r["mfma_util"] = round(c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (1024.0 * g / 8.0), 4) if g else None
+                r["mfma_insts_per_step"] = c.get("SQ_INSTS_MFMA", 0.0) / steps
+            else:
+                r["valu_insts_per_step"] = c.get("SQ_INSTS_VALU", 0.0) / steps
+                lds = c.get("SQ_INSTS_LDS", 0.0)
+                r["lds_conflicts_per_lds_inst"] = round(c.get("SQ_LDS_BANK_CONFLICT", 0.0) / lds, 3) if lds else None
+    for r in res.values():
+        r["hbm_bytes_per_step"] = r.get("fetch_bytes_per_step", 0.0) + r.get("write_bytes_per_step", 0.0)
+        mi = r.get("mfma_insts_per_step")
+        r["valu_per_mfma"] = round(r.get("valu_insts_per_step", 0.0) / mi, 2) if mi else None
+    meta = {"src_sha": sha, "source": f"rocprofv3 --pmc passes in {src} (tools/gpu_evidence.sh, tools/profile_step.py "
+            "bench workload), dispatches aligned with libm2s's stage-tagged launch log", "alignment": notes}
+    with open(prefix + "_stages.json", "w") as fh:
+        json.dump({"meta": meta, "stages": res}, fh, indent=1)
+    return res
+
+
 def main(src, prefix):
     sha = open(os.path.join(src, "src_sha.txt")).read().strip()
     fe, wr = per_kernel(os.path.join(src, "fetch"), "FETCH_SIZE"), per_kernel(os.path.join(src, "write"), "WRITE_SIZE")
@@ -81,6 +163,11 @@ def main(src, prefix):
     with open(prefix + "_sq_mfma.txt", "w") as fh:
         fh.write("\n".join(lines) + "\n")
     print("\n".join(lines[:40]))
+    st = stages(src, sha, prefix)
+    if st:
+        for k, v in st.items():
+            print(f"stage {k:10s} hbm {v['hbm_bytes_per_step'] / 1e6:9.1f} MB/step  mfma {v.get('mfma_util')}  "
+                  f"valu/mfma {v.get('valu_per_mfma')}")
 
 
 if __name__ == "__main__":

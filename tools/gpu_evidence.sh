@@ -18,7 +18,7 @@ export STEPS=${STEPS:-2}
 python3 -c "import bench; print(bench.source_sha())" > "$OUT/src_sha.txt" || exit 1
 pmc() {  # pmc <dir> <counters...>
   local d=$1; shift
-  (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc "$@" --output-format csv -d "$ROOT/$OUT/$d" -o run -- \
+  (cd /tmp && M2S_LAUNCH_LOG="$ROOT/$OUT/$d.launches.json" timeout -s KILL 150 rocprofv3 --pmc "$@" --output-format csv -d "$ROOT/$OUT/$d" -o run -- \
      python3 "$ROOT/tools/profile_step.py" > "$ROOT/$OUT/$d.log" 2>&1)
 }
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/trace" -o run -- \

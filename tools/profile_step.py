@@ -20,7 +20,16 @@ voc = runtime.VocoderEngine(synth.synth_generator_state(0), HIFIGAN_H, dtype=dt,
 mean, std = synth.synth_scaler()
 pipe = runtime.Pipeline(ac, voc, mean, std)
 x = bench.make_frames(clips, frames, 256, 0, dev)
+log = os.environ.get("M2S_LAUNCH_LOG")  # the launch sequence with libm2s's stage tags (tools/evidence.py aligns the
+if log:                                 # PMC dispatches with it)
+    from m2s import _native
+    _native.prof_enable(True)
 for _ in range(steps):
     pipe.forward(x)
 torch.cuda.synchronize()
+if log:
+    import json
+    _native.prof_enable(False)
+    with open(log, "w") as fh:
+        json.dump({"steps": steps, "launches": [[r["name"], r["stage"]] for r in _native.prof_launches()]}, fh)
 print("done")
