@@ -86,15 +86,19 @@ int m2s_acoustic_create(const m2s_tensor* sd, int n, int n_mels, int rnn_hidden,
 void m2s_acoustic_destroy(m2s_acoustic* m);
 /* frames per CNN pass (bounds the CNN workspace); default 1920 (= m2s.config.CNN_CHUNK, the size bench.py times) */
 int m2s_acoustic_set_chunk(m2s_acoustic* m, int frames);
-/* Asynchronous failure report.  The persistent BiLSTM waits at a grid barrier once per time step;
- * a wait that exceeds its poll limit (workgroups not co-resident) poisons the outputs with NaN and
- * raises a host-visible flag.  This call returns M2S_E_INTERNAL (and clears the flag) when such a
+/* Asynchronous failure report.  The persistent BiLSTM waits at a grid barrier once per time step, and
+ * the persistent CNN kernels (ir_ws, se_ws) at LDS flags between their producer and consumer waves;
+ * a wait that exceeds its poll limit poisons the affected outputs with NaN and raises a host-visible flag.  This call returns M2S_E_INTERNAL (and clears the flag) when such a
  * launch has happened: call it after synchronising the stream.  The next forward / bilstm /
  * pipeline call on the engine fails the same way.  Synchronous, host only. */
 int m2s_acoustic_status(m2s_acoustic* m);
 /* Fault injection for tests: polls per BiLSTM barrier wait before it times out (default 2^24); 0 makes
  * the first wait time out unconditionally. */
 int m2s_acoustic_set_lstm_spin_limit(m2s_acoustic* m, unsigned polls);
+/* Fault injection for tests: polls per LDS flag-ring wait of the persistent CNN kernels (ir_ws producers'
+ * weight-slot wait, se_ws FULL / FREE waits; default 2^20) before it times out; 0 makes every such wait time out.
+ * A timeout poisons the affected outputs with NaN and is reported by m2s_acoustic_status. */
+int m2s_acoustic_set_ws_spin_limit(m2s_acoustic* m, unsigned polls);
 size_t m2s_acoustic_workspace_bytes(const m2s_acoustic* m, int B, int T, int H, int W);
 /* frames (B,T,H,W) fp32 in [0,1] -> mel_norm (B,T,n_mels) fp32. */
 int m2s_acoustic_forward(m2s_acoustic* m, const float* frames, int B, int T, int H, int W, float* mel_norm,

@@ -71,7 +71,11 @@ hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
 
 // an earlier launch of this engine hit a BiLSTM barrier timeout (its outputs hold NaN): fail loudly
 void no_pending_error(m2s::Acoustic& a) {
-  if (a.take_async_error() != M2S_OK)
+  const unsigned e = a.take_async_error();
+  if (e == m2s::M2S_ASYNC_WS)
+    throw m2s::Error(M2S_E_INTERNAL, "a previous CNN launch timed out at an LDS flag-ring wait (ir_ws / se_ws "
+                                     "producer-consumer hand-off); the affected outputs were poisoned with NaN");
+  if (e != 0)
     throw m2s::Error(M2S_E_INTERNAL, "a previous BiLSTM launch timed out at its grid barrier (workgroups not "
                                      "co-resident?); its outputs were poisoned with NaN");
 }
@@ -117,6 +121,13 @@ int m2s_acoustic_set_lstm_spin_limit(m2s_acoustic* m, unsigned polls) {
   return guarded([&] {
     M2S_CHECK(m, "bad argument");
     m->impl.lstm_spin_max_ = polls;
+  });
+}
+
+int m2s_acoustic_set_ws_spin_limit(m2s_acoustic* m, unsigned polls) {
+  return guarded([&] {
+    M2S_CHECK(m, "bad argument");
+    m->impl.ws_spin_max_ = polls;
   });
 }
 

@@ -97,7 +97,8 @@ template <int W, int KS>
 __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     ir_ws_kernel(const bf16_t* __restrict__ x, int N, int H, int cs_mid, const bf16_t* __restrict__ wpw,
                  const float* __restrict__ bpw, const float* __restrict__ wdw, const float* __restrict__ bdw,
-                 bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, unsigned long long* __restrict__ trace) {
+                 bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, unsigned long long* __restrict__ trace,
+                 unsigned spin_max, unsigned* __restrict__ err) {
   constexpr int CS = KS * 32;  // input channel stride = expand K
   constexpr int CPP = (CS * 2 + 255) / 256 * 16;
   constexpr int CPR = 2 * CPP;  // 16-byte chunks per LDS x row
@@ -117,6 +118,9 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   float* se_acc = red + 2 * WS_NC * 32;                       // [cs_mid] (NB > 1)
   // producer waves that finished slice f's MFMAs (monotonic): W(f + 2) may then overwrite W(f)'s slot
   unsigned* pdone = reinterpret_cast<unsigned*>(smem + Lg.total - 16);
+  // set by a producer whose pdone wait timed out (reported through `err`): the squeeze of every slice finalized
+  // from then on stores NaN, so the images of this workgroup come out NaN instead of silently wrong
+  unsigned* poison = pdone + 1;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -150,7 +154,10 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     return d;
   };
 
-  if (tid == 0) *pdone = 0u;  // ordered before any use by the first barrier of the slice loop
+  if (tid == 0) {  // ordered before any use by the first barrier of the slice loop
+    *pdone = 0u;
+    *poison = 0u;
+  }
   // the tiles' halo columns are zero for good (the producers write only interior columns)
   for (int i = tid; i < 2 * 8 * Lg.TROWS; i += 64 * (WS_NP + WS_NC)) {
     const int pl = i / Lg.TROWS, r = i - pl * Lg.TROWS, c = r % WT;
@@ -208,11 +215,19 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"((uint32_t)(uintptr_t)pdone), "v"(1u) : "memory");
     if (!more) return;
     const unsigned target = (unsigned)(WS_NP * (f + 1));
-    for (unsigned n = 0; n < (1u << 20); ++n) {
+    bool ok = false;
+    for (unsigned n = 0; n < spin_max; ++n) {
       unsigned v;
       asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((uint32_t)(uintptr_t)pdone) : "memory");
-      if (__builtin_amdgcn_readfirstlane(v) >= target) break;
+      if (__builtin_amdgcn_readfirstlane(v) >= target) {
+        ok = true;
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
+    }
+    if (!ok) {  // W(f + 2) may now overwrite a slot another producer still reads: report it, poison the squeeze
+      report_async(err, M2S_ASYNC_WS, lane);
+      if (lane == 0) asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)poison), "v"(1u) : "memory");
     }
     issue_w(f + 2, d2);
   };
@@ -380,7 +395,8 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       if (d.band > 0) t += se_acc[c];
       se_acc[c] = t;
     }
-    if (d.band == NB - 1) act_st<sp_t>(reinterpret_cast<sp_t*>(se_mean), d.img, cs_mid, c, t / (float)P);
+    if (d.band == NB - 1)
+      act_st<sp_t>(reinterpret_cast<sp_t*>(se_mean), d.img, cs_mid, c, *poison ? __builtin_nanf("") : t / (float)P);
   };
 
   // ---- the slice pipeline: producers on f = i, consumers on f = i - 1 (and the squeeze of i - 2) --
@@ -472,7 +488,7 @@ bool ir_ws_supported(int H, int W, int cs_in, int kp, int cs_mid) {
 
 void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_mid, const void* wpw, const float* bpw,
                   const float* wdw, const float* bdw, void* y, void* se_mean, double flops, double bytes,
-                  hipStream_t s) {
+                  hipStream_t s, AsyncReport rep) {
   M2S_CHECK(ir_ws_supported(H, W, cs_in, kp, cs_mid) && N > 0, "ir_ws: unsupported shape");
   M2S_CHECK((double)N * H * W * cs_mid * 4.0 < 4294967296.0, "ir_ws: output map too large for 32-bit offsets");
   const WsLayout L = ws_layout(H, W, cs_in, cs_mid);
@@ -506,7 +522,7 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
     allow_lds(reinterpret_cast<const void*>(&ir_ws_kernel<W_, KS_>));                                 \
     ProfScope ps("ir_ws_kernel<" #W_ ", " #KS_ ">", flops, bytes, s);                                   \
     hipLaunchKernelGGL((ir_ws_kernel<W_, KS_>), grid, dim3(64 * (WS_NP + WS_NC)), L.total, s, xb, N, H, cs_mid, wb, \
-                       bpw, wdw, bdw, yb, mb, tr);                                                      \
+                       bpw, wdw, bdw, yb, mb, tr, rep.spin_max, rep.err);                                \
     M2S_IRWS_DUMP(#W_ "," #KS_)                                                                         \
     M2S_HIP(hipGetLastError());                                                                         \
     return;                                                                                             \

@@ -5,6 +5,18 @@
 
 namespace m2s {
 
+// Asynchronous failure report of the persistent kernels' bounded waits (LDS flag rings, grid hand-offs): the
+// engine's host-mapped error word takes one of these codes; m2s_acoustic_status turns it into an error.
+enum AsyncCode : unsigned { M2S_ASYNC_LSTM = 1u, M2S_ASYNC_WS = 2u };
+struct AsyncReport {
+  unsigned spin_max = 1u << 20;  // polls per LDS flag wait (each ~1 s_sleep) before it counts as timed out
+  unsigned* err = nullptr;       // host-mapped error word, or null (no report)
+};
+// one lane of the wave stores `code` to the host-mapped word (system scope: the host reads it after a sync)
+__device__ __forceinline__ void report_async(unsigned* err, unsigned code, int lane) {
+  if (err && lane == 0) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // conv_stem (3x3 s2 TF-SAME, grey repeat folded: w[o][9]) + bn1 + SiLU.  frames fp32 (N,H,W)
 // -> y (N,OH,OW,cs_out) T.  timm conv_stem/bn1, mri_acoustic_model.py:41-46.
 template <typename T>
@@ -66,8 +78,10 @@ void launch_se_gemm_sp(const void* x, int M, int P, int cs_in, const void* w, in
 // per-K-step barrier; the ring runs across tiles).  Same operands as launch_se_gemm_sp; P % 256 == 0 with
 // cs_out <= 128 (16x16 maps) or P == 64 with 128 < cs_out <= 224 (8x8 maps).  (se_ws.hip)
 bool se_ws_supported(int P, int cs_in, int cs_out);
+// Every FULL / FREE wait is bounded by rep.spin_max polls; a timeout is reported through rep.err and the
+// consumer's tiles from then on are stored as NaN.
 void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_pad, const float* bias, const void* gate,
-                  const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes);
+                  const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes, AsyncReport rep = {});
 
 // fp8 engines: launch_se_gemm_f8's operation (e4m3 x8 / w8, bf16 gate / res / y) on the same warp-specialised
 // flag ring.  (se_ws.hip)
@@ -75,7 +89,7 @@ bool se_ws_f8_supported(int P, int cs_in, int cs_out);
 // y8 (optional): an e4m3 copy of y, rows of ld8 bytes (the next IR block's e4m3 expand operand, launch_ir_pwdw x8)
 void launch_se_ws_f8(const void* x8, int M, int P, int cs_in, const void* w8, int kp, int n_pad, const float* wscale,
                      const float* bias, const void* gate, const void* res, void* y, int cs_out, hipStream_t s, double flops,
-                     double bytes, void* y8 = nullptr, int ld8 = 0);
+                     double bytes, void* y8 = nullptr, int ld8 = 0, AsyncReport rep = {});
 
 // The same for a stride-2 depthwise (TF-SAME, top / left pads pad_t / pad_l) on an IH x IW <= 256-pixel
 // conv_pw map: y (N, OH*OW, cs_mid), se_mean over the OH x OW output.  (ir_fused.hip)
@@ -83,9 +97,11 @@ void launch_se_ws_f8(const void* x8, int M, int P, int cs_in, const void* w8, in
 // W = 8 / 16 maps as one persistent warp-specialised workgroup per CU; same outputs as
 // launch_ir_pwdw(split = true).  wdw: fp32 tap-major [9][cs_mid].  (ir_ws.hip)
 bool ir_ws_supported(int H, int W, int cs_in, int kp, int cs_mid);
+// The producers' weight-slot wait is bounded by rep.spin_max polls; a timeout is reported through rep.err and
+// the images of that workgroup's slice get a NaN SE mean (their block output is NaN).
 void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_mid, const void* wpw, const float* bpw,
                   const float* wdw, const float* bdw, void* y, void* se_mean, double flops, double bytes,
-                  hipStream_t s);
+                  hipStream_t s, AsyncReport rep = {});
 // Stride-2 IR front half on bands of 4 output rows (blocks.3.0: 32x32 -> 16x16), split fp32 or bf16: y =
 // the SE GEMM's operand (N, OH*OW, cs_mid; split: interleaved hi/lo), psum = squeeze partial sums
 // (N, OH / 4, cs_mid) for launch_se_mean.  wdw: fp32 tap-major [9][cs_mid].  (ir_s2band.hip)

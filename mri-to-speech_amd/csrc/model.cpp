@@ -451,10 +451,7 @@ Acoustic::~Acoustic() {
   if (err_host_) (void)hipHostFree(err_host_);
 }
 
-int Acoustic::take_async_error() {
-  const unsigned e = __atomic_exchange_n(err_host_, 0u, __ATOMIC_ACQ_REL);
-  return e ? M2S_E_INTERNAL : M2S_OK;
-}
+unsigned Acoustic::take_async_error() { return __atomic_exchange_n(err_host_, 0u, __ATOMIC_ACQ_REL); }
 
 void Acoustic::effnet_dims(int H, int W, size_t* io, size_t* mid, size_t* se) const {
   int oh, ow, ph, pw;
@@ -703,7 +700,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                        static_cast<const float*>(arena_.ptr(b.dw_b)), M2, se_mean, 2.0 * nc * P * b.mid * (b.c1.cin + 9),
                        // algorithmic bytes on the real channel counts (split fp32: 4 B an element): the block input,
                        // the depthwise output, the split expand weights, taps and biases
-                       4.0 * nc * P * (b.c1.cin + b.mid) + 4.0 * b.mid * (b.c1.cin + 11.0), s);
+                       4.0 * nc * P * (b.c1.cin + b.mid) + 4.0 * b.mid * (b.c1.cin + 11.0), s, ws_report());
         } else if (FUSABLE && b.stride == 1 && ir_fused_ && ir_fused_supported(nh, nw, b.c1.cs_in, cs, SPL)) {
           const double P = (double)nh * nw, es = SPL ? 4.0 : 2.0;
           f8 = b.f8_pwl && se_gemm_f8_supported(nh * nw, cs, chan_stride(b.cout));
@@ -778,7 +775,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                           scale, b.skip ? cur : nullptr, nxt, chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
                           rows * b.mid + 2.0 * rows * b.cout * (b.skip ? 2.0 : 1.0) + (double)b.cout * b.mid + 2.0 * nc * b.mid +
                               (next8 ? rows * b.cout : 0.0),
-                          next8, ld8);
+                          next8, ld8, ws_report());
         } else if (f8) {
           const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
           launch_se_gemm_f8(M2, nc * nh * nw, nh * nw, cs, arena_.ptr(b.f8_w), b.f8_kp, b.f8_npad,
@@ -791,7 +788,8 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
           const double rows = (double)nc * nh * nw;
           launch_se_ws(M2, nc * nh * nw, nh * nw, cs, b.c2.w, b.c2.n_pad, b.c2.b, scale, b.skip ? cur : nullptr, nxt,
                        chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
-                       4.0 * rows * b.mid + 4.0 * rows * b.cout * (b.skip ? 2.0 : 1.0) + 4.0 * b.cout * b.mid + 4.0 * nc * b.mid);
+                       4.0 * rows * b.mid + 4.0 * rows * b.cout * (b.skip ? 2.0 : 1.0) + 4.0 * b.cout * b.mid + 4.0 * nc * b.mid,
+                       ws_report());
         } else if (SPL && se_sp_ && se_gemm_sp_supported(nh * nw, cs, chan_stride(b.cout))) {
           const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
           launch_se_gemm_sp(M2, nc * nh * nw, nh * nw, cs, b.c2.w, b.c2.n_pad, b.c2.b, scale, b.skip ? cur : nullptr, nxt,

@@ -86,8 +86,15 @@ class Acoustic {
   Acoustic(const Acoustic&) = delete;
   Acoustic& operator=(const Acoustic&) = delete;
   // M2S_E_INTERNAL (and clears the flag) if a BiLSTM barrier of an earlier launch timed out
-  int take_async_error();
+  unsigned take_async_error();
   unsigned lstm_spin_max_ = LSTM_SPIN_MAX;  // fault injection: m2s_acoustic_set_lstm_spin_limit
+  unsigned ws_spin_max_ = 1u << 20;        // LDS flag-ring waits of ir_ws / se_ws; m2s_acoustic_set_ws_spin_limit
+  AsyncReport ws_report() const {
+    AsyncReport r;
+    r.spin_max = ws_spin_max_;
+    r.err = err_dev_;
+    return r;
+  }
   int device() const { return device_; }
   int n_mels() const { return n_mels_; }
   int chunk = 1920;  // = m2s.config.CNN_CHUNK (the benched pass size)

@@ -25,7 +25,9 @@
 //     tile's first slots.
 //
 // Flags are monotonic per-slot counters in LDS (ds_add_u32 by one lane, ds_read polls with s_sleep); every
-// wait is bounded (a poll limit, then the wave goes on: a wrong result, never a hang).  LDS-DMA data is in
+// wait is bounded: past its poll limit the wave reports the timeout through the engine's host-mapped error
+// word (m2s_acoustic_status, as the BiLSTM's barrier waits do), a consumer stores its tiles as NaN from then
+// on, and the wave goes on (a reported failure, never a hang).  LDS-DMA data is in
 // LDS when the issuing wave's vmcnt retires it, and a consumer reads a slot only after the loader's flag
 // update that follows that vmcnt wait, so the flag orders the data.
 #include <cstdlib>
@@ -40,7 +42,6 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int ROWB = 128;            // bytes per LDS row: 32 channels [hi 32 | lo 32] bf16
-constexpr unsigned SPIN_MAX = 1u << 20;  // ~0.1 s of polls: a broken protocol gives wrong results, not a hang
 
 __device__ __attribute__((aligned(16))) uint4 g_se_ws_zero[4];  // DMA source of padding lanes
 
@@ -54,14 +55,16 @@ __device__ __forceinline__ void dma16(const void* src, uint32_t lds_wave_base) {
 }
 __device__ __forceinline__ uint32_t lds_u32(const void* p) { return (uint32_t)(uintptr_t)p; }
 
-// flag poll: one ds_read (all lanes read the same dword), then a scalar copy; bounded
-__device__ __forceinline__ void wait_flag(uint32_t addr, unsigned target) {
-  for (unsigned i = 0; i < SPIN_MAX; ++i) {
+// flag poll: one ds_read (all lanes read the same dword), then a scalar copy; bounded by `spin_max` polls
+// (0: the wait fails at once, the fault injection of m2s_acoustic_set_ws_spin_limit).  false = timed out
+__device__ __forceinline__ bool wait_flag(uint32_t addr, unsigned target, unsigned spin_max) {
+  for (unsigned i = 0; i < spin_max; ++i) {
     unsigned v;
     asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
-    if (__builtin_amdgcn_readfirstlane(v) >= target) return;
+    if (__builtin_amdgcn_readfirstlane(v) >= target) return true;
     __builtin_amdgcn_s_sleep(1);
   }
+  return false;
 }
 __device__ __forceinline__ void bump_flag(uint32_t addr, int lane) {
   if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"(addr), "v"(1u) : "memory");
@@ -78,6 +81,8 @@ struct SeWsArgs {
   uint8_t* y8;            // F8: e4m3 copy of y (the next IR block's expand operand, rows of ld8 bytes) or null
   int M, P, cs_in, cs_out, n_tiles_m, kp;  // kp: F8 weight row bytes (cs_in rounded up to 128)
   int ld8;
+  unsigned spin_max;  // polls per flag wait before it times out
+  unsigned* err;      // host-mapped error word (M2S_ASYNC_WS on a timeout) or null
 };
 
 constexpr int E8M0_ONE = 0x7f7f7f7f;  // 2^0 block scale in every byte
@@ -141,7 +146,7 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
       const uint8_t* xt = a.x + (size_t)m0 * xrow_b;
       for (int st = 0; st < nsteps; ++st, ++s) {
         const int slot = s % NS, use = s / NS;
-        if (use > 0) wait_flag(free0 + 4 * slot, (unsigned)(NC * use));
+        if (use > 0 && !wait_flag(free0 + 4 * slot, (unsigned)(NC * use), a.spin_max)) report_async(a.err, M2S_ASYNC_WS, lane);
         if (st == 0 && l == 0) {  // the tile's gate rows: nimg x 2 cs_in bf16, 16 B a lane
           const int img0 = m0 / a.P, nb = grow / 16;
           char* gdst = gbuf + (it & 1) * nimg * gimg;
@@ -199,6 +204,7 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
   const uint32_t a_lds0 = sm0 + (uint32_t)((wn * NT * 16 + r16) * ROWB);
   const uint32_t b_lds0 = sm0 + (uint32_t)((BN + wm * 64 + r16) * ROWB);
   const uint32_t g_lds0 = lds_u32(gbuf) + (uint32_t)(g * (F8 ? 64 : 16));
+  bool bad = false;  // a FULL wait timed out: this wave's tiles are stored as NaN from then on
   int s = 0;
   for (int it = 0; it < my_tiles; ++it) {
     const int tile = blockIdx.x + it * gridDim.x;
@@ -213,7 +219,10 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
 
     for (int st = 0; st < nsteps; ++st, ++s) {
       const int slot = s % NS, use = s / NS;
-      wait_flag(full0 + 4 * slot, (unsigned)(NL * (use + 1)));
+      if (!wait_flag(full0 + 4 * slot, (unsigned)(NL * (use + 1)), a.spin_max)) {
+        report_async(a.err, M2S_ASYNC_WS, lane);
+        bad = true;
+      }
       const uint32_t so = (uint32_t)(slot * SLOT);
       if constexpr (F8) {
         // the lane's 32 gates k = 128 st + 32 g + j (bf16) and its MT activation fragments (e4m3 chunks 2g,
@@ -365,8 +374,9 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
           const float4 ws = *reinterpret_cast<const float4*>(a.wscale + n4);
           float r[4];
           unpack_bf16x4(rv[mi][ni], r);
-          const float v[4] = {fmaf(acc[ni][mi][0], ws.x, bb.x) + r[0], fmaf(acc[ni][mi][1], ws.y, bb.y) + r[1],
-                              fmaf(acc[ni][mi][2], ws.z, bb.z) + r[2], fmaf(acc[ni][mi][3], ws.w, bb.w) + r[3]};
+          float v[4] = {fmaf(acc[ni][mi][0], ws.x, bb.x) + r[0], fmaf(acc[ni][mi][1], ws.y, bb.y) + r[1],
+                        fmaf(acc[ni][mi][2], ws.z, bb.z) + r[2], fmaf(acc[ni][mi][3], ws.w, bb.w) + r[3]};
+          if (bad) v[0] = v[1] = v[2] = v[3] = __builtin_nanf("");
           *reinterpret_cast<uint2*>(a.y + (size_t)m * a.cs_out + n4) =
               make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
           if (a.y8) {
@@ -414,8 +424,9 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
         float r[4], rl[4];
         unpack_bf16x4(rv[mi & 1][ni][0], r);
         unpack_bf16x4(rv[mi & 1][ni][1], rl);
-        const float v[4] = {acc[ni][mi][0] + bb.x + (r[0] + rl[0]), acc[ni][mi][1] + bb.y + (r[1] + rl[1]),
-                            acc[ni][mi][2] + bb.z + (r[2] + rl[2]), acc[ni][mi][3] + bb.w + (r[3] + rl[3])};
+        float v[4] = {acc[ni][mi][0] + bb.x + (r[0] + rl[0]), acc[ni][mi][1] + bb.y + (r[1] + rl[1]),
+                      acc[ni][mi][2] + bb.z + (r[2] + rl[2]), acc[ni][mi][3] + bb.w + (r[3] + rl[3])};
+        if (bad) v[0] = v[1] = v[2] = v[3] = __builtin_nanf("");
         uint2 hi, lo;
         split4(v, hi, lo);
         bf16_t* yo = Y + (size_t)m * a.cs_out * 2 + n4;
@@ -456,7 +467,7 @@ bool se_ws_supported(int P, int cs_in, int cs_out) {
 }
 
 void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_pad, const float* bias, const void* gate,
-                  const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes) {
+                  const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes, AsyncReport rep) {
   M2S_CHECK(se_ws_supported(P, cs_in, cs_out) && M % P == 0 && cs_out % 4 == 0, "se_ws: unsupported shape");
   M2S_CHECK(x && w && bias && gate && y && y != res && y != x, "se_ws: operand pointers");
   M2S_CHECK((double)M * cs_in * 4 < 2147483647.0 * 2, "se_ws: input too large");
@@ -473,6 +484,8 @@ void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_p
   a.P = P;
   a.cs_in = cs_in;
   a.cs_out = cs_out;
+  a.spin_max = rep.spin_max;
+  a.err = rep.err;
   // tile / ring variants (M2S_SE_WS_CFG, A/B only; 0 = the default)
   static const int cfg = [] {
     const char* e = std::getenv("M2S_SE_WS_CFG");
@@ -505,7 +518,7 @@ bool se_ws_f8_supported(int P, int cs_in, int cs_out) {
 
 void launch_se_ws_f8(const void* x8, int M, int P, int cs_in, const void* w8, int kp, int n_pad, const float* wscale,
                      const float* bias, const void* gate, const void* res, void* y, int cs_out, hipStream_t s, double flops,
-                     double bytes, void* y8, int ld8) {
+                     double bytes, void* y8, int ld8, AsyncReport rep) {
   M2S_CHECK(se_ws_f8_supported(P, cs_in, cs_out) && kp % 128 == 0 && kp >= cs_in && M % P == 0 && cs_out % 4 == 0,
             "se_ws_f8: unsupported shape");
   M2S_CHECK(!y8 || (ld8 >= cs_out && ld8 % 16 == 0 && y8 != x8), "se_ws_f8: e4m3 output rows");
@@ -528,6 +541,8 @@ void launch_se_ws_f8(const void* x8, int M, int P, int cs_in, const void* w8, in
   a.kp = kp;
   a.y8 = static_cast<uint8_t*>(y8);
   a.ld8 = ld8;
+  a.spin_max = rep.spin_max;
+  a.err = rep.err;
   if (cs_out <= 128) {
     M2S_CHECK(n_pad >= 128, "se_ws_f8: weight rows");
     // 128 x 128 (half a 16x16 image), 4 consumers + 4 loaders, 4 slots: the 8-consumer 256-row tile of the

@@ -71,6 +71,7 @@ def lib():
         "m2s_acoustic_set_chunk": (i, [vp, i]),
         "m2s_acoustic_status": (i, [vp]),
         "m2s_acoustic_set_lstm_spin_limit": (i, [vp, C.c_uint]),
+        "m2s_acoustic_set_ws_spin_limit": (i, [vp, C.c_uint]),
         "m2s_acoustic_workspace_bytes": (sz, [vp, i, i, i, i]),
         "m2s_acoustic_forward": (i, [vp, fp, i, i, i, i, fp, vp, sz, vp]),
         "m2s_effnet_forward": (i, [vp, fp, i, i, i, fp, vp, sz, vp]),
@@ -120,7 +121,7 @@ def check(rc: int) -> None:
 def exported_symbols() -> List[str]:
     return [n for n in ("m2s_abi_version", "m2s_last_error", "m2s_device_check", "m2s_acoustic_create",
                         "m2s_acoustic_destroy", "m2s_acoustic_set_chunk", "m2s_acoustic_status",
-                        "m2s_acoustic_set_lstm_spin_limit", "m2s_acoustic_workspace_bytes",
+                        "m2s_acoustic_set_lstm_spin_limit", "m2s_acoustic_set_ws_spin_limit", "m2s_acoustic_workspace_bytes",
                         "m2s_acoustic_forward", "m2s_effnet_forward", "m2s_effnet_probe", "m2s_bilstm_summerge",
                         "m2s_mel_glue", "m2s_preprocess_frames", "m2s_vocoder_create", "m2s_vocoder_destroy",
                         "m2s_vocoder_workspace_bytes", "m2s_vocoder_forward", "m2s_pipeline_workspace_bytes",

@@ -385,3 +385,25 @@ def test_bilstm_barrier_timeout_is_reported(rt, ac_state, B, dtype):
     y2, _ = eng.bilstm(x)
     eng.check()
     assert torch.isfinite(y2).all()
+
+
+@pytest.mark.parametrize("dtype", ["bf16x3", "fp8"])
+def test_ws_flag_timeout_is_reported(rt, ac_state, dtype):
+    """The persistent CNN kernels' LDS flag waits (ir_ws producers' weight-slot wait, se_ws FULL / FREE) are bounded;
+    forced to time out (spin limit 0 = every wait fails), the launch poisons its outputs and reports it:
+    m2s_acoustic_status -> M2SError naming the flag ring, then a normal limit gives finite features again.
+    bf16x3: ir_ws + the split se_ws; fp8: the e4m3 se_ws."""
+    import ctypes
+    from m2s import _native
+    eng = rt.AcousticEngine(ac_state[1], dtype=dtype, device=DEV)
+    fr = torch.rand(4, 256, 256, device=DEV)
+    _native.check(_native.lib().m2s_acoustic_set_ws_spin_limit(ctypes.c_void_p(eng.handle), 0))
+    f = eng.effnet(fr)
+    with pytest.raises(_native.M2SError, match="flag-ring"):
+        eng.check()
+    assert torch.isnan(f).any()
+    eng.check()  # the report is consumed once
+    _native.check(_native.lib().m2s_acoustic_set_ws_spin_limit(ctypes.c_void_p(eng.handle), 1 << 20))
+    f2 = eng.effnet(fr)
+    eng.check()
+    assert torch.isfinite(f2).all()
