@@ -1,0 +1,369 @@
+// Fused EdgeResidual block of the fp8 engines on e4m3 operands, stride 1 with skip, 56 -> 224 -> 56 channels
+// (channel strides 64 / 224 / 64): tf_efficientnetv2_b2 blocks.2.1/.2 at 32x32 (timm EdgeResidual conv_exp 3x3 +
+// bn1 + SiLU -> conv_pwl 1x1 + bn2 -> + shortcut; mri_acoustic_model.py:28-34 builds the backbone).
+//
+// er8_fused.hip's e4m3 dataflow (block-scaled v_mfma_scale_f32_16x16x128_f8f6f4, unit E8M0 scales, per-output-
+// channel weight scales in the epilogues; the 224-channel map never leaves the registers: after scale + bias +
+// SiLU a lane's accumulators are its conv_pwl B fragments through a host-permuted K) with er2_fused.hip's weight
+// stream (conv_exp's e4m3 weights are 140 KB: they cannot sit in LDS, every tile streams them):
+//   conv_exp: K = (tap, input channel) in steps of 2 taps x 64 channels (5 steps; the last pairs tap 8 with a zero
+//     tap): lane (r16, g) of a B fragment holds tap 2q + (g >> 1), channels 32 (g & 1) .. + 31 of pixel r16,
+//     32 contiguous bytes of the e4m3 halo plane (g & 1).  A K step is one 32 KB ring stage (16 n16 tiles, the
+//     last two zero) instead of er2_fused's four 16 KB bf16 stages: 176 KB streamed per tile against 320 KB.
+//   conv_pwl: 2 K steps of 128 (mid channels 16 (8 kq + b / 4) + 4 g + (b & 3) in byte b of lane g's fragment),
+//     4 n16 tiles, one 16 KB stage.
+// Tile = 16 x 16 output pixels, 8 waves x 2 rows.  Its e4m3 halo (18 x 18 pixels, two 32-channel planes of 32 B a
+// pixel, plane 1 at an odd 16-byte offset: the 16 lanes of every ds_read_b128 lane group hit 16 distinct bank
+// quads) is the producer's e4m3 copy of this block's input (ers2_fused / this kernel's y8), DMA'd a tile ahead;
+// the bf16 shortcut is read from the input in the epilogue.  One barrier per stage (6 per tile); the ring has 3
+// slots, stage s + 2 is DMA'd when stage s starts.  Waits are counted vmcnt's over a fixed per-wave issue order:
+//   stage 0: S(2) x4, H(next) x3 | 1: S(3) x4 | 2: S(4) x4 | 3: S(5) x2 | 4: shortcut loads x8, S(next 0) x4 |
+//   5: S(next 1) x4 | epilogue: 8 stores (16 with y8)
+// (LDS-DMA and stores count together in issue order, MI355X_MICROARCH.md; the DMA is inline asm, so the compiler
+// neither counts it nor drains it before the LDS reads).
+#include <algorithm>
+
+#include "kernels.hpp"
+#include "prof.hpp"
+
+namespace m2s {
+namespace {
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int E8M0_ONE = 0x7f7f7f7f;
+
+__device__ __attribute__((aligned(16))) uint4 g_er8w_zero[4];  // DMA source for padding pixels
+
+constexpr int EW_T = 16, EW_HW = 18, EW_HPIX = EW_HW * EW_HW;  // 16 x 16 tile, 18 x 18 halo
+constexpr int EW_MID = 224, EW_NT = 14, EW_ON = 4, EW_QS = 5;  // mid channels, n16 tiles, out n16 tiles, K steps
+constexpr int EW_STAGE = 32 * 1024;                           // ring slot: a conv_exp K step, 16 n16 x 2 KB
+constexpr int EW_SLOTS = 3;
+constexpr int EW_PLANE = 12 * 1024;                           // halo plane: 384 pixels x 32 B (12 DMA pieces)
+constexpr int EW_PB = EW_PLANE + 16;                          // plane 1: an odd 16-byte offset from plane 0
+constexpr int EW_BUF = EW_PB + EW_PLANE + 16;                 // 24 592 B (a multiple of 32)
+constexpr int EW_HALO0 = EW_SLOTS * EW_STAGE;
+constexpr int EW_ZERO = EW_HALO0 + 2 * EW_BUF;                // 32 zero bytes (the padding tap's fragment)
+constexpr int EW_SB = EW_ZERO + 32;                           // [224] conv_exp scales, [224] bn1 biases
+constexpr int EW_SB2 = EW_SB + 2 * EW_MID * 4;                // [64] conv_pwl scales, [64] bn2 biases
+constexpr int EW_LDS = EW_SB2 + 2 * 64 * 4;
+constexpr int EW_NST = 6;                                     // stages per tile
+static_assert(EW_LDS <= 160 * 1024, "LDS budget");
+
+struct Er8wArgs {
+  const bf16_t* x;      // (N, H, W, 64) bf16 (the shortcut)
+  const uint8_t* x8;    // (N, H, W, 64) e4m3 copy of x (the conv_exp operand)
+  const uint8_t* wst;   // stage stream: 5 x [16 n16][2 halves][64 lanes][16 B], then [4 on][2 kq][2 halves][64][16]
+  const float* sexp;    // [224]
+  const float* bexp;    // [224]
+  const float* spwl;    // [64] (1 past 56)
+  const float* bpwl;    // [64] (0 past 56)
+  bf16_t* y;            // (N, H, W, 64)
+  uint8_t* y8;          // e4m3 copy of y (the next block's x8) or null
+  int N, H, W, tiles_x, tiles_y;
+};
+
+__device__ __forceinline__ void dma16(const void* src, uint32_t lds_wave_base) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds_wave_base)
+               : "memory");
+}
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ i32x8 cat8(u32x4 a, u32x4 b) {
+  return i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+}
+
+template <bool Y8>
+__global__ void __launch_bounds__(512, 1) er8w_fused_kernel(const Er8wArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NSTORE = Y8 ? 16 : 8;  // stores per wave and tile
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int tpi = a.tiles_x * a.tiles_y, ntiles = a.N * tpi;
+  const uint32_t sm0 = lds_off(smem);
+
+  // stage ls of the stream -> ring slot: conv_exp K steps 4 pieces a wave (n16 tiles 2 wave, 2 wave + 1), the
+  // conv_pwl stage 2 pieces a wave
+  auto stage_dma = [&](int ls, int slot) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));  // rebuilt per call: hoisted lane offsets cost registers
+    const uint32_t dst = sm0 + (uint32_t)(slot * EW_STAGE);
+    if (ls < EW_QS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int piece = wave * 4 + j;
+        dma16(a.wst + ((size_t)ls * 32 + piece) * 1024 + ln * 16, dst + piece * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int piece = wave * 2 + j;
+        dma16(a.wst + ((size_t)EW_QS * 32 + piece) * 1024 + ln * 16, dst + piece * 1024);
+      }
+    }
+  };
+  // tile T's e4m3 halo: 2 planes x 12 pieces of 32 pixels (a lane = half a pixel), 3 pieces a wave
+  auto halo_dma = [&](int T, int buf) {
+    const int n = T / tpi, tr = T - n * tpi;
+    const int ty0 = (tr / a.tiles_x) * EW_T - 1, tx0 = (tr - (tr / a.tiles_x) * a.tiles_x) * EW_T - 1;
+    const uint8_t* xi = a.x8 + (size_t)n * a.H * a.W * 64;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int piece = wave * 3 + j, pl = piece / 12, pb = piece - pl * 12;
+      const int hp = pb * 32 + (ln >> 1), hy = hp / EW_HW, hx = hp - hy * EW_HW;
+      const int iy = ty0 + hy, ix = tx0 + hx;
+      const void* src = g_er8w_zero;
+      if (hp < EW_HPIX && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+        src = xi + ((size_t)iy * a.W + ix) * 64 + pl * 32 + (ln & 1) * 16;
+      dma16(src, sm0 + (uint32_t)(EW_HALO0 + buf * EW_BUF + (pl ? EW_PB : 0) + pb * 1024));
+    }
+  };
+
+  // ---- once: scales and biases -> LDS, the zero slot; the first tile's stages 0, 1 and halo ---------------------
+  float* sb = reinterpret_cast<float*>(smem + EW_SB);
+  float* sb2 = reinterpret_cast<float*>(smem + EW_SB2);
+  if (tid < EW_MID) sb[tid] = a.sexp[tid];
+  else if (tid < 2 * EW_MID) sb[tid] = a.bexp[tid - EW_MID];
+  else if (tid < 2 * EW_MID + 64) sb2[tid - 2 * EW_MID] = a.spwl[tid - 2 * EW_MID];
+  else if (tid < 2 * EW_MID + 128) sb2[tid - 2 * EW_MID] = a.bpwl[tid - 2 * EW_MID - 64];
+  else if (tid < 2 * EW_MID + 130) *reinterpret_cast<uint4*>(smem + EW_ZERO + (tid - 2 * EW_MID - 128) * 16) = make_uint4(0u, 0u, 0u, 0u);
+  if ((int)blockIdx.x < ntiles) {
+    stage_dma(0, 0);
+    stage_dma(1, 1);
+    halo_dma(blockIdx.x, 0);
+  }
+  wait_vm<0>();
+  __syncthreads();
+
+  int gs = 0;  // global stage counter: ring slot gs % 3
+  for (int it = 0, tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
+    const bool hn = tile + (int)gridDim.x < ntiles;  // has a next tile (uniform)
+    const int buf = it & 1;
+    const uint32_t hb = sm0 + (uint32_t)(EW_HALO0 + buf * EW_BUF);
+    const int n = tile / tpi, tr = tile - n * tpi;
+    const int oy0 = (tr / a.tiles_x) * EW_T, ox = (tr - (tr / a.tiles_x) * a.tiles_x) * EW_T + r16;
+
+    f32x4 acc[2][EW_NT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int nt = 0; nt < EW_NT; ++nt) acc[i][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // ---- stage s of this tile landed for every wave: counted wait (the table in the header), barrier, then this
+    // stage's DMA issue; returns the lane's address in the stage's ring slot
+    uint2 skip[2][EW_ON];
+    auto begin_stage = [&](int s) -> uint32_t {
+      if (s == 0) {
+        if (it == 0) wait_vm<0>();
+        else wait_vm<4 + NSTORE>();
+      } else if (s == 1) {
+        if (hn) wait_vm<NSTORE + 7>();
+        else wait_vm<NSTORE + 4>();
+      } else if (s == 2) {
+        if (hn) wait_vm<7>();
+        else wait_vm<4>();
+      } else if (s == 3) {
+        wait_vm<4>();
+      } else if (s == 4) {
+        wait_vm<2>();
+      } else {
+        if (hn) wait_vm<8 + 4>();
+        else wait_vm<8>();
+      }
+      __builtin_amdgcn_s_barrier();  // slot (gs - 1) % 3 and, at s = 0, the other halo buffer are free
+      asm volatile("" ::: "memory");
+      const int slot = gs % EW_SLOTS, nslot = (gs + 2) % EW_SLOTS;
+      if (s + 2 < EW_NST) stage_dma(s + 2, nslot);
+      if (s == 0 && hn) halo_dma(tile + gridDim.x, buf ^ 1);
+      if (s == 4) {  // the shortcut rows (bf16 x) a stage ahead of their use, then the next tile's stage 0
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const size_t px = ((size_t)n * a.H + oy0 + 2 * wave + i) * a.W + ox;
+#pragma unroll
+          for (int on = 0; on < EW_ON; ++on) skip[i][on] = *reinterpret_cast<const uint2*>(a.x + px * 64 + on * 16 + 4 * (ln >> 4));
+        }
+        asm volatile("" ::: "memory");
+        if (hn) stage_dma(0, nslot);
+      }
+      ++gs;
+      int ln = lane;  // rebuilt per stage: the lane's LDS offsets hoisted out of the tile loop spilled
+      asm volatile("" : "+v"(ln));
+      return sm0 + (uint32_t)(slot * EW_STAGE) + ln * 16;
+    };
+
+    // ================= conv_exp: K steps q = 0..4 (taps 2q, 2q + 1 x 64 channels) =================
+#pragma unroll 1
+    for (int q = 0; q < EW_QS; ++q) {
+      const uint32_t ws = begin_stage(q);
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const int g = ln >> 4, r16 = ln & 15;
+      const int tap = 2 * q + (g >> 1), ky = tap / 3, kx = tap - ky * 3;
+      u32x4 b0[2], b1[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t o = tap < 9 ? hb + ((g & 1) ? EW_PB : 0) + (((2 * wave + i + ky) * EW_HW + r16 + kx) * 32)
+                                   : sm0 + EW_ZERO;
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16" : "=&v"(b0[i]), "=&v"(b1[i]) : "v"(o) : "memory");
+      }
+      u32x4 a0[3], a1[3];
+      auto read_a = [&](int nt) {
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024"
+                     : "=&v"(a0[nt % 3]), "=&v"(a1[nt % 3])
+                     : "v"(ws + nt * 2048)
+                     : "memory");
+      };
+      read_a(0);
+      read_a(1);
+      i32x8 bx[2];
+#pragma unroll
+      for (int nt = 0; nt < EW_NT; ++nt) {
+        if (nt + 2 < EW_NT) read_a(nt + 2);
+        // reads younger than A(nt): A(nt + 1), A(nt + 2) (two each)
+        if (nt + 2 < EW_NT) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(a0[nt % 3]), "+v"(a1[nt % 3]));
+        else if (nt + 1 < EW_NT) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(a0[nt % 3]), "+v"(a1[nt % 3]));
+        else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0[nt % 3]), "+v"(a1[nt % 3]));
+        if (nt == 0) {  // the B reads were issued before every A read
+          asm volatile("" : "+v"(b0[0]), "+v"(b1[0]), "+v"(b0[1]), "+v"(b1[1]));
+          bx[0] = cat8(b0[0], b1[0]);
+          bx[1] = cat8(b0[1], b1[1]);
+        }
+        const i32x8 af = cat8(a0[nt % 3], a1[nt % 3]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bx[i], acc[i][nt], 0, 0, 0, E8M0_ONE, 0, E8M0_ONE);
+        // keep the MFMAs of n16 tile nt ahead of the fragment reads of nt + 3
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+
+    // ================= stage 5: scale + bias + SiLU -> e4m3 conv_pwl B fragments; conv_pwl; + bias + shortcut ======
+    const uint32_t ws = begin_stage(5);
+    {
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const int g = ln >> 4;
+      if (hn) stage_dma(1, (gs + 1) % EW_SLOTS);  // = (stage gs - 1) + 2
+      // the shortcut loads (issued at stage 4, before the next tile's stages 0 and 1)
+      if (hn) wait_vm<8>();
+      else wait_vm<0>();
+      // per row and conv_pwl K step kq: the e4m3 B fragment of mid channels 16 (8 kq .. 8 kq + 7) + 4 g + e (scale,
+      // bn1 bias, SiLU), then the step's 4 MFMAs (one fragment live at a time)
+      const uint32_t sb0 = sm0 + EW_SB + (uint32_t)(16 * g);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        f32x4 o[EW_ON];
+#pragma unroll
+        for (int on = 0; on < EW_ON; ++on) o[on] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kq = 0; kq < 2; ++kq) {
+          i32x8 mid;
+#pragma unroll
+          for (int ntp = 0; ntp < 8; ntp += 2) {
+            const int nt = 8 * kq + ntp;
+            if (nt >= EW_NT) {  // mid channels past 223: zero bytes (zero conv_pwl weights too)
+              mid[ntp] = mid[ntp + 1] = 0;
+              continue;
+            }
+            u32x4 s0, s1, c0, c1;  // scales and bn1 biases of channels 16 nt + 4 g .. + 3 and 16 (nt + 1) + 4 g ..
+            asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:896\n\t"
+                         "ds_read_b128 %3, %4 offset:960\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&v"(s0), "=&v"(s1), "=&v"(c0), "=&v"(c1)
+                         : "v"(sb0 + (uint32_t)(nt * 64))
+                         : "memory");
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = silu_e4m3(acc[i][nt][e] * __uint_as_float(s0[e]) + __uint_as_float(c0[e]));
+              v[4 + e] = silu_e4m3(acc[i][nt + 1][e] * __uint_as_float(s1[e]) + __uint_as_float(c1[e]));
+            }
+            const uint2 m = e4m3x8_nosat(v);
+            mid[ntp] = (int)m.x;
+            mid[ntp + 1] = (int)m.y;
+          }
+#pragma unroll
+          for (int on = 0; on < EW_ON; ++on) {
+            u32x4 w0, w1;
+            asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&v"(w0), "=&v"(w1)
+                         : "v"(ws + (on * 2 + kq) * 2048)
+                         : "memory");
+            o[on] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(cat8(w0, w1), mid, o[on], 0, 0, 0, E8M0_ONE, 0, E8M0_ONE);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const size_t px = ((size_t)n * a.H + oy0 + 2 * wave + i) * a.W + ox;
+#pragma unroll
+        for (int on = 0; on < EW_ON; ++on) {
+          const int c4 = on * 16 + 4 * g;
+          const float4 sc = *reinterpret_cast<const float4*>(sb2 + c4);
+          const float4 bb = *reinterpret_cast<const float4*>(sb2 + 64 + c4);
+          const uint2 r = skip[i][on];
+          const float v0 = o[on][0] * sc.x + bb.x + __uint_as_float(r.x << 16);
+          const float v1 = o[on][1] * sc.y + bb.y + __uint_as_float(r.x & 0xffff0000u);
+          const float v2 = o[on][2] * sc.z + bb.z + __uint_as_float(r.y << 16);
+          const float v3 = o[on][3] * sc.w + bb.w + __uint_as_float(r.y & 0xffff0000u);
+          const uint2 yb = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+          // every tile is whole (H, W multiples of 16): exactly 8 stores (16 with y8) per wave and tile
+          *reinterpret_cast<uint2*>(a.y + px * 64 + c4) = yb;
+          if constexpr (Y8) *reinterpret_cast<uint32_t*>(a.y8 + px * 64 + c4) = e4m3x4_bf16(yb);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  wait_vm<0>();
+}
+
+}  // namespace
+
+bool er8w_fused_supported(int H, int W, int cs_in, int mid, int cout) {
+  return cs_in == 64 && mid == EW_MID && cout > 32 && cout <= 64 && H % EW_T == 0 && W % EW_T == 0 && H > 0 && W > 0;
+}
+
+size_t er8w_stream_bytes() { return (size_t)EW_QS * EW_STAGE + 16 * 1024; }
+
+void launch_er8w_fused(const bf16_t* x, const uint8_t* x8, int N, int H, int W, const uint8_t* wst, const float* sexp,
+                       const float* bexp, const float* spwl, const float* bpwl, bf16_t* y, uint8_t* y8, double flops,
+                       double bytes, hipStream_t s) {
+  M2S_CHECK(er8w_fused_supported(H, W, 64, EW_MID, 64) && N > 0, "er8w_fused: unsupported shape");
+  M2S_CHECK(x && x8 && wst && sexp && bexp && spwl && bpwl && y, "er8w_fused: operand pointers");
+  M2S_CHECK(static_cast<const void*>(y) != static_cast<const void*>(x) && static_cast<const void*>(y8) != static_cast<const void*>(x8),
+            "er8w_fused: in-place");
+  Er8wArgs a;
+  a.x = x;
+  a.x8 = x8;
+  a.wst = wst;
+  a.sexp = sexp;
+  a.bexp = bexp;
+  a.spwl = spwl;
+  a.bpwl = bpwl;
+  a.y = y;
+  a.y8 = y8;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.tiles_x = W / EW_T;
+  a.tiles_y = H / EW_T;
+  auto k = y8 ? er8w_fused_kernel<true> : er8w_fused_kernel<false>;
+  allow_lds(reinterpret_cast<const void*>(k));
+  const int grid = std::min(N * a.tiles_x * a.tiles_y, device_cus());
+  ProfScope ps(y8 ? "er8w_fused_kernel<true>" : "er8w_fused_kernel<false>", flops, bytes, s);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(512), EW_LDS, s, a);
+  M2S_HIP(hipGetLastError());
+}
+
+}  // namespace m2s

@@ -167,6 +167,15 @@ void launch_er8_fused(const bf16_t* x, int N, int H, int W, const uint8_t* wexp,
 // (er2_fused.hip)
 bool er2_fused_supported(int H, int W, int cs_in, int mid, int cout, int kp_exp, int kp_pwl);
 int er2_stage_elems();
+// fp8 engines: the same block (56 -> 224 -> 56, 32x32, skip) on e4m3 operands (er8w_fused.hip): x8 = the input as
+// e4m3 bytes (N, H, W, 64) written by the producer block, wst = the e4m3 stage stream (er8w_stream_bytes(); conv_exp
+// 5 K steps of [16 n16][2][64][16 B], then conv_pwl [4][2][2][64][16 B] with the permuted K), per-channel scales
+// sexp [224] / spwl [64]; y8 (optional) = e4m3 of y for the next such block.
+bool er8w_fused_supported(int H, int W, int cs_in, int mid, int cout);
+size_t er8w_stream_bytes();
+void launch_er8w_fused(const bf16_t* x, const uint8_t* x8, int N, int H, int W, const uint8_t* wst, const float* sexp,
+                       const float* bexp, const float* spwl, const float* bpwl, bf16_t* y, uint8_t* y8, double flops,
+                       double bytes, hipStream_t s);
 void launch_er2_fused(const bf16_t* x, int N, int H, int W, const bf16_t* wst, const float* bexp, const float* bpwl,
                       bf16_t* y, double flops, double bytes, hipStream_t s);
 

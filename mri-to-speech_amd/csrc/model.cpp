@@ -86,6 +86,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_F8_EXPAND")) f8_expand_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_ER")) f8_er_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER8_X8")) er8_x8_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_F8_ER2")) f8_er2_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_FUSED")) se_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER_FUSED")) er_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_SP")) se_sp_ = std::strcmp(e, "0") != 0;  // A/B only
@@ -308,6 +309,52 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
                 }
           b.er_wexp = arena_.add_vec(st);
           b.er_frag = true;
+          if (dtype == M2S_DT_FP8 && er8w_fused_supported(32, 32, b.c1.cs_in, b.mid, b.cout)) {
+            // er8w_fused.hip stage stream: conv_exp K step q = [nt 0..15][half][lane (r16, g)][16 B], byte 16 half + j =
+            // tap 2q + (g >> 1), input channel 32 (g & 1) + 16 half + j of output channel 16 nt + r16 (zero past tap 8,
+            // channel 55, mid channel 223); conv_pwl [on][kq][half][lane][16 B], byte b = 16 half + j = mid channel
+            // 16 (8 kq + b / 4) + 4 g + (b & 3) of output channel 16 on + r16.  Weights / per-channel scale s = amax / 448
+            const int mid = b.mid, co = b.cout;
+            std::vector<float> s1(mid, 1.f), s2(64, 1.f);
+            auto wexp_at = [&](int n, int c, int t) { return we[((size_t)n * cin + c) * 9 + t] * e1.a[n]; };
+            for (int n = 0; n < mid; ++n) {
+              float amax = 0.f;
+              for (int c = 0; c < cin; ++c)
+                for (int t = 0; t < 9; ++t) amax = std::max(amax, std::fabs(wexp_at(n, c, t)));
+              if (amax > 0.f) s1[n] = amax / 448.f;
+            }
+            for (int o = 0; o < co; ++o) {
+              float amax = 0.f;
+              for (int c = 0; c < mid; ++c) amax = std::max(amax, std::fabs(wq[(size_t)o * mid + c] * e2.a[o]));
+              if (amax > 0.f) s2[o] = amax / 448.f;
+            }
+            std::vector<uint8_t> w8(er8w_stream_bytes(), 0);
+            for (int q2 = 0; q2 < 5; ++q2)
+              for (int nt = 0; nt < 16; ++nt)
+                for (int h = 0; h < 2; ++h)
+                  for (int ln = 0; ln < 64; ++ln)
+                    for (int j = 0; j < 16; ++j) {
+                      const int g4 = ln >> 4, t = 2 * q2 + (g4 >> 1), c = 32 * (g4 & 1) + 16 * h + j, n = 16 * nt + (ln & 15);
+                      if (t < 9 && c < cin && n < mid)
+                        w8[(((((size_t)q2 * 16 + nt) * 2 + h) * 64 + ln) * 16) + j] = e4m3_bits_host(e4m3_host(wexp_at(n, c, t) / s1[n]));
+                    }
+            const size_t pw0 = (size_t)5 * 32 * 1024;
+            for (int on = 0; on < 4; ++on)
+              for (int kq = 0; kq < 2; ++kq)
+                for (int h = 0; h < 2; ++h)
+                  for (int ln = 0; ln < 64; ++ln)
+                    for (int j = 0; j < 16; ++j) {
+                      const int o = 16 * on + (ln & 15), bb = 16 * h + j, ntp = 8 * kq + (bb >> 2);
+                      const int c = 16 * ntp + 4 * (ln >> 4) + (bb & 3);
+                      if (o < co && ntp < mid / 16)
+                        w8[pw0 + (((((size_t)on * 2 + kq) * 2 + h) * 64 + ln) * 16) + j] =
+                            e4m3_bits_host(e4m3_host(wq[(size_t)o * mid + c] * e2.a[o] / s2[o]));
+                    }
+            b.er8w_w = arena_.add_vec(w8);
+            b.er8w_sexp = arena_.add_vec(s1);
+            b.er8w_spwl = arena_.add_vec(s2);
+            b.er8w = true;
+          }
         } else if (pdt == M2S_DT_BF16 && b.stride == 2 && k == 3 &&
                    ers2_fused_supported(8, 16, b.c1.cs_in, b.mid, chan_stride(b.cout), b.c1.kp, b.c2.kp)) {
           // ers2_fused.hip: conv_exp [k-step][n16][lane][8] (CIN 16: lane groups 0-1 tap 2s, 2-3 tap
@@ -489,6 +536,7 @@ size_t Acoustic::effnet_x8(int H, int W) const {
     same_pad(ow, 3, b.stride, &nw, &pw);
     if (b.f8_pw && f8_expand_) mx = std::max(mx, (size_t)nh * nw * b.f8x_kp);  // stride 1: the block input's map
     if (b.er8 && f8_er_) mx = std::max(mx, (size_t)nh * nw * 32);              // er8_fused x8 / y8 (N, H, W, 32)
+    if (b.er8w && f8_er_) mx = std::max(mx, (size_t)nh * nw * 64);             // er8w_fused x8 / y8 (N, H, W, 64)
     oh = nh;
     ow = nw;
   }
@@ -608,8 +656,12 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
       // the next block takes an e4m3 expand operand (fp8 engines, stride-1 IR blocks)
       const bool want8 = X8[0] && f8_expand_ && k + 1 < blocks_.size() && blocks_[k + 1].f8_pw && blocks_[k + 1].stride == 1;
       // the next block is an e4m3 EdgeResidual (er8_fused): this block also stores its output as e4m3 bytes
-      uint8_t* const er8_next = X8[0] && f8_er_ && er8_x8_ && k + 1 < blocks_.size() && blocks_[k + 1].er8 ? (cur8 == X8[0] ? X8[1] : X8[0])
-                                                                                              : nullptr;
+      // (er8w_fused, blocks.2.1/.2, always takes its e4m3 operand from the producer; M2S_ER8_X8=0 switches only
+      // er8_fused to its in-kernel conversion)
+      uint8_t* const er8_next = X8[0] && f8_er_ && k + 1 < blocks_.size() &&
+                                        ((er8_x8_ && blocks_[k + 1].er8) || (f8_er2_ && blocks_[k + 1].er8w))
+                                    ? (cur8 == X8[0] ? X8[1] : X8[0])
+                                    : nullptr;
       int nh, nw, qt, ql;
       same_pad(oh, 3, b.stride, &nh, &qt);
       same_pad(ow, 3, b.stride, &nw, &ql);
@@ -659,6 +711,17 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                         static_cast<const bf16_t*>(arena_.ptr(b.er_wexp)), b.c1.b,
                         static_cast<const bf16_t*>(arena_.ptr(b.er_wpwl)), b.c2.b, reinterpret_cast<bf16_t*>(nxt),
                         2.0 * px * b.mid * (9.0 * b.cin + b.cout), 2.0 * px * (2.0 * b.cin) + 2.0 * (9.0 * 32 * 128 + 128 * 32), s);
+      } else if (b.type == 1 && std::is_same<T, bf16_t>::value && er_fused_ && f8_er_ && f8_er2_ && b.er8w && cur8 &&
+                 er8w_fused_supported(nh, nw, b.c1.cs_in, b.mid, b.cout)) {
+        const double px = (double)nc * nh * nw;
+        uint8_t* y8 = er8_next && blocks_[k + 1].er8w ? er8_next : nullptr;
+        launch_er8w_fused(reinterpret_cast<const bf16_t*>(cur), cur8, nc, nh, nw, static_cast<const uint8_t*>(arena_.ptr(b.er8w_w)),
+                          static_cast<const float*>(arena_.ptr(b.er8w_sexp)), b.c1.b,
+                          static_cast<const float*>(arena_.ptr(b.er8w_spwl)), b.c2.b, reinterpret_cast<bf16_t*>(nxt), y8,
+                          2.0 * px * b.mid * (9.0 * b.cin + b.cout),
+                          // e4m3 input + bf16 shortcut + bf16 output (+ its e4m3 copy) + the weights once
+                          px * (b.cin + 2.0 * b.cin + 2.0 * b.cout + (y8 ? b.cout : 0.0)) + (9.0 * b.cin + b.cout) * b.mid, s);
+        next8 = y8;
       } else if (b.type == 1 && std::is_same<T, bf16_t>::value && er_fused_ && b.er_frag &&
                  er2_fused_supported(nh, nw, b.c1.cs_in, b.mid, b.cout, b.c1.kp, b.c2.kp)) {
         const double px = (double)nc * nh * nw;
@@ -669,7 +732,10 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                  ers2_fused_supported(nh, nw, b.c1.cs_in, b.mid, chan_stride(b.cout), b.c1.kp, b.c2.kp)) {
         const double px = (double)nc * nh * nw;
         // fp8: an e4m3 copy of the output for an er8_fused next block (the copy is (N, OH, OW, cs_out) bytes)
-        uint8_t* y8 = er8_next && chan_stride(b.cout) == 32 && er8_fused_supported(nh, nw, 32, 128, 32) ? er8_next : nullptr;
+        uint8_t* y8 = er8_next && ((chan_stride(b.cout) == 32 && blocks_[k + 1].er8 && er8_fused_supported(nh, nw, 32, 128, 32)) ||
+                                   (chan_stride(b.cout) == 64 && blocks_[k + 1].er8w && er8w_fused_supported(nh, nw, 64, 224, b.cout)))
+                          ? er8_next
+                          : nullptr;
         launch_ers2_fused(reinterpret_cast<const bf16_t*>(cur), nc, oh, ow, nh, nw, qt, ql, b.c1.cs_in, b.mid,
                           chan_stride(b.cout), static_cast<const bf16_t*>(arena_.ptr(b.er_wexp)), b.c1.b,
                           static_cast<const bf16_t*>(arena_.ptr(b.er_wpwl)), b.c2.b, reinterpret_cast<bf16_t*>(nxt),

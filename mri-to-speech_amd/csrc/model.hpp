@@ -102,6 +102,7 @@ class Acoustic {
   bool ir_ws_ = true;     // split fp32: the persistent warp-specialised form of it (env M2S_IR_WS=0 disables)
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
   bool f8_er_ = true;            // fp8: EdgeResidual blocks.1.1/.2 on e4m3 (env M2S_F8_ER=0: bf16 er_fused)
+  bool f8_er2_ = true;           // fp8: EdgeResidual blocks.2.1/.2 on e4m3 (er8w_fused; env M2S_F8_ER2=0: bf16 er2_fused)
   bool er8_x8_ = true;           // ... their input as e4m3 bytes from the producer (env M2S_ER8_X8=0: converted
                                  // in er8_fused; the same bytes, test_fp8_er8_e4m3_handoff_is_exact)
   bool f8_expand_ = true;        // fp8: the stride-1 IR expand on e4m3 (env M2S_F8_EXPAND=0: bf16 expand)
@@ -139,6 +140,9 @@ class Acoustic {
     // fp8 engines, er 32 -> 128 -> 32 stride 1 on e4m3 (er8_fused.hip): fragments, per-channel scales
     size_t er8_wexp = 0, er8_sexp = 0, er8_wpwl = 0, er8_spwl = 0;
     bool er8 = false;
+    // fp8 engines, er 56 -> 224 -> 56 stride 1 on e4m3 (er8w_fused.hip): stage stream, per-channel scales
+    size_t er8w_w = 0, er8w_sexp = 0, er8w_spwl = 0;
+    bool er8w = false;
     size_t er_sp_w = 0;  // split fp32 er stride 1: er_sp_fused.hip stage stream
     bool er_sp = false;
     bool ers_sp = false;  // split fp32 er stride 2 (blocks.1.0): er_wexp / er_wpwl in [hi/lo] fragment order
