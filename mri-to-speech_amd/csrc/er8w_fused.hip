@@ -133,11 +133,13 @@ __global__ void __launch_bounds__(512, 1) er8w_fused_kernel(const Er8wArgs a) {
   // ---- once: scales and biases -> LDS, the zero slot; the first tile's stages 0, 1 and halo ---------------------
   float* sb = reinterpret_cast<float*>(smem + EW_SB);
   float* sb2 = reinterpret_cast<float*>(smem + EW_SB2);
-  if (tid < EW_MID) sb[tid] = a.sexp[tid];
-  else if (tid < 2 * EW_MID) sb[tid] = a.bexp[tid - EW_MID];
-  else if (tid < 2 * EW_MID + 64) sb2[tid - 2 * EW_MID] = a.spwl[tid - 2 * EW_MID];
-  else if (tid < 2 * EW_MID + 128) sb2[tid - 2 * EW_MID] = a.bpwl[tid - 2 * EW_MID - 64];
-  else if (tid < 2 * EW_MID + 130) *reinterpret_cast<uint4*>(smem + EW_ZERO + (tid - 2 * EW_MID - 128) * 16) = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = tid; i < 2 * EW_MID + 128 + 2; i += 512) {  // 578 items over 512 threads
+    if (i < EW_MID) sb[i] = a.sexp[i];
+    else if (i < 2 * EW_MID) sb[i] = a.bexp[i - EW_MID];
+    else if (i < 2 * EW_MID + 64) sb2[i - 2 * EW_MID] = a.spwl[i - 2 * EW_MID];
+    else if (i < 2 * EW_MID + 128) sb2[i - 2 * EW_MID] = a.bpwl[i - 2 * EW_MID - 64];
+    else *reinterpret_cast<uint4*>(smem + EW_ZERO + (i - 2 * EW_MID - 128) * 16) = make_uint4(0u, 0u, 0u, 0u);
+  }
   if ((int)blockIdx.x < ntiles) {
     stage_dma(0, 0);
     stage_dma(1, 1);
