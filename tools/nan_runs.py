@@ -13,7 +13,7 @@ from m2s import _native, runtime as rt, synth  # noqa: E402
 DEV = torch.device("cuda", 0)
 st = synth.synth_acoustic_state(3)
 clean = torch.from_numpy(synth.synth_frames(1, 4, seed=2)[0]).to(DEV)
-taps = list(range(1, 30))
+taps = list(range(1, 29))
 for dtype in ("fp8", "bf16", "bf16x3"):
     for mode in ("nanframe", "timeout"):
         eng = rt.AcousticEngine(st, dtype=dtype, device=DEV)
