@@ -49,7 +49,9 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int CIN, int MID, int CO>
+// Y8: also store y's e4m3 bytes (a.y8).  A template parameter, so the per-tile store count the counted vmcnt wait
+// at the top of the tile loop relies on (ON, 2 ON with y8) is fixed when the kernel is compiled.
+template <int CIN, int MID, int CO, bool Y8>
 __global__ void __launch_bounds__(512, (CIN == 16 ? 2 : 1)) ers2_fused_kernel(const Es2Args a) {
   constexpr int NCH = CIN / 8;             // input chunks
   constexpr int KS = (9 * CIN + 31) / 32;  // conv_exp k-steps
@@ -110,7 +112,7 @@ __global__ void __launch_bounds__(512, (CIN == 16 ? 2 : 1)) ers2_fused_kernel(co
   for (int it = 0, tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
     char* hb = hbuf + (it & 1) * BUF;
     if (it > 0) {
-      if (a.y8) wait_vm<2 * ON>();  // this tile's halo landed (the younger ops are the last tile's stores)
+      if constexpr (Y8) wait_vm<2 * ON>();  // this tile's halo landed (the younger ops are the last tile's stores)
       else wait_vm<ON>();
       __builtin_amdgcn_s_barrier();  // ... for every wave; every wave is done with the other buffer
       asm volatile("" ::: "memory");  // (a raw barrier: __syncthreads would also wait for the stores)
@@ -163,7 +165,7 @@ __global__ void __launch_bounds__(512, (CIN == 16 ? 2 : 1)) ers2_fused_kernel(co
       const uint2 yb = make_uint2(pack_bf16x2(o[on][0] + bp[on].x, o[on][1] + bp[on].y),
                                   pack_bf16x2(o[on][2] + bp[on].z, o[on][3] + bp[on].w));
       *reinterpret_cast<uint2*>(a.y + px * CO + c4) = yb;
-      if (a.y8) *reinterpret_cast<uint32_t*>(a.y8 + px * CO + c4) = e4m3x4_bf16(yb);
+      if constexpr (Y8) *reinterpret_cast<uint32_t*>(a.y8 + px * CO + c4) = e4m3x4_bf16(yb);
     }
   }
   wait_vm<0>();
@@ -320,19 +322,19 @@ void launch_cfg_sp(const Es2Args& a, double flops, double bytes, hipStream_t s) 
   M2S_HIP(hipGetLastError());
 }
 
-template <int CIN, int MID, int CO>
+template <int CIN, int MID, int CO, bool Y8>
 void launch_cfg(const Es2Args& a, double flops, double bytes, hipStream_t s) {
   constexpr int KS = (9 * CIN + 31) / 32;
   const size_t lds = (size_t)KS * (MID / 16) * 1024 + 2 * (size_t)(CIN / 8) * 2 * ES_PLANE;
-  allow_lds(reinterpret_cast<const void*>(&ers2_fused_kernel<CIN, MID, CO>));
+  allow_lds(reinterpret_cast<const void*>(&ers2_fused_kernel<CIN, MID, CO, Y8>));
   M2S_CHECK(lds <= 160 * 1024, "ers2_fused: LDS budget");
   const int cus = device_cus();
   // CIN 16: 60 KB of LDS and < 128 VGPRs, so two workgroups per CU
   const int grid = std::min(a.N * a.tiles_x * a.tiles_y, (CIN == 16 ? 2 : 1) * cus);
   char name[64];
-  snprintf(name, sizeof(name), "ers2_fused_kernel<%d, %d, %d>", CIN, MID, CO);
+  snprintf(name, sizeof(name), "ers2_fused_kernel<%d, %d, %d, %s>", CIN, MID, CO, Y8 ? "true" : "false");
   ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((ers2_fused_kernel<CIN, MID, CO>), dim3(grid), dim3(512), lds, s, a);
+  hipLaunchKernelGGL((ers2_fused_kernel<CIN, MID, CO, Y8>), dim3(grid), dim3(512), lds, s, a);
   M2S_HIP(hipGetLastError());
 }
 
@@ -394,10 +396,13 @@ void launch_ers2_fused(const bf16_t* x, int N, int H, int W, int OH, int OW, int
   a.pad_l = pad_l;
   a.tiles_x = OW / ES_TW;
   a.tiles_y = OH / ES_TH;
-  if (cs_in == 16)
-    launch_cfg<16, 64, 32>(a, flops, bytes, s);
-  else
-    launch_cfg<32, 128, 64>(a, flops, bytes, s);
+  if (cs_in == 16) {
+    if (y8) launch_cfg<16, 64, 32, true>(a, flops, bytes, s);
+    else launch_cfg<16, 64, 32, false>(a, flops, bytes, s);
+  } else {
+    if (y8) launch_cfg<32, 128, 64, true>(a, flops, bytes, s);
+    else launch_cfg<32, 128, 64, false>(a, flops, bytes, s);
+  }
 }
 
 }  // namespace m2s

@@ -384,11 +384,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) gemm128_kernel(const G128Args
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = a.accum == 2 ? (p[j] + v[j]) / a.accum_div : p[j] + v[j];
       }
-      if (SE || Y) *reinterpret_cast<uint2*>(Y + o) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-      if (SE && a.y8) {  // the next IR block's e4m3 expand operand
-        const float l[8] = {v[0], v[1], v[2], v[3], 0.f, 0.f, 0.f, 0.f};
-        *reinterpret_cast<uint32_t*>(a.y8 + (size_t)m * a.ld8 + n4) = e4m3x8(l).x;
-      }
+      const uint2 yb = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      if (SE || Y) *reinterpret_cast<uint2*>(Y + o) = yb;
+      // the next IR block's e4m3 expand operand: e4m3 of the STORED bf16 values (one rounding chain, the bytes
+      // launch_rows_e4m3 gives when no producer writes them; test_fp8_se_y8_e4m3_handoff_is_exact)
+      if (SE && a.y8) *reinterpret_cast<uint32_t*>(a.y8 + (size_t)m * a.ld8 + n4) = e4m3x4_bf16(yb);
       if (!SE && a.y8) {  // the next conv's operand: e4m3(lrelu(v))
         float l[8];
 #pragma unroll

@@ -87,6 +87,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_F8_ER")) f8_er_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER8_X8")) er8_x8_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_ER2")) f8_er2_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_SE_Y8")) se_y8_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_FUSED")) se_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER_FUSED")) er_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SE_SP")) se_sp_ = std::strcmp(e, "0") != 0;  // A/B only
@@ -833,7 +834,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         }
         // fp8: an e4m3 copy of the output for the next block's expand, into the buffer cur8 does not hold
         const int ld8 = want8 ? blocks_[k + 1].f8x_kp : 0;
-        if (f8 && want8) next8 = cur8 == X8[0] ? X8[1] : X8[0];
+        if (f8 && want8 && se_y8_) next8 = cur8 == X8[0] ? X8[1] : X8[0];
         if (f8 && se_ws_ && se_ws_f8_supported(nh * nw, cs, chan_stride(b.cout))) {
           const double rows = (double)nc * nh * nw;
           launch_se_ws_f8(M2, nc * nh * nw, nh * nw, cs, arena_.ptr(b.f8_w), b.f8_kp, b.f8_npad,

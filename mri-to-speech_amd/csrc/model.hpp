@@ -102,6 +102,8 @@ class Acoustic {
   bool ir_ws_ = true;     // split fp32: the persistent warp-specialised form of it (env M2S_IR_WS=0 disables)
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
   bool f8_er_ = true;            // fp8: EdgeResidual blocks.1.1/.2 on e4m3 (env M2S_F8_ER=0: bf16 er_fused)
+  bool se_y8_ = true;            // fp8: the SE GEMM also stores the next expand's e4m3 operand (env M2S_SE_Y8=0:
+                                 // launch_rows_e4m3 converts it; the same bytes, test_fp8_se_y8_e4m3_handoff_is_exact)
   bool f8_er2_ = true;           // fp8: EdgeResidual blocks.2.1/.2 on e4m3 (er8w_fused; env M2S_F8_ER2=0: bf16 er2_fused)
   bool er8_x8_ = true;           // ... their input as e4m3 bytes from the producer (env M2S_ER8_X8=0: converted
                                  // in er8_fused; the same bytes, test_fp8_er8_e4m3_handoff_is_exact)

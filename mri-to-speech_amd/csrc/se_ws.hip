@@ -377,12 +377,10 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
           float v[4] = {fmaf(acc[ni][mi][0], ws.x, bb.x) + r[0], fmaf(acc[ni][mi][1], ws.y, bb.y) + r[1],
                         fmaf(acc[ni][mi][2], ws.z, bb.z) + r[2], fmaf(acc[ni][mi][3], ws.w, bb.w) + r[3]};
           if (bad) v[0] = v[1] = v[2] = v[3] = __builtin_nanf("");
-          *reinterpret_cast<uint2*>(a.y + (size_t)m * a.cs_out + n4) =
-              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-          if (a.y8) {
-            const float l[8] = {v[0], v[1], v[2], v[3], 0.f, 0.f, 0.f, 0.f};
-            *reinterpret_cast<uint32_t*>(a.y8 + (size_t)m * a.ld8 + n4) = e4m3x8(l).x;
-          }
+          const uint2 yb = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+          *reinterpret_cast<uint2*>(a.y + (size_t)m * a.cs_out + n4) = yb;
+          // e4m3 of the stored bf16 values: the bytes launch_rows_e4m3 gives (test_fp8_se_y8_e4m3_handoff_is_exact)
+          if (a.y8) *reinterpret_cast<uint32_t*>(a.y8 + (size_t)m * a.ld8 + n4) = e4m3x4_bf16(yb);
         }
       }
       continue;

@@ -241,3 +241,18 @@ def test_fp8_er8_e4m3_handoff_is_exact(rt, monkeypatch):
     for i in (4, 5, 8):
         assert torch.equal(ex.probe(fr, i), ec.probe(fr, i)), i
     assert torch.equal(ex.effnet(fr), ec.effnet(fr))
+
+
+def test_fp8_se_y8_e4m3_handoff_is_exact(rt, monkeypatch):
+    """The SE GEMMs of the fp8 engine (se_ws / gemm128 KIND_F8_SE) store the next IR block's e4m3 expand operand
+    (y8) as the e4m3 bytes of the bf16 values they store, so the next block reads the same bytes as when
+    launch_rows_e4m3 converts its bf16 input (M2S_SE_Y8=0): the two paths agree bit for bit (one rounding chain)."""
+    st = synth.synth_acoustic_state(8)
+    fr = torch.from_numpy(synth.synth_frames(1, 37, seed=48)[0]).to(DEV)
+    monkeypatch.setenv("M2S_SE_Y8", "1")
+    ey = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    monkeypatch.setenv("M2S_SE_Y8", "0")
+    ec = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    for i in (10, 12, 14, 18, 20, 28):
+        assert torch.equal(ey.probe(fr, i), ec.probe(fr, i)), i
+    assert torch.equal(ey.effnet(fr), ec.effnet(fr))
