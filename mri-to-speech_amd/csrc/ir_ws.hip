@@ -40,11 +40,6 @@ namespace m2s {
 namespace {
 
 __device__ __attribute__((aligned(16))) uint4 g_ws_zero[4];  // DMA source of padding chunks
-#ifdef IRWS_TRACE
-// diagnostic ablations (M2S_IRWS_ABL bits): 1 = consumers skip their work, 2 = producers skip MFMA + epilogue,
-// 4 = no weight / tap DMA per slice (stale LDS weights); results are wrong by design
-__device__ int g_irws_abl;
-#endif
 
 constexpr int WS_SL = 32;  // expanded channels per slice
 constexpr int WS_BR = 8;   // output rows per band
@@ -68,7 +63,6 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
 }
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 struct WsLayout {
   int XR, TROWS, x_bytes, tile_bytes, w_bytes, total;
@@ -89,7 +83,7 @@ __host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mi
   L.tile_bytes = 2 * 8 * L.TROWS * 16;
   L.w_bytes = 2 * (cs_in / 32) * 4096;
   const int nb = (H + WS_BR - 1) / WS_BR;
-  L.total = L.x_bytes + L.tile_bytes + L.w_bytes + (2 * 320 + 2 * 32 + 2 * WS_NC * 32) * 4 + (nb > 1 ? cs_mid * 4 : 0) + 16;
+  L.total = L.x_bytes + L.tile_bytes + L.w_bytes + (2 * 320 + 2 * 32 + 2 * WS_NC * 32) * 4 + (nb > 1 ? cs_mid * 4 : 0) + 32;
   return L;
 }
 
@@ -116,11 +110,18 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   float* bpl = wdl + 2 * 320;                                 // [2][32] expand bias
   float* red = bpl + 2 * 32;                                  // [2][WS_NC][32]
   float* se_acc = red + 2 * WS_NC * 32;                       // [cs_mid] (NB > 1)
-  // producer waves that finished slice f's MFMAs (monotonic): W(f + 2) may then overwrite W(f)'s slot
-  unsigned* pdone = reinterpret_cast<unsigned*>(smem + Lg.total - 16);
-  // set by a producer whose pdone wait timed out (reported through `err`): the squeeze of every slice finalized
+  // Monotonic LDS counters, one add per wave and event (the hand-offs that replace the per-slice barrier):
+  unsigned* ctr = reinterpret_cast<unsigned*>(smem + Lg.total - 32);
+  unsigned* pdone = ctr + 0;   // producers done with slice f's MFMAs: W(f)'s slot and (band end) the x rows free
+  unsigned* wrdy = ctr + 1;    // producers whose pieces of W(f) (+ bias) landed
+  unsigned* xrdy = ctr + 2;    // producers whose pieces of a band's x rows landed
+  unsigned* tfull = ctr + 3;   // producers done writing tile f (and, waves NP-2 / NP-1, taps f landed)
+  unsigned* tfree = ctr + 4;   // consumers done reading tile f and taps f
+  unsigned* rdone = ctr + 5;   // consumers that wrote slice f's squeeze partials
+  unsigned* fdone = ctr + 6;   // consumers that finalized slice f (its partials' buffer free)
+  // set by a wave whose counter wait timed out (reported through `err`): the squeeze of every slice finalized
   // from then on stores NaN, so the images of this workgroup come out NaN instead of silently wrong
-  unsigned* poison = pdone + 1;
+  unsigned* poison = ctr + 7;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -154,15 +155,31 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     return d;
   };
 
-  if (tid == 0) {  // ordered before any use by the first barrier of the slice loop
-    *pdone = 0u;
-    *poison = 0u;
-  }
+  if (tid < 8) ctr[tid] = 0u;  // ordered before any use by the kernel's one barrier
   // the tiles' halo columns are zero for good (the producers write only interior columns)
   for (int i = tid; i < 2 * 8 * Lg.TROWS; i += 64 * (WS_NP + WS_NC)) {
     const int pl = i / Lg.TROWS, r = i - pl * Lg.TROWS, c = r % WT;
     if (c == 0 || c == WT - 1) *reinterpret_cast<float4*>(tiles + pl * PLT + r * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+
+  // counter wait: one lane polls (ds_read + lgkmcnt(0), which also retires this wave's own LDS ops), bounded by
+  // spin_max polls; a timeout is reported and poisons the workgroup's squeeze (a wrong hand-off, never a hang)
+  auto wait_ge = [&](const unsigned* c, unsigned target) {
+    const uint32_t a = (uint32_t)(uintptr_t)c;
+    for (unsigned n = 0; n < spin_max; ++n) {
+      unsigned v;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+      if (__builtin_amdgcn_readfirstlane(v) >= target) return;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    report_async(err, M2S_ASYNC_WS, lane);
+    if (lane == 0) asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)poison), "v"(1u) : "memory");
+  };
+  // count this wave in: its LDS writes retire first (lgkmcnt(0)); LDS-DMA data is covered by the caller's vmcnt
+  auto bump = [&](unsigned* c) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"((uint32_t)(uintptr_t)c), "v"(1u) : "memory");
+  };
 
   // ---- producer pieces -----------------------------------------------------------------------
   auto issue_w = [&](int f, Step d) {  // the slice's expand weights (4 * KS DMA pieces) + expand bias
@@ -211,24 +228,9 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   // of slice f + 1 they arrived one slice ahead only, and the wait for them was exposed: without the
   // per-slice weight DMA ir_ws ran 11-15 % faster, ablation M2S_IRWS_ABL=4, gpurun_out)
   auto after_mfma = [&](int f, bool more, Step d2) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"((uint32_t)(uintptr_t)pdone), "v"(1u) : "memory");
+    bump(pdone);
     if (!more) return;
-    const unsigned target = (unsigned)(WS_NP * (f + 1));
-    bool ok = false;
-    for (unsigned n = 0; n < spin_max; ++n) {
-      unsigned v;
-      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((uint32_t)(uintptr_t)pdone) : "memory");
-      if (__builtin_amdgcn_readfirstlane(v) >= target) {
-        ok = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (!ok) {  // W(f + 2) may now overwrite a slot another producer still reads: report it, poison the squeeze
-      report_async(err, M2S_ASYNC_WS, lane);
-      if (lane == 0) asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)poison), "v"(1u) : "memory");
-    }
+    wait_ge(pdone, (unsigned)(WS_NP * (f + 1)));
     issue_w(f + 2, d2);
   };
   auto produce = [&](int f, Step d, bool more, Step d2) {
@@ -284,6 +286,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       }
       TR(f, 6);
       after_mfma(f, more, d2);
+      if (f >= 2) wait_ge(tfree, (unsigned)(WS_NC * (f - 1)));  // the consumers are done with tile f - 2 (same buffer)
       // bias + SiLU -> tile[f % 2]; lane holds channels 4g..4g+3 (of 16-channel tile nt) of position r16
 #pragma unroll
       for (int k = 0; k < NU; ++k) {
@@ -299,7 +302,10 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     if (nu == 3) units(std::integral_constant<int, 3>());
     else if (nu == 2) units(std::integral_constant<int, 2>());
     else if (nu == 1) units(std::integral_constant<int, 1>());
-    else after_mfma(f, more, d2);
+    else {
+      after_mfma(f, more, d2);
+      if (f >= 2) wait_ge(tfree, (unsigned)(WS_NC * (f - 1)));
+    }
     // halo rows outside the image (above the first band, below the last) hold zeros
     if (tid < 8 * W) {
       const int pl = tid / W, c = tid - pl * W;
@@ -320,7 +326,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   auto consume = [&](int f, Step d) {
     const int c0 = d.sl * WS_SL, r0 = d.band * WS_BR, br = min(WS_BR, H - r0);
     float s[4] = {0.f, 0.f, 0.f, 0.f};
-    TR(f + 1, 4);
+    TR(f, 4);
     const uint32_t pbase = (uint32_t)(d.img * P + r0 * W);  // uniform
     const uint32_t yoff0 = __builtin_amdgcn_readfirstlane(4u * (uint32_t)c0) + 8u * (uint32_t)cg +
                            (pbase + (uint32_t)cpl) * (4u * (uint32_t)cs_mid);  // launch_ir_ws: < 2^32
@@ -368,7 +374,8 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       for (int k = 0; k < WS_PXL; ++k)
         if (cpl + 64 * k < br * W) pixel(k);
     }
-    TR(f + 1, 5);
+    TR(f, 5);
+    bump(tfree);  // every tile and tap read of slice f returned: the producers may refill both buffers
     // squeeze partials: the wave's 8 pixel lanes of each plane (lane bits 3..5): a DPP row rotation
     // inside each 16-lane row, then gfx950's row / half swaps (v_permlane16_swap, v_permlane32_swap: VALU,
     // no LDS round trip, where two ds_bpermute shuffles were); one row of 32 channels per wave
@@ -380,9 +387,11 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(s[j]), __float_as_uint(s[j]), false, false);
       s[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
     }
+    if (f >= 2) wait_ge(fdone, (unsigned)(WS_NC * (f - 1)));  // red[f % 2] held slice f - 2: finalized everywhere
     if (lane < 8)
 #pragma unroll
       for (int j = 0; j < 4; ++j) red[((f & 1) * WS_NC + cw) * 32 + lane * 4 + j] = s[j];
+    bump(rdone);
   };
   auto finalize = [&](int f, Step d) {  // slice f's channel sums -> bands -> SE mean (4 channels a wave)
     if (lane >= 4) return;
@@ -399,59 +408,75 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       act_st<sp_t>(reinterpret_cast<sp_t*>(se_mean), d.img, cs_mid, c, *poison ? __builtin_nanf("") : t / (float)P);
   };
 
-  // ---- the slice pipeline: producers on f = i, consumers on f = i - 1 (and the squeeze of i - 2) --
-  Step cur{(int)blockIdx.x, 0, 0}, prev{}, prev2{};  // steps i, i - 1, i - 2
-  // DMA pieces a producer wave issues per slice (W pieces j = wave + 8 k of 4 KS, + the bias on wave 0)
-  const int npw = (wave < 4 * KS ? (4 * KS - 1 - wave) / WS_NP + 1 : 0) + (wave == 0 ? 1 : 0);
-  Step nxt = next_step(cur);
-  if (prod && T > 0) issue_w(0, cur);
-  if (prod && T > 1) issue_w(1, nxt);
-  for (int i = 0; i <= T + 1; ++i) {
-    nxt = next_step(cur);
-    const Step nxt2 = next_step(nxt);
-    TR(i, 0);
-    if (prod) {  // this wave's pieces of W(i) (and taps of i - 1) landed; W(i + 1) may stay in flight
-      const int young = i + 1 < T ? npw : 0;
-      static_assert(4 * KS <= 4 * WS_NP, "pieces per wave");
-      if (young == 0) wait_vm0();
-      else if (young == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else if (young == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else if (young == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else if (young == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      else wait_vm0();
-    }
-    TR(i, 1);
-    lds_fence();
-    __builtin_amdgcn_s_barrier();  // W(i) everywhere; tile[i % 2], W[(i + 1) % 2], taps[i % 2] free
-    TR(i, 2);
-    if (i < T && cur.sl == 0) {  // a new band: its input rows (the producers finished the last band's MFMAs)
-      if (prod) {
+  // ---- the slice pipeline.  No workgroup barrier per slice: each role runs its own loop and the hand-offs are
+  // the LDS counters above.  Producers may run up to two slices ahead of the consumers (two tile / tap buffers);
+  // W(f + 2) is DMA'd into W(f)'s slot once every producer finished slice f's MFMAs, x rows of a band once every
+  // producer finished the last band's.  Consumers finalize slice f's squeeze one slice later.
+  __syncthreads();  // the counters and the tiles' zero halo columns
+  if (prod) {
+    // DMA pieces a producer wave issues per slice (W pieces j = wave + 8 k of 4 KS, + the bias on wave 0)
+    const int npw = (wave < 4 * KS ? (4 * KS - 1 - wave) / WS_NP + 1 : 0) + (wave == 0 ? 1 : 0);
+    const bool tap_wave = wave >= WS_NP - 2;  // issue_wd's two waves
+    Step cur{(int)blockIdx.x, 0, 0};
+    if (T > 0) issue_w(0, cur);
+    if (T > 1) issue_w(1, next_step(cur));
+    int bands = 0;
+    for (int i = 0; i < T; ++i) {
+      const Step nxt = next_step(cur), nxt2 = next_step(nxt);
+      TR(i, 0);
+      if (cur.sl == 0) {  // a new band: its input rows, once every producer is done with the last band's
+        if (i > 0) wait_ge(pdone, (unsigned)(WS_NP * i));
         issue_x(cur.img, cur.band);
         wait_vm0();
+        bump(xrdy);
+        wait_ge(xrdy, (unsigned)(WS_NP * ++bands));
       }
-      __builtin_amdgcn_s_barrier();
-    }
-#ifdef IRWS_TRACE
-    const int abl = g_irws_abl;
-#else
-    constexpr int abl = 0;
-#endif
-    if (prod) {
-      TR(i, 4);
-      if (i < T) {
-        if (!(abl & 4)) issue_wd(i, cur);  // read by the consumers next iteration
-        TR(i, 5);
-        if (!(abl & 2)) produce(i, cur, i + 2 < T && !(abl & 4), nxt2);
-        else after_mfma(i, i + 2 < T && !(abl & 4), nxt2);
+      {  // this wave's pieces of W(i) landed (W(i + 1)'s may stay in flight), then every producer's
+        const int young = i + 1 < T ? npw : 0;
+        static_assert(4 * KS <= 4 * WS_NP, "pieces per wave");
+        if (young == 0) wait_vm0();
+        else if (young == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else if (young == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else if (young == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (young == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else wait_vm0();
+        bump(wrdy);
+        wait_ge(wrdy, (unsigned)(WS_NP * (i + 1)));
       }
-    } else if (!(abl & 1)) {  // no global loads here: the consumers' VM counter holds only their stores
-      if (i >= 2) finalize(i - 2, prev2);
-      if (i >= 1 && i <= T) consume(i - 1, prev);
+      TR(i, 1);
+      if (tap_wave) {  // slice i's taps into taps[i % 2], once the consumers are done with slice i - 2's
+        if (i >= 2) wait_ge(tfree, (unsigned)(WS_NC * (i - 1)));
+        issue_wd(i, cur);
+      }
+      TR(i, 2);
+      produce(i, cur, i + 2 < T, nxt2);
+      if (tap_wave) {  // the taps landed: only W(i + 2)'s pieces were issued after them
+        if (i + 2 < T && npw == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else if (i + 2 < T && npw == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else wait_vm0();
+      }
+      bump(tfull);
+      TR(i, 3);
+      cur = nxt;
     }
-    TR(i, 3);
-    prev2 = prev;
-    prev = cur;
-    cur = nxt;
+  } else {
+    Step cur{(int)blockIdx.x, 0, 0}, prev{};
+    for (int i = 0; i < T; ++i) {
+      wait_ge(tfull, (unsigned)(WS_NP * (i + 1)));  // tile i and taps i
+      consume(i, cur);
+      if (i >= 1) {  // slice i - 1's partials from every consumer -> its SE mean
+        wait_ge(rdone, (unsigned)(WS_NC * i));
+        finalize(i - 1, prev);
+        bump(fdone);
+      }
+      TR(i, 7);
+      prev = cur;
+      cur = next_step(cur);
+    }
+    if (T > 0) {
+      wait_ge(rdone, (unsigned)(WS_NC * T));
+      finalize(T - 1, prev);
+    }
   }
 }
 
@@ -467,9 +492,10 @@ static void dump_trace(unsigned long long* tr, hipStream_t s, const char* tag) {
   auto at = [&](int i, int c, int k) { return (long long)h[((i * 2 + c) * 8 + k) * 64]; };
   fprintf(stderr, "TRACE %s:", tag);
   for (int i = 2; i < 12; ++i)
-    fprintf(stderr, " [P wait %lld bar %lld dmaw %lld dmawd %lld mfma %lld epi %lld | C bar %lld pre %lld px %lld red %lld]", at(i, 0, 1) - at(i, 0, 0),
-            at(i, 0, 2) - at(i, 0, 1), at(i, 0, 4) - at(i, 0, 2), at(i, 0, 5) - at(i, 0, 4), at(i, 0, 6) - at(i, 0, 5), at(i, 0, 3) - at(i, 0, 6),
-            at(i, 1, 2) - at(i, 1, 0), at(i, 1, 4) - at(i, 1, 2), at(i, 1, 5) - at(i, 1, 4), at(i, 1, 3) - at(i, 1, 5));
+    // producer: W ready, taps issued, MFMAs, epilogue + hand-off; consumer: tile wait, pixels, squeeze + finalize
+    fprintf(stderr, " [P w %lld tap %lld mfma %lld epi %lld | C wait %lld px %lld red+fin %lld]", at(i, 0, 1) - at(i, 0, 0),
+            at(i, 0, 2) - at(i, 0, 1), at(i, 0, 6) - at(i, 0, 2), at(i, 0, 3) - at(i, 0, 6), at(i, 1, 4) - at(i - 1, 1, 7),
+            at(i, 1, 5) - at(i, 1, 4), at(i, 1, 7) - at(i, 1, 5));
   fprintf(stderr, "\n");
   M2S_HIP(hipMemset(tr, 0, h.size() * 8));
 }
@@ -500,13 +526,6 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
     if (getenv("M2S_IR_WS_TRACE")) M2S_HIP(hipMalloc(&p, 64 * 2 * 8 * 64 * 8));
     return p;
   }();
-  static const int abl_set = [] {
-    const char* e = getenv("M2S_IRWS_ABL");
-    const int v = e ? atoi(e) : 0;
-    M2S_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_irws_abl), &v, sizeof(int)));
-    return v;
-  }();
-  (void)abl_set;
 #define M2S_IRWS_DUMP(tag) \
   if (tr) dump_trace(tr, s, tag);
 #else
