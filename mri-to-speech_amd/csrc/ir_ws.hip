@@ -83,7 +83,7 @@ __host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mi
   L.tile_bytes = 2 * 8 * L.TROWS * 16;
   L.w_bytes = 2 * (cs_in / 32) * 4096;
   const int nb = (H + WS_BR - 1) / WS_BR;
-  L.total = L.x_bytes + L.tile_bytes + L.w_bytes + (2 * 320 + 2 * 32 + 2 * WS_NC * 32) * 4 + (nb > 1 ? cs_mid * 4 : 0) + 32;
+  L.total = L.x_bytes + L.tile_bytes + L.w_bytes + (2 * 320 + 2 * 32 + 2 * WS_NC * 32) * 4 + (nb > 1 ? cs_mid * 4 : 0) + 128;
   return L;
 }
 
@@ -110,18 +110,22 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   float* bpl = wdl + 2 * 320;                                 // [2][32] expand bias
   float* red = bpl + 2 * 32;                                  // [2][WS_NC][32]
   float* se_acc = red + 2 * WS_NC * 32;                       // [cs_mid] (NB > 1)
-  // Monotonic LDS counters, one add per wave and event (the hand-offs that replace the per-slice barrier):
-  unsigned* ctr = reinterpret_cast<unsigned*>(smem + Lg.total - 32);
+  // The hand-offs that replace the per-slice barrier, in LDS.  Producer events are shared monotonic counters
+  // (one add per producer wave and event): a producer adds slice f + 1's count only after a wait that needed
+  // every producer's slice-f add, so "counter >= NP x k" cannot be met by one wave running ahead.  Consumers are
+  // not in lockstep with each other (one may consume slice f + 1 while another is still on f), so a shared count
+  // could be met that way: their events are one word per consumer wave, and a wait needs every word >= k.
+  unsigned* ctr = reinterpret_cast<unsigned*>(smem + Lg.total - 128);
   unsigned* pdone = ctr + 0;   // producers done with slice f's MFMAs: W(f)'s slot and (band end) the x rows free
   unsigned* wrdy = ctr + 1;    // producers whose pieces of W(f) (+ bias) landed
   unsigned* xrdy = ctr + 2;    // producers whose pieces of a band's x rows landed
   unsigned* tfull = ctr + 3;   // producers done writing tile f (and, waves NP-2 / NP-1, taps f landed)
-  unsigned* tfree = ctr + 4;   // consumers done reading tile f and taps f
-  unsigned* rdone = ctr + 5;   // consumers that wrote slice f's squeeze partials
-  unsigned* fdone = ctr + 6;   // consumers that finalized slice f (its partials' buffer free)
-  // set by a wave whose counter wait timed out (reported through `err`): the squeeze of every slice finalized
-  // from then on stores NaN, so the images of this workgroup come out NaN instead of silently wrong
-  unsigned* poison = ctr + 7;
+  // set by a wave whose wait timed out (reported through `err`): the squeeze of every slice finalized from then
+  // on stores NaN, so the images of this workgroup come out NaN instead of silently wrong
+  unsigned* poison = ctr + 4;
+  unsigned* tfree = ctr + 8;   // [WS_NC] slices whose tile and taps consumer wave c is done reading
+  unsigned* rdone = ctr + 16;  // [WS_NC] slices whose squeeze partials consumer wave c wrote
+  unsigned* fdone = ctr + 24;  // [WS_NC] slices consumer wave c finalized (their partials' buffer free)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -155,7 +159,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     return d;
   };
 
-  if (tid < 8) ctr[tid] = 0u;  // ordered before any use by the kernel's one barrier
+  if (tid < 32) ctr[tid] = 0u;  // ordered before any use by the kernel's one barrier
   // the tiles' halo columns are zero for good (the producers write only interior columns)
   for (int i = tid; i < 2 * 8 * Lg.TROWS; i += 64 * (WS_NP + WS_NC)) {
     const int pl = i / Lg.TROWS, r = i - pl * Lg.TROWS, c = r % WT;
@@ -170,6 +174,18 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       unsigned v;
       asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
       if (__builtin_amdgcn_readfirstlane(v) >= target) return;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    report_async(err, M2S_ASYNC_WS, lane);
+    if (lane == 0) asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)poison), "v"(1u) : "memory");
+  };
+  // per-consumer words: lanes 0..WS_NC-1 read one word each; done when every word >= target
+  auto wait_all = [&](const unsigned* words, unsigned target) {
+    const uint32_t a = (uint32_t)(uintptr_t)(words + (lane < WS_NC ? lane : 0));
+    for (unsigned n = 0; n < spin_max; ++n) {
+      unsigned v;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+      if (__builtin_amdgcn_ballot_w64(lane < WS_NC && v < target) == 0) return;
       __builtin_amdgcn_s_sleep(1);
     }
     report_async(err, M2S_ASYNC_WS, lane);
@@ -286,7 +302,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       }
       TR(f, 6);
       after_mfma(f, more, d2);
-      if (f >= 2) wait_ge(tfree, (unsigned)(WS_NC * (f - 1)));  // the consumers are done with tile f - 2 (same buffer)
+      if (f >= 2) wait_all(tfree, (unsigned)(f - 1));  // every consumer is done with tile f - 2 (same buffer)
       // bias + SiLU -> tile[f % 2]; lane holds channels 4g..4g+3 (of 16-channel tile nt) of position r16
 #pragma unroll
       for (int k = 0; k < NU; ++k) {
@@ -304,7 +320,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     else if (nu == 1) units(std::integral_constant<int, 1>());
     else {
       after_mfma(f, more, d2);
-      if (f >= 2) wait_ge(tfree, (unsigned)(WS_NC * (f - 1)));
+      if (f >= 2) wait_all(tfree, (unsigned)(f - 1));
     }
     // halo rows outside the image (above the first band, below the last) hold zeros
     if (tid < 8 * W) {
@@ -375,7 +391,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
         if (cpl + 64 * k < br * W) pixel(k);
     }
     TR(f, 5);
-    bump(tfree);  // every tile and tap read of slice f returned: the producers may refill both buffers
+    bump(tfree + cw);  // every tile and tap read of slice f returned: the producers may refill both buffers
     // squeeze partials: the wave's 8 pixel lanes of each plane (lane bits 3..5): a DPP row rotation
     // inside each 16-lane row, then gfx950's row / half swaps (v_permlane16_swap, v_permlane32_swap: VALU,
     // no LDS round trip, where two ds_bpermute shuffles were); one row of 32 channels per wave
@@ -387,11 +403,11 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(s[j]), __float_as_uint(s[j]), false, false);
       s[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
     }
-    if (f >= 2) wait_ge(fdone, (unsigned)(WS_NC * (f - 1)));  // red[f % 2] held slice f - 2: finalized everywhere
+    if (f >= 2) wait_all(fdone, (unsigned)(f - 1));  // red[f % 2] held slice f - 2: finalized by every consumer
     if (lane < 8)
 #pragma unroll
       for (int j = 0; j < 4; ++j) red[((f & 1) * WS_NC + cw) * 32 + lane * 4 + j] = s[j];
-    bump(rdone);
+    bump(rdone + cw);
   };
   auto finalize = [&](int f, Step d) {  // slice f's channel sums -> bands -> SE mean (4 channels a wave)
     if (lane >= 4) return;
@@ -445,7 +461,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       }
       TR(i, 1);
       if (tap_wave) {  // slice i's taps into taps[i % 2], once the consumers are done with slice i - 2's
-        if (i >= 2) wait_ge(tfree, (unsigned)(WS_NC * (i - 1)));
+        if (i >= 2) wait_all(tfree, (unsigned)(i - 1));
         issue_wd(i, cur);
       }
       TR(i, 2);
@@ -465,16 +481,16 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       wait_ge(tfull, (unsigned)(WS_NP * (i + 1)));  // tile i and taps i
       consume(i, cur);
       if (i >= 1) {  // slice i - 1's partials from every consumer -> its SE mean
-        wait_ge(rdone, (unsigned)(WS_NC * i));
+        wait_all(rdone, (unsigned)i);
         finalize(i - 1, prev);
-        bump(fdone);
+        bump(fdone + cw);
       }
       TR(i, 7);
       prev = cur;
       cur = next_step(cur);
     }
     if (T > 0) {
-      wait_ge(rdone, (unsigned)(WS_NC * T));
+      wait_all(rdone, (unsigned)T);
       finalize(T - 1, prev);
     }
   }
