@@ -25,7 +25,13 @@ namespace {
 constexpr int SB_SL = 32;                // expanded channels per slice
 constexpr int SB_BO = 4;                 // output rows per band
 constexpr int SB_ROWS = 2 * SB_BO + 1;   // input rows per band
-constexpr int SB_MROW = SB_SL + 4;       // fp32 tile row stride (floats): 144 B
+constexpr int SB_MROW = SB_SL + 8;       // fp32 tile row stride (floats): 160 B = 10 16-byte units
+// 16-byte unit u (4 channels) of tile position q is stored at unit u ^ sb_swz(q): with the 10-unit stride, the
+// depthwise's ds_read_b128 lane groups (4 channel groups x 4 pixels two positions apart) hit 16 distinct bank
+// quads and the expand epilogue's ds_write_b128 groups (8 consecutive positions) 8 distinct ones, at every
+// offset (exhaustive search, tools/swizzle_search.py); the plain 9-unit stride had 3-way read conflicts
+// (SQ_LDS_BANK_CONFLICT 1.7 per LDS instruction, profiles/r04fin9_sq_mfma.txt)
+__device__ __forceinline__ int sb_swz(int q) { return ((q >> 1) ^ ((q >> 2) * 6)) & 7; }
 constexpr int SB_IWMAX = 32;             // input width bound (tile 9 x 34 rows: 44 KB)
 constexpr int SB_MT = 5;                 // 16-position tiles per wave at most: ceil(9 x 32 / 16 / 4)
 
@@ -108,11 +114,12 @@ __global__ void __launch_bounds__(256, 3)
         }
         acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[nt][ks], bh[i][ks], acc[nt], 0, 0, 0);
       }
-    if (m < MP) {  // lane = channels 4 g .. 4 g + 3 of n-tile nt at position m
-      float* tp = tile + ((size_t)r * TW + ix + 1) * SB_MROW + 4 * g;
+    if (m < MP) {  // lane = channels 4 g .. 4 g + 3 of n-tile nt at position m (unit g + 4 nt, swizzled)
+      const int q = r * TW + ix + 1, sq = sb_swz(q);
+      float* tp = tile + (size_t)q * SB_MROW;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
-        *reinterpret_cast<float4*>(tp + nt * 16) =
+        *reinterpret_cast<float4*>(tp + ((g + 4 * nt) ^ sq) * 4) =
             inside ? make_float4(silu(acc[nt][0] + bb[nt].x), silu(acc[nt][1] + bb[nt].y), silu(acc[nt][2] + bb[nt].z),
                                  silu(acc[nt][3] + bb[nt].w))
                    : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -141,9 +148,10 @@ __global__ void __launch_bounds__(256, 3)
       for (int j = 0; j < 8; ++j) a[j] = b[j];
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const float* tp = tile + ((size_t)(2 * oyl + t / 3) * TW + 2 * ox - pad_l + t % 3 + 1) * SB_MROW + cg * 8;
-        const float4 u0 = *reinterpret_cast<const float4*>(tp);
-        const float4 u1 = *reinterpret_cast<const float4*>(tp + 4);
+        const int q = (2 * oyl + t / 3) * TW + 2 * ox - pad_l + t % 3 + 1, sq = sb_swz(q);
+        const float* tp = tile + (size_t)q * SB_MROW;
+        const float4 u0 = *reinterpret_cast<const float4*>(tp + ((2 * cg) ^ sq) * 4);
+        const float4 u1 = *reinterpret_cast<const float4*>(tp + ((2 * cg + 1) ^ sq) * 4);
         a[0] += w[t][0] * u0.x; a[1] += w[t][1] * u0.y; a[2] += w[t][2] * u0.z; a[3] += w[t][3] * u0.w;
         a[4] += w[t][4] * u1.x; a[5] += w[t][5] * u1.y; a[6] += w[t][6] * u1.z; a[7] += w[t][7] * u1.w;
       }
