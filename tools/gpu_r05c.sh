@@ -7,7 +7,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_bf16x3.py tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread \
-  -k "ir_ws or every_block or timeout or config" > "$OUT/pytest.log" 2>&1
+  -k "ir_ws or every_block or timeout or config or s2band" > "$OUT/pytest.log" 2>&1
 rc=$?
 tail -3 "$OUT/pytest.log"
 [ $rc = 0 ] || exit $rc
