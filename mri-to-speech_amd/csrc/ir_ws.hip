@@ -82,8 +82,8 @@ __host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mi
   L.x_bytes = L.XR * W * xp;
   L.tile_bytes = 2 * 8 * L.TROWS * 16;
   L.w_bytes = 2 * (cs_in / 32) * 4096;
-  const int nb = (H + WS_BR - 1) / WS_BR;
-  L.total = L.x_bytes + L.tile_bytes + L.w_bytes + (2 * 320 + 2 * 32 + 2 * WS_NC * 32) * 4 + (nb > 1 ? cs_mid * 4 : 0) + 128;
+  // taps + biases, the squeeze's fixed-point channel sums [cs_mid] (u64) and arrival counts [cs_mid / 32], counters
+  L.total = L.x_bytes + L.tile_bytes + L.w_bytes + (2 * 320 + 2 * 32) * 4 + cs_mid * 8 + (cs_mid / WS_SL) * 4 + 128;
   return L;
 }
 
@@ -108,8 +108,11 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   char* wbuf = tiles + Lg.tile_bytes;
   float* wdl = reinterpret_cast<float*>(wbuf + Lg.w_bytes);  // [2][9 x 32 taps | 32 depthwise bias]
   float* bpl = wdl + 2 * 320;                                 // [2][32] expand bias
-  float* red = bpl + 2 * 32;                                  // [2][WS_NC][32]
-  float* se_acc = red + 2 * WS_NC * 32;                       // [cs_mid] (NB > 1)
+  // the squeeze: per channel the sum of the image's SiLU outputs as 32.32 fixed point, added by every consumer
+  // wave of every band with an integer LDS atomic (the same bits in any arrival order); per slice index the
+  // number of (band, wave) arrivals, whose last one turns the sums into the slice's SE means
+  unsigned long long* sq = reinterpret_cast<unsigned long long*>(bpl + 2 * 32);  // [cs_mid]
+  unsigned* sq_n = reinterpret_cast<unsigned*>(sq + cs_mid);                      // [NS]
   // The hand-offs that replace the per-slice barrier, in LDS.  Producer events are shared monotonic counters
   // (one add per producer wave and event): a producer adds slice f + 1's count only after a wait that needed
   // every producer's slice-f add, so "counter >= NP x k" cannot be met by one wave running ahead.  Consumers are
@@ -124,8 +127,6 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   // on stores NaN, so the images of this workgroup come out NaN instead of silently wrong
   unsigned* poison = ctr + 4;
   unsigned* tfree = ctr + 8;   // [WS_NC] slices whose tile and taps consumer wave c is done reading
-  unsigned* rdone = ctr + 16;  // [WS_NC] slices whose squeeze partials consumer wave c wrote
-  unsigned* fdone = ctr + 24;  // [WS_NC] slices consumer wave c finalized (their partials' buffer free)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -160,6 +161,8 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   };
 
   if (tid < 32) ctr[tid] = 0u;  // ordered before any use by the kernel's one barrier
+  for (int i = tid; i < cs_mid; i += 64 * (WS_NP + WS_NC)) sq[i] = 0ull;
+  for (int i = tid; i < NS; i += 64 * (WS_NP + WS_NC)) sq_n[i] = 0u;
   // the tiles' halo columns are zero for good (the producers write only interior columns)
   for (int i = tid; i < 2 * 8 * Lg.TROWS; i += 64 * (WS_NP + WS_NC)) {
     const int pl = i / Lg.TROWS, r = i - pl * Lg.TROWS, c = r % WT;
@@ -240,14 +243,18 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     }
   };
   // after its MFMAs of slice f a producer wave counts itself done with W(f)'s slot; once all WS_NP are,
-  // it DMAs its pieces of W(f + 2) there, ~1.5 slices before they are needed (issued after the barrier
-  // of slice f + 1 they arrived one slice ahead only, and the wait for them was exposed: without the
-  // per-slice weight DMA ir_ws ran 11-15 % faster, ablation M2S_IRWS_ABL=4, gpurun_out)
+  // it DMAs its pieces of W(f + 2) there, ~1.5 slices before they are needed (issued one slice ahead
+  // only, the wait for them was exposed: without the per-slice weight DMA ir_ws ran 11-15 % faster).
+  // W(f + 1)'s pieces of this wave landed before it counts itself done with slice f (only slice f's taps, on the two
+  // tap waves, were issued after them): so once every producer is done with slice f, W(f + 1) is complete too, and
+  // W(f + 2) may go into W(f)'s slot
+  const bool tap_wave = wave >= WS_NP - 2;  // issue_wd's two waves
   auto after_mfma = [&](int f, bool more, Step d2) {
+    if (tap_wave) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else wait_vm0();
     bump(pdone);
-    if (!more) return;
-    wait_ge(pdone, (unsigned)(WS_NP * (f + 1)));
-    issue_w(f + 2, d2);
+    if (f + 1 < T) wait_ge(pdone, (unsigned)(WS_NP * (f + 1)));
+    if (more) issue_w(f + 2, d2);
   };
   auto produce = [&](int f, Step d, bool more, Step d2) {
     const int r0 = d.band * WS_BR, br = min(WS_BR, H - r0), xr0 = max(r0 - 1, 0), xr1 = min(r0 + WS_BR + 1, H);
@@ -403,62 +410,56 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(s[j]), __float_as_uint(s[j]), false, false);
       s[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
     }
-    if (f >= 2) wait_all(fdone, (unsigned)(f - 1));  // red[f % 2] held slice f - 2: finalized by every consumer
+    // lane L < 8 holds the wave's partial sums of plane L (channels c0 + 4 L ..): add them to the image's fixed-point
+    // sums, then count this (band, wave) in; the last of the NB x WS_NC arrivals writes the slice's SE means and
+    // clears the sums and the count for the next image (no wait on the other consumers: the atomics are the sync)
     if (lane < 8)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) red[((f & 1) * WS_NC + cw) * 32 + lane * 4 + j] = s[j];
-    bump(rdone + cw);
-  };
-  auto finalize = [&](int f, Step d) {  // slice f's channel sums -> bands -> SE mean (4 channels a wave)
-    if (lane >= 4) return;
-    const int cl = 4 * cw + lane, c = d.sl * WS_SL + cl;
-    const float* rf = red + (f & 1) * WS_NC * 32 + cl;
-    float t = 0.f;
-#pragma unroll
-    for (int w = 0; w < WS_NC; ++w) t += rf[32 * w];
-    if (NB > 1) {
-      if (d.band > 0) t += se_acc[c];
-      se_acc[c] = t;
+      for (int j = 0; j < 4; ++j)
+        __hip_atomic_fetch_add(sq + c0 + 4 * lane + j, (unsigned long long)(long long)(s[j] * 4294967296.0f), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    unsigned arrived = 0;
+    if (lane == 0) arrived = __hip_atomic_fetch_add(sq_n + d.sl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (__builtin_amdgcn_readfirstlane(arrived) == (unsigned)(NB * WS_NC - 1) && lane < WS_SL) {
+      const int c = c0 + lane;
+      const long long t = (long long)__hip_atomic_exchange(sq + c, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const float m = (float)((double)t * (1.0 / 4294967296.0) / (double)P);
+      act_st<sp_t>(reinterpret_cast<sp_t*>(se_mean), d.img, cs_mid, c, *poison ? __builtin_nanf("") : m);
+      if (lane == 0) sq_n[d.sl] = 0u;
     }
-    if (d.band == NB - 1)
-      act_st<sp_t>(reinterpret_cast<sp_t*>(se_mean), d.img, cs_mid, c, *poison ? __builtin_nanf("") : t / (float)P);
   };
 
   // ---- the slice pipeline.  No workgroup barrier per slice: each role runs its own loop and the hand-offs are
   // the LDS counters above.  Producers may run up to two slices ahead of the consumers (two tile / tap buffers);
   // W(f + 2) is DMA'd into W(f)'s slot once every producer finished slice f's MFMAs, x rows of a band once every
-  // producer finished the last band's.  Consumers finalize slice f's squeeze one slice later.
+  // producer finished the last band's.  Consumers wait only for their tiles (the squeeze is atomic).
   __syncthreads();  // the counters and the tiles' zero halo columns
   if (prod) {
     // DMA pieces a producer wave issues per slice (W pieces j = wave + 8 k of 4 KS, + the bias on wave 0)
     const int npw = (wave < 4 * KS ? (4 * KS - 1 - wave) / WS_NP + 1 : 0) + (wave == 0 ? 1 : 0);
-    const bool tap_wave = wave >= WS_NP - 2;  // issue_wd's two waves
     Step cur{(int)blockIdx.x, 0, 0};
     if (T > 0) issue_w(0, cur);
     if (T > 1) issue_w(1, next_step(cur));
+    if (T > 0) {  // W(0) landed everywhere (W(1) may stay in flight); later slices' W: after_mfma
+      if (T > 1 && npw == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if (T > 1 && npw == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else if (T > 1 && npw == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (T > 1 && npw == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else wait_vm0();
+      bump(wrdy);
+      wait_ge(wrdy, (unsigned)WS_NP);
+    }
     int bands = 0;
     for (int i = 0; i < T; ++i) {
       const Step nxt = next_step(cur), nxt2 = next_step(nxt);
       TR(i, 0);
-      if (cur.sl == 0) {  // a new band: its input rows, once every producer is done with the last band's
-        if (i > 0) wait_ge(pdone, (unsigned)(WS_NP * i));
+      if (cur.sl == 0) {  // a new band: its input rows (every producer is done with the last band's: after_mfma)
         issue_x(cur.img, cur.band);
         wait_vm0();
         bump(xrdy);
         wait_ge(xrdy, (unsigned)(WS_NP * ++bands));
       }
-      {  // this wave's pieces of W(i) landed (W(i + 1)'s may stay in flight), then every producer's
-        const int young = i + 1 < T ? npw : 0;
-        static_assert(4 * KS <= 4 * WS_NP, "pieces per wave");
-        if (young == 0) wait_vm0();
-        else if (young == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else if (young == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else if (young == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else if (young == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-        else wait_vm0();
-        bump(wrdy);
-        wait_ge(wrdy, (unsigned)(WS_NP * (i + 1)));
-      }
+      static_assert(4 * KS <= 4 * WS_NP, "pieces per wave");
       TR(i, 1);
       if (tap_wave) {  // slice i's taps into taps[i % 2], once the consumers are done with slice i - 2's
         if (i >= 2) wait_all(tfree, (unsigned)(i - 1));
@@ -476,22 +477,12 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       cur = nxt;
     }
   } else {
-    Step cur{(int)blockIdx.x, 0, 0}, prev{};
+    Step cur{(int)blockIdx.x, 0, 0};
     for (int i = 0; i < T; ++i) {
       wait_ge(tfull, (unsigned)(WS_NP * (i + 1)));  // tile i and taps i
       consume(i, cur);
-      if (i >= 1) {  // slice i - 1's partials from every consumer -> its SE mean
-        wait_all(rdone, (unsigned)i);
-        finalize(i - 1, prev);
-        bump(fdone + cw);
-      }
       TR(i, 7);
-      prev = cur;
       cur = next_step(cur);
-    }
-    if (T > 0) {
-      wait_all(rdone, (unsigned)T);
-      finalize(T - 1, prev);
     }
   }
 }
@@ -508,8 +499,8 @@ static void dump_trace(unsigned long long* tr, hipStream_t s, const char* tag) {
   auto at = [&](int i, int c, int k) { return (long long)h[((i * 2 + c) * 8 + k) * 64]; };
   fprintf(stderr, "TRACE %s:", tag);
   for (int i = 2; i < 12; ++i)
-    // producer: W ready, taps issued, MFMAs, epilogue + hand-off; consumer: tile wait, pixels, squeeze + finalize
-    fprintf(stderr, " [P w %lld tap %lld mfma %lld epi %lld | C wait %lld px %lld red+fin %lld]", at(i, 0, 1) - at(i, 0, 0),
+    // producer: band x, taps issued, MFMAs (+ W hand-off), epilogue; consumer: tile wait, pixels, squeeze
+    fprintf(stderr, " [P w %lld tap %lld mfma %lld epi %lld | C wait %lld px %lld sq %lld]", at(i, 0, 1) - at(i, 0, 0),
             at(i, 0, 2) - at(i, 0, 1), at(i, 0, 6) - at(i, 0, 2), at(i, 0, 3) - at(i, 0, 6), at(i, 1, 4) - at(i - 1, 1, 7),
             at(i, 1, 5) - at(i, 1, 4), at(i, 1, 7) - at(i, 1, 5));
   fprintf(stderr, "\n");
