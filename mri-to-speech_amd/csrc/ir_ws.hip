@@ -63,6 +63,16 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)p);
 }
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// vmcnt(n) for a wave-uniform n the immediate cannot take: the nearest count <= n (waiting for more is safe)
+__device__ __forceinline__ void wait_vm_le(int n) {
+  if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if (n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 struct WsLayout {
   int XR, TROWS, x_bytes, tile_bytes, w_bytes, total;
@@ -83,16 +93,32 @@ __host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mi
   L.tile_bytes = 2 * 8 * L.TROWS * 16;
   L.w_bytes = 2 * (cs_in / 32) * 4096;
   // taps + biases, the squeeze's fixed-point channel sums [cs_mid] (u64) and arrival counts [cs_mid / 32], counters
-  L.total = L.x_bytes + L.tile_bytes + L.w_bytes + (2 * 320 + 2 * 32) * 4 + cs_mid * 8 + (cs_mid / WS_SL) * 4 + 128;
+  L.total = L.x_bytes + L.tile_bytes + L.w_bytes + (3 * 320 + 2 * 32) * 4 + cs_mid * 8 + (cs_mid / WS_SL) * 4 + 128;
   return L;
 }
 
+// Scheduling switches (same results; diagnostic builds set them, tools/build_irws_variants.sh + ab_kern.py):
+// HAND_END = the W ring hand-off at the end of a slice, else right after the MFMAs (2: by shape); TAPS_AHEAD =
+// slice f + 1's depthwise taps issued at the end of slice f, else at the start of slice f + 1 behind a wait for
+// the consumers; PF_DEEP = 2-4 k-steps of MFMA operand reads in flight by unit count, else 2.  Same-box A/B
+// (gpurun_out/r05m, us per launch): 16x16 HAND_END 0 682-688 / 1 699-705; 8x8 0 540-553 / 1 531-533; TAPS_AHEAD
+// and PF_DEEP within 1-2 %
+#ifndef IRWS_HAND_END
+#define IRWS_HAND_END 2
+#endif
+#ifndef IRWS_PF_DEEP
+#define IRWS_PF_DEEP 1
+#endif
+#ifndef IRWS_TAPS_AHEAD
+#define IRWS_TAPS_AHEAD 1
+#endif
 template <int W, int KS>
 __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     ir_ws_kernel(const bf16_t* __restrict__ x, int N, int H, int cs_mid, const bf16_t* __restrict__ wpw,
                  const float* __restrict__ bpw, const float* __restrict__ wdw, const float* __restrict__ bdw,
                  bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, unsigned long long* __restrict__ trace,
                  unsigned spin_max, unsigned* __restrict__ err) {
+  constexpr bool HAND_END = IRWS_HAND_END == 2 ? W == 8 : IRWS_HAND_END, TAPS_AHEAD = IRWS_TAPS_AHEAD;
   constexpr int CS = KS * 32;  // input channel stride = expand K
   constexpr int CPP = (CS * 2 + 255) / 256 * 16;
   constexpr int CPR = 2 * CPP;  // 16-byte chunks per LDS x row
@@ -106,8 +132,10 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   char* xs = smem;
   char* tiles = xs + Lg.x_bytes;
   char* wbuf = tiles + Lg.tile_bytes;
-  float* wdl = reinterpret_cast<float*>(wbuf + Lg.w_bytes);  // [2][9 x 32 taps | 32 depthwise bias]
-  float* bpl = wdl + 2 * 320;                                 // [2][32] expand bias
+  // [3][9 x 32 taps | 32 depthwise bias]: three slots, so slice f + 1's taps can go out at the end of slice f
+  // under the tile buffer's own wait (consumers done with slice f - 2), not a later one
+  float* wdl = reinterpret_cast<float*>(wbuf + Lg.w_bytes);
+  float* bpl = wdl + 3 * 320;  // [2][32] expand bias
   // the squeeze: per channel the sum of the image's SiLU outputs as 32.32 fixed point, added by every consumer
   // wave of every band with an integer LDS atomic (the same bits in any arrival order); per slice index the
   // number of (band, wave) arrivals, whose last one turns the sums into the slice's SE means
@@ -137,9 +165,9 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
 
   auto TR = [&](int i, int k) {
 #ifdef IRWS_TRACE
-    if (trace && blockIdx.x == 0 && (wave == 0 || wave == WS_NP) && i < 64) {
+    if (trace && blockIdx.x == 0 && i < 64) {  // every wave of workgroup 0: slot = wave within its role
       const unsigned long long t = __builtin_amdgcn_s_memtime();
-      trace[((i * 2 + (wave == WS_NP)) * 8 + k) * 64 + lane] = t;
+      if (lane == 0) trace[((i * 2 + (wave >= WS_NP)) * 16 + k) * 64 + (wave & 7)] = t;
     }
 #else
     (void)i; (void)k; (void)trace;
@@ -216,7 +244,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   };
   auto issue_wd = [&](int f, Step d) {  // the slice's depthwise taps [9][32] + bias: 80 lanes of 16 B
     const int c0 = d.sl * WS_SL;
-    float* dst = wdl + (f & 1) * 320;
+    float* dst = wdl + (f % 3) * 320;
     // the lane's source offset is rebuilt here each time (asm barrier): hoisted out of the slice loop
     // it became two 64-bit pointers spilled to scratch, and their reload's vmcnt wait drained the
     // weight DMA in flight
@@ -242,21 +270,27 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       dma16(src, lds_addr(xs + j * 1024));
     }
   };
-  // after its MFMAs of slice f a producer wave counts itself done with W(f)'s slot; once all WS_NP are,
-  // it DMAs its pieces of W(f + 2) there, ~1.5 slices before they are needed (issued one slice ahead
-  // only, the wait for them was exposed: without the per-slice weight DMA ir_ws ran 11-15 % faster).
-  // W(f + 1)'s pieces of this wave landed before it counts itself done with slice f (only slice f's taps, on the two
-  // tap waves, were issued after them): so once every producer is done with slice f, W(f + 1) is complete too, and
-  // W(f + 2) may go into W(f)'s slot
+  // W ring (two slots): a producer wave counts itself done with W(f)'s slot right after its MFMAs of slice f
+  // (pdone, no wait there).  At the end of slice f, its epilogue stored, it waits for its own W(f + 1) pieces
+  // (issued a slice earlier: landed) and counts them in (wrdy), then waits until every producer is done with
+  // slice f (by then normally true: the wait is where the slowest wave's MFMAs have long ended, not right
+  // after this wave's own) and DMAs its pieces of W(f + 2) into W(f)'s slot.  Slice f + 1 starts once wrdy
+  // says W(f + 1) is complete.  (Waiting for pdone right after the MFMAs put the slowest wave's MFMA tail and
+  // the hand-off latency, ~800 cycles a slice, on every producer's critical path; in-kernel stamps r05k.)
   const bool tap_wave = wave >= WS_NP - 2;  // issue_wd's two waves
-  auto after_mfma = [&](int f, bool more, Step d2) {
-    if (tap_wave) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else wait_vm0();
-    bump(pdone);
-    if (f + 1 < T) wait_ge(pdone, (unsigned)(WS_NP * (f + 1)));
-    if (more) issue_w(f + 2, d2);
+  const int npw = (wave < 4 * KS ? (4 * KS - 1 - wave) / WS_NP + 1 : 0) + (wave == 0 ? 1 : 0);  // W pieces a slice
+  auto after_mfma = [&](int f, Step d2) {
+    if (HAND_END) {
+      bump(pdone);
+    } else {  // W(f + 1) of this wave landed (younger: only the tap waves' slice-f taps), then every producer's
+      if (tap_wave) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else wait_vm0();
+      bump(pdone);
+      if (f + 1 < T) wait_ge(pdone, (unsigned)(WS_NP * (f + 1)));
+      if (f + 2 < T) issue_w(f + 2, d2);
+    }
   };
-  auto produce = [&](int f, Step d, bool more, Step d2) {
+  auto produce = [&](int f, Step d, Step d2) {
     const int r0 = d.band * WS_BR, br = min(WS_BR, H - r0), xr0 = max(r0 - 1, 0), xr1 = min(r0 + WS_BR + 1, H);
     const int PB = (xr1 - xr0) * W, nunit = 2 * ((PB + 15) / 16);
     const char* wb = wbuf + (f & 1) * KS * 4096;
@@ -282,7 +316,10 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       f32x4 acc[NU];
 #pragma unroll
       for (int k = 0; k < NU; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-      bf16x8 ah[2], al[2], bh[2][NU], bl[2][NU];
+      // k-steps in flight: the LDS round trip under the consumers' tile reads is several hundred cycles, so a wave
+      // with one unit (8x8: 21 MFMAs a slice) keeps 3 k-steps of reads ahead, with 2 units 2, with 3 units 1
+      constexpr int D = !IRWS_PF_DEEP ? 2 : NU == 1 ? 4 : NU == 2 ? 3 : 2;
+      bf16x8 ah[D], al[D], bh[D][NU], bl[D][NU];
       auto load = [&](int ks, int bsel) {
         const int Lh = ks * 4 + g, Ll = CPP + ks * 4 + g;
         const int ph = ((Lh & ~15) | ((Lh & 15) ^ hxl)) << 4, pl = ((Ll & ~15) | ((Ll & 15) ^ hxl)) << 4;
@@ -295,11 +332,15 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
           bl[bsel][k] = *reinterpret_cast<const bf16x8*>(xr + pl);
         }
       };
-      load(0, 0);
+#pragma unroll
+      for (int ks = 0; ks < D - 1 && ks < KS; ++ks) load(ks, ks);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const int c = ks & 1;
-        if (ks + 1 < KS) load(ks + 1, c ^ 1);
+        const int c = ks % D;
+        if (ks + D - 1 < KS) load(ks + D - 1, (ks + D - 1) % D);
+        // keep the reads where they are: left to itself the scheduler sinks each one to its MFMA (least registers)
+        // and every k-step waits out a full LDS round trip
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k = 0; k < NU; ++k) {
           acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[c], bh[c][k], acc[k], 0, 0, 0);
@@ -308,8 +349,10 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
         }
       }
       TR(f, 6);
-      after_mfma(f, more, d2);
+      after_mfma(f, d2);
+      TR(f, 8);
       if (f >= 2) wait_all(tfree, (unsigned)(f - 1));  // every consumer is done with tile f - 2 (same buffer)
+      TR(f, 9);
       // bias + SiLU -> tile[f % 2]; lane holds channels 4g..4g+3 (of 16-channel tile nt) of position r16
 #pragma unroll
       for (int k = 0; k < NU; ++k) {
@@ -326,7 +369,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     else if (nu == 2) units(std::integral_constant<int, 2>());
     else if (nu == 1) units(std::integral_constant<int, 1>());
     else {
-      after_mfma(f, more, d2);
+      after_mfma(f, d2);
       if (f >= 2) wait_all(tfree, (unsigned)(f - 1));
     }
     // halo rows outside the image (above the first band, below the last) hold zeros
@@ -354,7 +397,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     const uint32_t yoff0 = __builtin_amdgcn_readfirstlane(4u * (uint32_t)c0) + 8u * (uint32_t)cg +
                            (pbase + (uint32_t)cpl) * (4u * (uint32_t)cs_mid);  // launch_ir_ws: < 2^32
     // lane = (4-channel plane cg, pixels cpl + 64 k): the plane's 9 taps stay in registers
-    const float* wd = wdl + (f & 1) * 320 + 4 * cg;
+    const float* wd = wdl + (f % 3) * 320 + 4 * cg;
     float w[9][4], b[4];
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
@@ -399,6 +442,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     }
     TR(f, 5);
     bump(tfree + cw);  // every tile and tap read of slice f returned: the producers may refill both buffers
+    TR(f, 10);
     // squeeze partials: the wave's 8 pixel lanes of each plane (lane bits 3..5): a DPP row rotation
     // inside each 16-lane row, then gfx950's row / half swaps (v_permlane16_swap, v_permlane32_swap: VALU,
     // no LDS round trip, where two ds_bpermute shuffles were); one row of 32 channels per wave
@@ -410,21 +454,27 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(s[j]), __float_as_uint(s[j]), false, false);
       s[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
     }
+    TR(f, 11);
     // lane L < 8 holds the wave's partial sums of plane L (channels c0 + 4 L ..): add them to the image's fixed-point
     // sums, then count this (band, wave) in; the last of the NB x WS_NC arrivals writes the slice's SE means and
     // clears the sums and the count for the next image (no wait on the other consumers: the atomics are the sync)
-    if (lane < 8)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        __hip_atomic_fetch_add(sq + c0 + 4 * lane + j, (unsigned long long)(long long)(s[j] * 4294967296.0f), __ATOMIC_RELAXED,
+    // (every lane with lane & 7 == L holds them after the shuffles: lane L + 8 j < 32 takes sum j, so one
+    // conversion and one atomic a lane cover the slice's 32 channels)
+    const int sc = 4 * (lane & 7) + ((lane >> 3) & 3);  // the lane's channel in the slice
+    {
+      const int j = (lane >> 3) & 3;
+      const float v = j == 0 ? s[0] : j == 1 ? s[1] : j == 2 ? s[2] : s[3];
+      if (lane < WS_SL)
+        __hip_atomic_fetch_add(sq + c0 + sc, (unsigned long long)(long long)(v * 4294967296.0f), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     unsigned arrived = 0;
     if (lane == 0) arrived = __hip_atomic_fetch_add(sq_n + d.sl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (__builtin_amdgcn_readfirstlane(arrived) == (unsigned)(NB * WS_NC - 1) && lane < WS_SL) {
-      const int c = c0 + lane;
-      const long long t = (long long)__hip_atomic_exchange(sq + c, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const float m = (float)((double)t * (1.0 / 4294967296.0) / (double)P);
-      act_st<sp_t>(reinterpret_cast<sp_t*>(se_mean), d.img, cs_mid, c, *poison ? __builtin_nanf("") : m);
+      const unsigned long long t = __hip_atomic_exchange(sq + c0 + sc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // 32.32 -> float: integer part (arithmetic high word) + fraction (low word)
+      const float m = __fmaf_rn((float)(unsigned)t, 2.3283064365386963e-10f, (float)(int)(t >> 32)) / (float)P;
+      act_st<sp_t>(reinterpret_cast<sp_t*>(se_mean), d.img, cs_mid, c0 + sc, *poison ? __builtin_nanf("") : m);
       if (lane == 0) sq_n[d.sl] = 0u;
     }
   };
@@ -435,44 +485,63 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   // producer finished the last band's.  Consumers wait only for their tiles (the squeeze is atomic).
   __syncthreads();  // the counters and the tiles' zero halo columns
   if (prod) {
-    // DMA pieces a producer wave issues per slice (W pieces j = wave + 8 k of 4 KS, + the bias on wave 0)
-    const int npw = (wave < 4 * KS ? (4 * KS - 1 - wave) / WS_NP + 1 : 0) + (wave == 0 ? 1 : 0);
+    __builtin_amdgcn_s_setprio(2);
     Step cur{(int)blockIdx.x, 0, 0};
     if (T > 0) issue_w(0, cur);
     if (T > 1) issue_w(1, next_step(cur));
-    if (T > 0) {  // W(0) landed everywhere (W(1) may stay in flight); later slices' W: after_mfma
-      if (T > 1 && npw == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else if (T > 1 && npw == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else if (T > 1 && npw == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else if (T > 1 && npw == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      else wait_vm0();
+    if (TAPS_AHEAD && T > 0 && tap_wave) issue_wd(0, cur);
+    if (T > 0) {  // W(0) landed (W(1) and the taps may stay in flight)
+      wait_vm_le((T > 1 ? npw : 0) + (TAPS_AHEAD && tap_wave ? 1 : 0));
       bump(wrdy);
-      wait_ge(wrdy, (unsigned)WS_NP);
+      if (!HAND_END) wait_ge(wrdy, (unsigned)WS_NP);
     }
+    static_assert(4 * KS <= 4 * WS_NP, "pieces per wave");
     int bands = 0;
     for (int i = 0; i < T; ++i) {
       const Step nxt = next_step(cur), nxt2 = next_step(nxt);
       TR(i, 0);
-      if (cur.sl == 0) {  // a new band: its input rows (every producer is done with the last band's: after_mfma)
+      if (cur.sl == 0) {  // a new band: its input rows, once every producer is done with the last band's
+        if (i > 0) wait_ge(pdone, (unsigned)(WS_NP * i));
         issue_x(cur.img, cur.band);
         wait_vm0();
         bump(xrdy);
         wait_ge(xrdy, (unsigned)(WS_NP * ++bands));
       }
-      static_assert(4 * KS <= 4 * WS_NP, "pieces per wave");
       TR(i, 1);
-      if (tap_wave) {  // slice i's taps into taps[i % 2], once the consumers are done with slice i - 2's
-        if (i >= 2) wait_all(tfree, (unsigned)(i - 1));
+      if (!TAPS_AHEAD && tap_wave) {  // slice i's taps into taps[i % 3], once every consumer is done with slice i - 3
+        if (i >= 3) wait_all(tfree, (unsigned)(i - 2));
         issue_wd(i, cur);
       }
+      if (HAND_END) wait_ge(wrdy, (unsigned)(WS_NP * (i + 1)));  // W(i) complete
       TR(i, 2);
-      produce(i, cur, i + 2 < T, nxt2);
-      if (tap_wave) {  // the taps landed: only W(i + 2)'s pieces were issued after them
-        if (i + 2 < T && npw == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else if (i + 2 < T && npw == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else wait_vm0();
+      produce(i, cur, nxt2);
+      if (HAND_END) {
+        // W(i + 1) and (tap waves) slice i's taps landed: nothing else of this wave's is in flight
+        wait_vm0();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile stores
+        if (lane == 0) {
+          asm volatile("ds_add_u32 %0, %1" ::"v"((uint32_t)(uintptr_t)wrdy), "v"(1u) : "memory");
+          asm volatile("ds_add_u32 %0, %1" ::"v"((uint32_t)(uintptr_t)tfull), "v"(1u) : "memory");
+        }
+        TR(i, 12);
+        const bool nw = i + 2 < T, nt = TAPS_AHEAD && tap_wave && i + 1 < T;
+        if (nw || nt) {
+          // W(i)'s slot is free once every producer is done with slice i.  Slice i + 1's taps go to taps[(i + 1) % 3],
+          // which held slice i - 2's: produce(i) waited for every consumer to be done with that slice before its
+          // tile stores.  Both land during slice i + 1
+          wait_ge(pdone, (unsigned)(WS_NP * (i + 1)));
+          if (nw) issue_w(i + 2, nxt2);
+          if (nt) issue_wd(i + 1, nxt);
+        }
+      } else {
+        if (tap_wave) {  // slice i's taps landed; younger: W(i + 2) (after_mfma) and, ahead, slice i + 1's taps
+          const bool nt = TAPS_AHEAD && i + 1 < T;
+          if (nt) issue_wd(i + 1, nxt);
+          wait_vm_le((i + 2 < T ? npw : 0) + (nt ? 1 : 0));
+        }
+        bump(tfull);
+        TR(i, 12);
       }
-      bump(tfull);
       TR(i, 3);
       cur = nxt;
     }
@@ -493,16 +562,29 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
 static void dump_trace(unsigned long long* tr, hipStream_t s, const char* tag) {
   static int calls = 0;
   if (++calls > 40) return;
-  std::vector<unsigned long long> h(64 * 2 * 8 * 64);
+  std::vector<unsigned long long> h(64 * 2 * 16 * 64);
   M2S_HIP(hipStreamSynchronize(s));
   M2S_HIP(hipMemcpy(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost));
-  auto at = [&](int i, int c, int k) { return (long long)h[((i * 2 + c) * 8 + k) * 64]; };
+  auto at = [&](int i, int c, int k, int w = 0) { return (long long)h[((i * 2 + c) * 16 + k) * 64 + w]; };
   fprintf(stderr, "TRACE %s:", tag);
   for (int i = 2; i < 12; ++i)
-    // producer: band x, taps issued, MFMAs (+ W hand-off), epilogue; consumer: tile wait, pixels, squeeze
-    fprintf(stderr, " [P w %lld tap %lld mfma %lld epi %lld | C wait %lld px %lld sq %lld]", at(i, 0, 1) - at(i, 0, 0),
-            at(i, 0, 2) - at(i, 0, 1), at(i, 0, 6) - at(i, 0, 2), at(i, 0, 3) - at(i, 0, 6), at(i, 1, 4) - at(i - 1, 1, 7),
-            at(i, 1, 5) - at(i, 1, 4), at(i, 1, 7) - at(i, 1, 5));
+    // producer: band x, W wait, MFMAs, tile-free wait, epilogue + counts, W / taps hand-off;
+    // consumer: tile wait, pixels, tfree bump, shuffles, atomics (+ SE mean)
+    fprintf(stderr, " [P x %lld wr %lld mfma %lld tf %lld epi %lld hand %lld | C wait %lld px %lld bump %lld shf %lld at %lld]",
+            at(i, 0, 1) - at(i, 0, 0), at(i, 0, 2) - at(i, 0, 1), at(i, 0, 6) - at(i, 0, 2), at(i, 0, 9) - at(i, 0, 6),
+            at(i, 0, 12) - at(i, 0, 9), at(i, 0, 3) - at(i, 0, 12), at(i, 1, 4) - at(i - 1, 1, 7), at(i, 1, 5) - at(i, 1, 4),
+            at(i, 1, 10) - at(i, 1, 5), at(i, 1, 11) - at(i, 1, 10), at(i, 1, 7) - at(i, 1, 11));
+  fprintf(stderr, "\n");
+  // per producer wave, relative to wave 0's slice start: MFMA start / end / done-count bump
+  fprintf(stderr, "TRACEW %s:", tag);
+  for (int i = 2; i < 4; ++i) {  // start / MFMA start / MFMA end / tiles free / stored + counted / end
+    fprintf(stderr, " [s%d", i);
+    for (int w = 0; w < 8; ++w) {
+      fprintf(stderr, " w%d", w);
+      for (int k : {0, 2, 6, 9, 12, 3}) fprintf(stderr, "%c%lld", k ? '/' : ' ', at(i, 0, k, w) - at(i, 0, 0));
+    }
+    fprintf(stderr, "]");
+  }
   fprintf(stderr, "\n");
   M2S_HIP(hipMemset(tr, 0, h.size() * 8));
 }
@@ -530,7 +612,7 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
 #ifdef IRWS_TRACE
   static unsigned long long* tr = [] {
     unsigned long long* p = nullptr;
-    if (getenv("M2S_IR_WS_TRACE")) M2S_HIP(hipMalloc(&p, 64 * 2 * 8 * 64 * 8));
+    if (getenv("M2S_IR_WS_TRACE")) M2S_HIP(hipMalloc(&p, 64 * 2 * 16 * 64 * 8));
     return p;
   }();
 #define M2S_IRWS_DUMP(tag) \
