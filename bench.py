@@ -59,13 +59,14 @@ PRECISION = {
             "input projection/head/glue fp32",
     "fp8": "e4m3 storage + block-scaled e4m3 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, per-output-channel "
            "weight scales) for the stride-1 IR blocks' expand, expanded maps and SE-gated conv_pwl GEMMs, the "
-           "EdgeResidual blocks.1.1/.2 (conv_exp + conv_pwl) and the C=128/256 MRF convs; the other convs (stem, "
-           "EdgeResidual blocks.1.0/2.x, IR depthwise, C=32/64 MRF, upsamplers) bf16; BiLSTM recurrence 3-term split products (B > 4), input projection/head/glue fp32",
+           "EdgeResidual blocks.1.1/.2 and blocks.2.1/.2 (conv_exp + conv_pwl) and the C=128/256 MRF convs; the other "
+           "convs (stem, stride-2 EdgeResidual blocks.1.0/2.0 and IR blocks.3.0/5.0, IR depthwise, C=32/64 MRF, "
+           "upsamplers) bf16; BiLSTM recurrence 3-term split products (B > 4), input projection/head/glue fp32",
 }
 
 MFMA_KERNELS = ("conv_gemm_kernel", "gemm128_kernel", "conv_halo_kernel", "conv1d_halo", "conv_igemm_kernel", "ir_pwdw",
                 "ir_ws_kernel", "se_ws_kernel", "lstm_persistent_kernel", "lstm_x3_kernel", "rb1_fused_kernel", "stem_b0_kernel", "se_excite_kernel",
-                "er_fused_kernel", "er8_fused_kernel", "er2_fused_kernel", "ers2_fused_kernel", "er_sp_kernel", "ers2_sp_kernel")
+                "er_fused_kernel", "er8_fused_kernel", "er8w_fused_kernel", "er2_fused_kernel", "ers2_fused_kernel", "er_sp_kernel", "ers2_sp_kernel")
 
 
 def kernel_arith(name: str, dtype: str) -> str:
@@ -78,7 +79,7 @@ def kernel_arith(name: str, dtype: str) -> str:
     if dtype == "fp8":  # only the e4m3 kernels run fp8 MFMA; the rest of an fp8 engine is bf16
         e4m3 = (name.startswith(("gemm128_kernel<0", "gemm128_kernel<1")) or (name.startswith("se_ws_kernel") and "true" in name)
                 or (name.startswith("ir_pwdw_kernel<") and name.rstrip(">").endswith(", 3"))  # the e4m3 expand
-                or name.startswith("er8_fused_kernel"))
+                or name.startswith(("er8_fused_kernel", "er8w_fused_kernel")))
         return "fp8" if e4m3 else "bf16"
     return dtype
 

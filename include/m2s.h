@@ -53,9 +53,12 @@ enum m2s_status { M2S_OK = 0, M2S_E_ARG = 1, M2S_E_HIP = 2, M2S_E_STATE = 3, M2S
  *                 accumulation; meets the fp32 tolerances of the parity tests
  *   M2S_DT_FP8    configs[4]: OCP e4m3 storage and block-scaled e4m3 MFMA
  *                 (v_mfma_scale_f32_16x16x128_f8f6f4, unit E8M0 block scales, per-output-channel
- *                 fp32 weight scales applied in the epilogue) for the IR blocks' expanded maps and
- *                 SE-gated conv_pwl GEMMs and the C = 128 / 256 MRF convs; every other conv is the
- *                 bf16 path */
+ *                 fp32 weight scales applied in the epilogue) for: the stride-1 IR blocks' conv_pw
+ *                 expand, expanded maps and SE-gated conv_pwl GEMMs; the EdgeResidual blocks.1.1/.2
+ *                 and blocks.2.1/.2 (conv_exp + conv_pwl); the C = 128 / 256 MRF convs.  The stem,
+ *                 the stride-2 blocks (EdgeResidual blocks.1.0 / 2.0, IR blocks.3.0 / 5.0), the IR
+ *                 depthwise convs (fp32 accumulation of a bf16 tile), the C = 32 / 64 MRF convs and
+ *                 the upsamplers run the bf16 path */
 enum m2s_dtype { M2S_DT_F32 = 0, M2S_DT_BF16 = 1, M2S_DT_BF16X3 = 2, M2S_DT_FP8 = 3 };
 /* host tensor element types */
 enum m2s_elem { M2S_ELEM_F32 = 0, M2S_ELEM_I64 = 1 };

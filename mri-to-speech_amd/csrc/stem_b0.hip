@@ -9,7 +9,10 @@
 //   S = stem output on (TH+4) x 20 pixels (32 ch), A = blocks.0.0 output on (TH+2) x 18 (16 ch).
 // Pixels outside the image are stored as exact zeros: they are the next conv's zero padding.
 //
-//   phase 1  stem on VALU in fp32 (one thread per S pixel, 32 channels, weights as scalar operands)
+//   phase 1  stem on MFMA 16x16x32 bf16, split into three terms (hi*hi + hi*lo + lo*hi, both engines):
+//            A = the 32 x 9 weights resident in VGPRs, B = 16 S pixels x their 9 frame values, prefetched a
+//            tile ahead in registers.  K = 32 holds tap row ky at k = 8 ky .. 8 ky + 2 (lane group g = ky < 3
+//            carries the three taps of one frame row; the other k are zero), so a lane keeps 3 values a pixel
 //   phase 2  blocks.0.0 on MFMA 16x16x32 bf16: weights (16 x 288) resident in VGPRs as 9 A
 //            fragments, B = 16 A-pixels x 32 channels of one tap from S
 //   phase 3  blocks.0.1 likewise (16 x 160: two taps of 16 channels per K step), + skip from A.
@@ -107,44 +110,43 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
   const int gx = gridDim.x / 8, xcd = blockIdx.x % 8;
   const int s_end = min(nstrip, (xcd + 1) * a.per_xcd);
 
-  // ---- phase-1 work of a tile: this thread's full pixel (32 channels) and its quarter pixels (the 8
-  // channels of group qg), both as S plane indices.  First tile of a strip: 400 pixels = 256 full + 144
-  // by quarters; later tiles: the 320 pixels of rows 4..19 = 256 full + 64 by quarters (40 channels a
-  // thread, balanced).  A wave's quarter lanes are 4 groups x 16 consecutive pixels: conflict-free stores.
-  // (t = the thread index, re-materialised per tile by the caller: addresses derived from it and hoisted
-  // out of the tile loop for both the first-tile and the later-tile variants spilled to scratch)
-  auto slot_px = [&](bool first, int k, int t) -> int {  // k = 0: full pixel; 1..3: quarter pixels (-1: none)
-    const int qoff = 16 * (t >> 6) + (t & 15);
-    if (k == 0) return first ? OFS + t : OFS + 4 * SB_SW + t;
-    const int m = k - 1;
-    if (first) return (m < 2 || qoff < 16) ? OFS + 256 + 64 * m + qoff : -1;
-    return m == 0 ? OFS + 4 * SB_SW + 256 + qoff : -1;
-  };
-  // frame values of slot k's 9 stem taps (zeros outside the frame / the map)
-  auto load9 = [&](float* x9, int st, int ty, int k, int t) {
+  // ---- phase-1 work of a tile: S position subtiles j (16 S pixels OFS + 16 j ..), j = j0 + wave + 4 i: a
+  // strip's first tile all 25 (rows 0..19), later tiles the 20 of rows 4..19 (j0 = 5; rows 0..3 are carried).
+  // A lane's B operand: pixel r16 of its subtile, k = 8 g + kx = tap (ky = g, kx) for g < 3 and kx < 3, else 0.
+  constexpr int SJ = SPIX / 16 - OFS / 16;  // 25 S subtiles
+  static_assert(OFS % 16 == 8 || OFS % 16 == 0, "subtile base");
+  constexpr int NPF = 5;                    // subtiles a wave prefetches (later tiles: exactly 5)
+  // raw loads at clamped (always valid) addresses; the padding mask (3 bits) is applied when the values are used,
+  // so nothing consumes a prefetched load before the next tile (a select right after each load made the compiler
+  // wait for every one of them, ~4k cycles of exposed HBM latency a tile)
+  auto load3 = [&](float* x3, int st, int ty, int j) -> unsigned {
     const int n = st / a.tiles_x, tx0 = (st - n * a.tiles_x) * SB_TW, ty0 = ty * TH;
     const float* fr = a.frames + (size_t)n * a.H * a.W;
-    const int px = slot_px(ty == 0, k, t);
-    const int i = px - OFS, sy = i / SB_SW, sx = i - (i / SB_SW) * SB_SW;
+    const int i = 16 * j + r16, sy = i / SB_SW, sx = i - (i / SB_SW) * SB_SW;
     const int oy = ty0 - 2 + sy, ox = tx0 - 2 + sx;  // stem output pixel
-    const bool ok = px >= 0 && oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW;
+    const int iy = oy * 2 - a.pad_t + g, ix0 = ox * 2 - a.pad_l;
+    const bool ok = j < SJ && g < 3 && oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW && iy >= 0 && iy < a.H;
+    // unconditional loads at clamped addresses, then the zero padding by select
+    const float* row = fr + (size_t)min(max(iy, 0), a.H - 1) * a.W;
+    unsigned m = 0;
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int iy = oy * 2 - a.pad_t + ky, ix = ox * 2 - a.pad_l + kx;
-        x9[ky * 3 + kx] = (ok && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) ? fr[(size_t)iy * a.W + ix] : 0.f;
-      }
+    for (int kx = 0; kx < 3; ++kx) {
+      const int ix = ix0 + kx;
+      x3[kx] = row[min(max(ix, 0), a.W - 1)];
+      m |= (ok && ix >= 0 && ix < a.W) ? 1u << kx : 0u;
+    }
+    return m;
   };
-  // slots 0 and 1 of the next tile are prefetched into registers (they land while phases 2 and 3 run);
-  // a strip's first tile loads its two further quarter slots when it needs them
-  float in[2][9];
-  auto load_in = [&](int st, int ty, int t) {
-    load9(in[0], st, ty, 0, t);
-    load9(in[1], st, ty, 1, t);
+  float xin[NPF][3];
+  unsigned xm = 0;  // 3 mask bits per prefetched subtile
+  auto load_in = [&](int st, int ty) {
+    const int j0 = ty == 0 ? 0 : 5;
+    xm = 0;
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) xm |= load3(xin[i], st, ty, j0 + wave + 4 * i) << (3 * i);
   };
   int st = xcd * a.per_xcd + (int)blockIdx.x / 8, ty = 0;
-  if (st < s_end) load_in(st, 0, tid);
+  if (st < s_end) load_in(st, 0);
 
   // resident weights of both convs (A fragments)
   bf16x8 wf0[9], wf1[5], wl0[SP ? 9 : 1], wl1[SP ? 5 : 1];
@@ -160,42 +162,25 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
     wf1[k] = *reinterpret_cast<const bf16x8*>(w);
     if constexpr (SP) wl1[k] = *reinterpret_cast<const bf16x8*>(w + a.kp1);
   }
-  // the stem's weights and biases in LDS, tap-major ([k][32 channels] + 32 biases): read from global
-  // inside the tile loop they were vector loads (the loop's stores of y rule out scalar loads)
-  __shared__ __attribute__((aligned(16))) float sw9[288 + 32];
-  for (int i = tid; i < 320; i += 256) sw9[i] = i < 288 ? a.w9[(i % 32) * 9 + i / 32] : a.b9[i - 288];
+  // the stem's weights in LDS as the lanes' A-fragment values: [channel tile][lane (g, r16)] 4 floats = taps
+  // (ky = g, kx = 0..2) of channel ni * 16 + r16 and 0 (g = 3: zeros), and the biases; a subtile reads its
+  // two fragments (split there) and biases instead of keeping them in registers, which phase 2's resident
+  // weights leave none of
+  __shared__ __attribute__((aligned(16))) float sw9[2 * 64 * 4 + 32];
+  for (int i = tid; i < 2 * 64 * 4 + 32; i += 256) {
+    float v = 0.f;
+    if (i < 512) {
+      const int ni = i >> 8, ln = (i >> 2) & 63, kx = i & 3, gg = ln >> 4;
+      if (gg < 3 && kx < 3) v = a.w9[(ni * 16 + (ln & 15)) * 9 + 3 * gg + kx];
+    } else {
+      v = a.b9[i - 512];
+    }
+    sw9[i] = v;
+  }
   const float4 bb0 = *reinterpret_cast<const float4*>(a.b0 + 4 * g);
   const float4 bb1 = *reinterpret_cast<const float4*>(a.b1 + 4 * g);
-  __syncthreads();
+  __syncthreads();  // sw9
 
-  // 8 stem channels (group grp) of one S pixel from its 9 frame values -> S planes (hi, lo): eight
-  // independent FMA chains, the tap's 8 weights by two 16-byte LDS reads (tap-major [k][32 channels])
-  auto stem8 = [&](const float* x9, int grp, bool ok, int px) {
-    float acc[8];
-    {
-      const float4 b0 = *reinterpret_cast<const float4*>(&sw9[288 + grp * 8]);
-      const float4 b1 = *reinterpret_cast<const float4*>(&sw9[288 + grp * 8 + 4]);
-      acc[0] = b0.x; acc[1] = b0.y; acc[2] = b0.z; acc[3] = b0.w;
-      acc[4] = b1.x; acc[5] = b1.y; acc[6] = b1.z; acc[7] = b1.w;
-    }
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      const float4 w0 = *reinterpret_cast<const float4*>(&sw9[k * 32 + grp * 8]);
-      const float4 w1 = *reinterpret_cast<const float4*>(&sw9[k * 32 + grp * 8 + 4]);
-      acc[0] += w0.x * x9[k]; acc[1] += w0.y * x9[k]; acc[2] += w0.z * x9[k]; acc[3] += w0.w * x9[k];
-      acc[4] += w1.x * x9[k]; acc[5] += w1.y * x9[k]; acc[6] += w1.z * x9[k]; acc[7] += w1.w * x9[k];
-    }
-    uint32_t v[4], vl[4];
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const float s0 = silu(acc[j]), s1 = silu(acc[j + 1]);
-      v[j / 2] = ok ? pack_bf16x2(s0, s1) : 0u;
-      if constexpr (SP)  // lo halves: v - hi
-        vl[j / 2] = ok ? pack_bf16x2(s0 - __uint_as_float(v[j / 2] << 16), s1 - __uint_as_float(v[j / 2] & 0xffff0000u)) : 0u;
-    }
-    *reinterpret_cast<uint4*>(sS + grp * SPLANE + px * 16) = make_uint4(v[0], v[1], v[2], v[3]);
-    if constexpr (SP) *reinterpret_cast<uint4*>(sS + SLO + grp * SPLANE + px * 16) = make_uint4(vl[0], vl[1], vl[2], vl[3]);
-  };
   auto copy16 = [&](char* base, int from, int to) {  // one 16-byte LDS chunk, hi (and lo) planes
     *reinterpret_cast<uint4*>(base + to) = *reinterpret_cast<const uint4*>(base + from);
   };
@@ -211,45 +196,69 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
   while (st < s_end) {
     const int n = st / a.tiles_x, tx0 = (st - n * a.tiles_x) * SB_TW, ty0 = ty * TH;
     const bool first = ty == 0;
-    int tl = tid;
-    asm volatile("" : "+v"(tl));
-    const int g = (tl & 63) >> 4, r16 = tl & 15, qg = (tl & 63) >> 4;
     TR(0);
     // ---- phase 1: stem (fp32 VALU) -> S -----------------------------------------------------
     // (S is free: every wave passed the previous tile's phase-2 barrier before reaching here.)
     {
-      // a later tile first moves the S rows it shares with the previous one (16..19 -> 0..3): each
-      // thread copies exactly the chunks it is about to overwrite, before it writes them
-      if (!first) {
-        const int fpx = slot_px(false, 0, tl), qpx = slot_px(false, 1, tl);
-        if (fpx >= OFS + SHIFT) {
+      const int j0 = first ? 0 : 5;
 #pragma unroll
-          for (int p = 0; p < 4 * R; ++p) copy16(sS + p * SPLANE, fpx * 16, (fpx - SHIFT) * 16);
+      for (int i = 0; i < 7; ++i) {
+        const int j = j0 + wave + 4 * i;  // wave-uniform
+        if (j >= SJ) break;
+        float xl[3];
+        const float* x3 = xin[i < NPF ? i : 0];
+        unsigned m3 = (xm >> (3 * (i < NPF ? i : 0))) & 7u;
+        if (i >= NPF) {  // a strip's first tile: its last rows, loaded now
+          m3 = load3(xl, st, ty, j);
+          x3 = xl;
         }
-        copy16(sS + qg * SPLANE, qpx * 16, (qpx - SHIFT) * 16);
-        if constexpr (SP) copy16(sS + SLO + qg * SPLANE, qpx * 16, (qpx - SHIFT) * 16);
-      }
+        const int px = OFS + 16 * j + r16;
+        // a later tile's rows 16..19 move to 0..3 first (this wave's subtiles j >= 20: the copy's reads precede
+        // its own writes in LDS order); lane (g, r16) = plane g of pixel r16
+        if (!first && j >= 20) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int px = slot_px(first, k, tl);
-        if (px < 0) continue;
-        const int i = px - OFS, sy = i / SB_SW, sx = i - (i / SB_SW) * SB_SW;
+          for (int h = 0; h < R; ++h) copy16(sS + h * SLO + g * SPLANE, px * 16, (px - SHIFT) * 16);
+        }
+        const float x4[4] = {m3 & 1u ? x3[0] : 0.f, m3 & 2u ? x3[1] : 0.f, m3 & 4u ? x3[2] : 0.f, 0.f};
+        uint2 xh, xlo;
+        split4(x4, xh, xlo);
+        const bf16x8 bh = __builtin_bit_cast(bf16x8, make_uint4(xh.x, xh.y, 0u, 0u));
+        const bf16x8 bl = __builtin_bit_cast(bf16x8, make_uint4(xlo.x, xlo.y, 0u, 0u));
+        int ln = lane;  // rebuilt per subtile: hoisted, the weight addresses stayed live across phases 2 and 3
+        asm volatile("" : "+v"(ln));
+        const int si = 16 * j + r16, sy = si / SB_SW, sx = si - (si / SB_SW) * SB_SW;
         const int oy = ty0 - 2 + sy, ox = tx0 - 2 + sx;
         const bool ok = oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW;
-        if (k == 0) {
 #pragma unroll
-          for (int grp = 0; grp < 4; ++grp) stem8(in[0], grp, ok, px);
-        } else if (k == 1) {
-          stem8(in[1], qg, ok, px);
-        } else {
-          float x9[9];
-          load9(x9, st, ty, k, tl);
-          stem8(x9, qg, ok, px);
+        for (int ni = 0; ni < 2; ++ni) {
+          const float4 w4 = *reinterpret_cast<const float4*>(&sw9[(ni * 64 + ln) * 4]);
+          const float4 b4 = *reinterpret_cast<const float4*>(&sw9[512 + ni * 16 + 4 * (ln >> 4)]);
+          const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+          uint2 wh, wl;
+          split4(wv, wh, wl);
+          const bf16x8 wsh = __builtin_bit_cast(bf16x8, make_uint4(wh.x, wh.y, 0u, 0u));
+          const bf16x8 wsl = __builtin_bit_cast(bf16x8, make_uint4(wl.x, wl.y, 0u, 0u));
+          const f32x4 acc = mma3(wsh, wsl, bh, bl, f32x4{b4.x, b4.y, b4.z, b4.w});
+          const float v[4] = {silu(acc[0]), silu(acc[1]), silu(acc[2]), silu(acc[3])};
+          uint2 hi = make_uint2(0u, 0u), lo = make_uint2(0u, 0u);
+          if (ok) {
+            if constexpr (SP) {
+              split4(v, hi, lo);
+            } else {
+              hi.x = pack_bf16x2(v[0], v[1]);
+              hi.y = pack_bf16x2(v[2], v[3]);
+            }
+          }
+          // channels ni * 16 + 4 g .. : plane 2 ni + g / 2, the (g & 1) half of its 16 bytes
+          char* d = sS + (2 * ni + (g >> 1)) * SPLANE + px * 16 + (g & 1) * 8;
+          *reinterpret_cast<uint2*>(d) = hi;
+          if constexpr (SP) *reinterpret_cast<uint2*>(d + SLO) = lo;
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
       // the next tile's frame pixels, in flight through phases 2 and 3
       const int nst = ty + 1 < a.tiles_y ? st : st + gx, nty = ty + 1 < a.tiles_y ? ty + 1 : 0;
-      if (nst < s_end) load_in(nst, nty, tl);
+      if (nst < s_end) load_in(nst, nty);
     }
     TR(1);
     __syncthreads();
