@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(512, 1) er8w_fused_kernel(const Er8wArgs a) {
   constexpr int NSTORE = Y8 ? 16 : 8;  // stores per wave and tile
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, r16 = lane & 15;
+  const int r16 = lane & 15;  // (the lane group g is rebuilt per stage from an opaque lane id)
   const int tpi = a.tiles_x * a.tiles_y, ntiles = a.N * tpi;
   const uint32_t sm0 = lds_off(smem);
 

@@ -1,23 +1,23 @@
-// Split-fp32 InvertedResidual front half for the stride-1 blocks on 16x16 and 8x8 maps, as one
-// persistent warp-specialised workgroup per CU:
+// Split-fp32 InvertedResidual front half for the stride-1 blocks on 16x16 and 8x8 maps and the stride-2 block
+// at 16x16 (blocks.5.0), as one persistent warp-specialised workgroup per CU:
 //   conv_pw (1x1 expand, 3-term MFMA) + bn1 + SiLU -> fp32 LDS tile -> conv_dw 3x3 + bn2 + SiLU -> HBM
 //   + the SE squeeze (per-image channel means).
 // (timm InvertedResidual conv_pw/bn1/conv_dw/bn2/se.mean; mri_acoustic_model.py:28-34.)  Same outputs
-// as ir_pwdw_kernel<.., SP = 1> (ir_fused.hip), which launches one short workgroup per (images, 32-
-// channel slice) and spends most of its ~16 us life waiting on a chain of loads and barriers.
+// as ir_pwdw_kernel<.., SP = 1> / ir_pwdw_s2_kernel<1> (ir_fused.hip), which launch one short workgroup per
+// (images, 32-channel slice) and spend most of their life waiting on a chain of loads and barriers.
 //
-// A workgroup (16 waves) owns whole images and walks their 32-channel slices:
-//   waves 0-7 (producers): the image's input rows sit in LDS (loaded once per band of 8 output rows
-//     plus the halo rows, by LDS-DMA); the slice's expand weights, biases and depthwise taps stream
-//     through double-buffered LDS stages (DMA one slice ahead).  MFMA A = weights (16 channels x 32
-//     k), B = 16 positions x 32 k, three terms hi*hi + hi*lo + lo*hi; SiLU(acc + b) -> tile[f % 2].
-//   waves 8-15 (consumers): the depthwise of the PREVIOUS slice from tile[(f - 1) % 2] (a lane = 4
-//     channels x 1-2 pixels, fp32 taps in registers, no bounds checks: the tile carries a zero halo),
-//     SiLU, split-fp32 stores, and the squeeze partial sums.
-// Every weight, tap and bias reaches LDS by DMA from the producers, so the consumers issue no loads
-// (a load's wait would also drain their in-flight stores).  One barrier per slice orders both; each
-// SIMD holds two producer and two consumer waves, whose MFMA and VALU work interleave.  Bands of one
-// image run back to back in the same workgroup, so the squeeze sums of a 16x16 image accumulate in LDS.
+// A workgroup (16 waves) owns whole images and walks their (band of 8 input rows, 32-channel slice) steps:
+//   waves 0-7 (producers): the band's input rows (+ halo rows) sit in LDS (LDS-DMA once per band); the
+//     slice's expand weights and biases stream through a two-slot ring, the depthwise taps through three
+//     slots (LDS-DMA one to two slices ahead).  MFMA A = weights (16 channels x 32 k), B = 16 positions x
+//     32 k, three terms hi*hi + hi*lo + lo*hi; SiLU(acc + b) -> tile[f % 2].
+//   waves 8-15 (consumers): the depthwise of slice f from tile[f % 2] (a lane = 4 channels x 1-2 pixels,
+//     fp32 taps in registers, no bounds checks: the tile carries a zero halo), SiLU, split-fp32 stores, and
+//     the squeeze: per-wave channel sums added to the image's 32.32 fixed-point sums by LDS atomics.
+// No workgroup barrier after the start: the roles hand off through monotonic LDS counters (below), every
+// wait bounded (a timeout is reported and NaNs the images' SE means).  Every weight, tap and bias reaches
+// LDS by DMA from the producers, so the consumers issue no loads (a load's wait would also drain their
+// in-flight stores).  Each SIMD holds two producer and two consumer waves, whose MFMA and VALU interleave.
 //
 // LDS layouts (reads conflict-free for ds_read_b128's lane groups, MI355X_MICROARCH.md LDS table):
 //   x     [pos][hi plane | lo plane], planes padded to 256-byte multiples; 16-byte chunk L of row r
@@ -112,12 +112,18 @@ __host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mi
 #ifndef IRWS_TAPS_AHEAD
 #define IRWS_TAPS_AHEAD 1
 #endif
-template <int W, int KS>
+// S = depthwise stride.  S = 2 (blocks.5.0, 16x16 -> 8x8, TF-SAME pads pad_t / pad_l): the producers expand the
+// same input bands; a band's output rows are its 4 stride-2 rows, one pixel a consumer lane (lanes of consumer
+// waves 0-3; waves 4-7 only take part in the hand-offs and the squeeze count).
+template <int W, int KS, int S>
 __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     ir_ws_kernel(const bf16_t* __restrict__ x, int N, int H, int cs_mid, const bf16_t* __restrict__ wpw,
                  const float* __restrict__ bpw, const float* __restrict__ wdw, const float* __restrict__ bdw,
                  bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, unsigned long long* __restrict__ trace,
-                 unsigned spin_max, unsigned* __restrict__ err) {
+                 unsigned spin_max, unsigned* __restrict__ err, int pad_t, int pad_l) {
+  static_assert(S == 1 || (S == 2 && W == 16), "stride 2: the 16-wide maps");
+  constexpr int OWS = W / S;                      // output row width
+  constexpr int OPB = (WS_BR / S) * OWS;          // output pixels of a full band
   constexpr bool HAND_END = IRWS_HAND_END == 2 ? W == 8 : IRWS_HAND_END, TAPS_AHEAD = IRWS_TAPS_AHEAD;
   constexpr int CS = KS * 32;  // input channel stride = expand K
   constexpr int CPP = (CS * 2 + 255) / 256 * 16;
@@ -128,6 +134,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const WsLayout Lg = ws_layout(H, W, CS, cs_mid);
   const int NB = (H + WS_BR - 1) / WS_BR, NS = cs_mid / WS_SL, P = H * W;
+  const int PO = S == 1 ? P : ((H + 1) / 2) * OWS;  // output pixels of an image (TF-SAME)
   const int PLT = Lg.TROWS * 16;
   char* xs = smem;
   char* tiles = xs + Lg.x_bytes;
@@ -388,12 +395,15 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   // (il_st4: position p, channel c -> element p * 2 cs + 2 (c & ~31) + (c & 31)) 64 positions apart.
   // The byte offset of a store is one 24-bit multiply-add on the band's scalar position base; the
   // per-pixel 64-bit position arithmetic (two v_mul_lo_u32 a pixel) was a fifth of the consumer VALU.
-  const int toff0 = ((cpl / W) * WT + cpl % W) * 16;
+  // (S = 2: output pixel cpl = (row oy, col ox) of the band's 4 rows; its window's top-left tile row and column
+  // are 2 oy - pad_t + 1 and 2 ox - pad_l + 1 (tile row = input row - r0 + 1, column = input column + 1))
+  const int toff0 = S == 1 ? ((cpl / W) * WT + cpl % W) * 16
+                           : ((2 * (cpl / OWS) - pad_t + 1) * WT + 2 * (cpl % OWS) - pad_l + 1) * 16;
   auto consume = [&](int f, Step d) {
     const int c0 = d.sl * WS_SL, r0 = d.band * WS_BR, br = min(WS_BR, H - r0);
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     TR(f, 4);
-    const uint32_t pbase = (uint32_t)(d.img * P + r0 * W);  // uniform
+    const uint32_t pbase = (uint32_t)(d.img * PO + (r0 / S) * OWS);  // uniform
     const uint32_t yoff0 = __builtin_amdgcn_readfirstlane(4u * (uint32_t)c0) + 8u * (uint32_t)cg +
                            (pbase + (uint32_t)cpl) * (4u * (uint32_t)cs_mid);  // launch_ir_ws: < 2^32
     // lane = (4-channel plane cg, pixels cpl + 64 k): the plane's 9 taps stay in registers
@@ -432,7 +442,9 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       *reinterpret_cast<uint2*>(u) = hi;
       *reinterpret_cast<uint2*>(u + 64) = lo;
     };
-    if (br == WS_BR) {  // a full band: every lane's pixels exist, so their chains interleave
+    if constexpr (S == 2) {
+      if (cpl < OPB) pixel(0);  // (the bands of a 16-row map are full)
+    } else if (br == WS_BR) {  // a full band: every lane's pixels exist, so their chains interleave
 #pragma unroll
       for (int k = 0; k < WS_PXL; ++k) pixel(k);
     } else {
@@ -473,7 +485,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     if (__builtin_amdgcn_readfirstlane(arrived) == (unsigned)(NB * WS_NC - 1) && lane < WS_SL) {
       const unsigned long long t = __hip_atomic_exchange(sq + c0 + sc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       // 32.32 -> float: integer part (arithmetic high word) + fraction (low word)
-      const float m = __fmaf_rn((float)(unsigned)t, 2.3283064365386963e-10f, (float)(int)(t >> 32)) / (float)P;
+      const float m = __fmaf_rn((float)(unsigned)t, 2.3283064365386963e-10f, (float)(int)(t >> 32)) / (float)PO;
       act_st<sp_t>(reinterpret_cast<sp_t*>(se_mean), d.img, cs_mid, c0 + sc, *poison ? __builtin_nanf("") : m);
       if (lane == 0) sq_n[d.sl] = 0u;
     }
@@ -592,6 +604,11 @@ static void dump_trace(unsigned long long* tr, hipStream_t s, const char* tag) {
 
 }  // namespace
 
+bool ir_ws_s2_supported(int H, int W, int cs_in, int kp, int cs_mid, int OH, int OW, int pad_t, int pad_l) {
+  return H == 16 && W == 16 && OH == 8 && OW == 8 && pad_t >= 0 && pad_t <= 1 && pad_l >= 0 && pad_l <= 1 &&
+         ir_ws_supported(H, W, cs_in, kp, cs_mid);
+}
+
 bool ir_ws_supported(int H, int W, int cs_in, int kp, int cs_mid) {
   if (!((W == 8 && (kp == 128 || kp == 224)) || (W == 16 && kp == 128)) || H < 1 || H > 64 || cs_in != kp) return false;
   if (cs_mid % WS_SL != 0 || cs_mid < WS_SL) return false;
@@ -603,8 +620,11 @@ bool ir_ws_supported(int H, int W, int cs_in, int kp, int cs_mid) {
 
 void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_mid, const void* wpw, const float* bpw,
                   const float* wdw, const float* bdw, void* y, void* se_mean, double flops, double bytes,
-                  hipStream_t s, AsyncReport rep) {
-  M2S_CHECK(ir_ws_supported(H, W, cs_in, kp, cs_mid) && N > 0, "ir_ws: unsupported shape");
+                  hipStream_t s, AsyncReport rep, int stride, int OH, int OW, int pad_t, int pad_l) {
+  M2S_CHECK(stride == 1 ? ir_ws_supported(H, W, cs_in, kp, cs_mid)
+                        : stride == 2 && ir_ws_s2_supported(H, W, cs_in, kp, cs_mid, OH, OW, pad_t, pad_l),
+            "ir_ws: unsupported shape");
+  M2S_CHECK(N > 0, "ir_ws: no images");
   M2S_CHECK((double)N * H * W * cs_mid * 4.0 < 4294967296.0, "ir_ws: output map too large for 32-bit offsets");
   const WsLayout L = ws_layout(H, W, cs_in, cs_mid);
   const int n_cu = device_cus();
@@ -625,17 +645,19 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
   const bf16_t* wb = static_cast<const bf16_t*>(wpw);
   bf16_t* yb = static_cast<bf16_t*>(y);
   bf16_t* mb = static_cast<bf16_t*>(se_mean);
-#define M2S_IRWS(W_, KS_)                                                                               \
-  if (W == W_ && kp == KS_ * 32) {                                                                      \
-    allow_lds(reinterpret_cast<const void*>(&ir_ws_kernel<W_, KS_>));                                 \
-    ProfScope ps("ir_ws_kernel<" #W_ ", " #KS_ ">", flops, bytes, s);                                   \
-    hipLaunchKernelGGL((ir_ws_kernel<W_, KS_>), grid, dim3(64 * (WS_NP + WS_NC)), L.total, s, xb, N, H, cs_mid, wb, \
-                       bpw, wdw, bdw, yb, mb, tr, rep.spin_max, rep.err);                                \
-    M2S_IRWS_DUMP(#W_ "," #KS_)                                                                         \
+#define M2S_IRWS(W_, KS_, S_, NAME_)                                                                    \
+  if (W == W_ && kp == KS_ * 32 && stride == S_) {                                                      \
+    allow_lds(reinterpret_cast<const void*>(&ir_ws_kernel<W_, KS_, S_>));                             \
+    ProfScope ps(NAME_, flops, bytes, s);                                                               \
+    hipLaunchKernelGGL((ir_ws_kernel<W_, KS_, S_>), grid, dim3(64 * (WS_NP + WS_NC)), L.total, s, xb, N, H, cs_mid, wb, \
+                       bpw, wdw, bdw, yb, mb, tr, rep.spin_max, rep.err, pad_t, pad_l);                  \
+    M2S_IRWS_DUMP(NAME_)                                                                                \
     M2S_HIP(hipGetLastError());                                                                         \
     return;                                                                                             \
   }
-  M2S_IRWS(8, 4) M2S_IRWS(8, 7) M2S_IRWS(16, 4)
+  // (the stride-1 kernels keep their two-argument names in profiles and the launch log)
+  M2S_IRWS(8, 4, 1, "ir_ws_kernel<8, 4>") M2S_IRWS(8, 7, 1, "ir_ws_kernel<8, 7>") M2S_IRWS(16, 4, 1, "ir_ws_kernel<16, 4>")
+  M2S_IRWS(16, 4, 2, "ir_ws_kernel<16, 4, 2>")
 #undef M2S_IRWS
 #undef M2S_IRWS_DUMP
   M2S_CHECK(false, "ir_ws: no variant for this shape");

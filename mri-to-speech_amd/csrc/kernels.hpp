@@ -93,15 +93,18 @@ void launch_se_ws_f8(const void* x8, int M, int P, int cs_in, const void* w8, in
 
 // The same for a stride-2 depthwise (TF-SAME, top / left pads pad_t / pad_l) on an IH x IW <= 256-pixel
 // conv_pw map: y (N, OH*OW, cs_mid), se_mean over the OH x OW output.  (ir_fused.hip)
-// Split-fp32 stride-1 IR front half (conv_pw + bn1 + SiLU + conv_dw + bn2 + SiLU + SE squeeze) on
-// W = 8 / 16 maps as one persistent warp-specialised workgroup per CU; same outputs as
-// launch_ir_pwdw(split = true).  wdw: fp32 tap-major [9][cs_mid].  (ir_ws.hip)
+// Split-fp32 IR front half (conv_pw + bn1 + SiLU + conv_dw + bn2 + SiLU + SE squeeze) on W = 8 / 16 maps as
+// one persistent warp-specialised workgroup per CU; same outputs as launch_ir_pwdw(split = true) (stride 1) and
+// launch_ir_pwdw_s2(split = true) (stride 2: 16x16 -> 8x8, TF-SAME pads pad_t / pad_l; y is the OH x OW map).
+// wdw: fp32 tap-major [9][cs_mid].  (ir_ws.hip)
 bool ir_ws_supported(int H, int W, int cs_in, int kp, int cs_mid);
-// The producers' weight-slot wait is bounded by rep.spin_max polls; a timeout is reported through rep.err and
-// the images of that workgroup's slice get a NaN SE mean (their block output is NaN).
+bool ir_ws_s2_supported(int H, int W, int cs_in, int kp, int cs_mid, int OH, int OW, int pad_t, int pad_l);
+// The hand-off waits are bounded by rep.spin_max polls; a timeout is reported through rep.err and the images of
+// that workgroup get NaN SE means (their block output is NaN).
 void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_mid, const void* wpw, const float* bpw,
                   const float* wdw, const float* bdw, void* y, void* se_mean, double flops, double bytes,
-                  hipStream_t s, AsyncReport rep = {});
+                  hipStream_t s, AsyncReport rep = {}, int stride = 1, int OH = 0, int OW = 0, int pad_t = 0,
+                  int pad_l = 0);
 // Stride-2 IR front half on bands of 4 output rows (blocks.3.0: 32x32 -> 16x16), split fp32 or bf16: y =
 // the SE GEMM's operand (N, OH*OW, cs_mid; split: interleaved hi/lo), psum = squeeze partial sums
 // (N, OH / 4, cs_mid) for launch_se_mean.  wdw: fp32 tap-major [9][cs_mid].  (ir_s2band.hip)

@@ -82,6 +82,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   M2S_CHECK(n_mels > 0 && hidden > 0 && hidden % 8 == 0, "bad n_mels / rnn_hidden");
   if (const char* e = std::getenv("M2S_IR_FUSED")) ir_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_IR_WS")) ir_ws_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_IR_WS_S2")) ir_ws_s2_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_EXPAND")) f8_expand_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_ER")) f8_er_ = std::strcmp(e, "0") != 0;
@@ -781,6 +782,13 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                          nc * P * ((f8x ? 1.0 : es) * b.c1.cin + (f8 ? 1.0 : es) * b.mid), s, f8, f8x ? cur8 : nullptr,
                          f8x ? arena_.ptr(b.f8x_w) : nullptr, f8x ? static_cast<const float*>(arena_.ptr(b.f8x_s)) : nullptr,
                          b.f8x_kp);
+        } else if (SPL && b.stride == 2 && ir_fused_ && ir_ws_ && ir_ws_s2_ &&
+                   ir_ws_s2_supported(oh, ow, b.c1.cs_in, b.c1.kp, cs, nh, nw, qt, ql)) {
+          const double Pi = (double)oh * ow, Po = (double)nh * nw;
+          launch_ir_ws(cur, nc, oh, ow, b.c1.cs_in, b.c1.kp, cs, b.c1.w, b.c1.b, static_cast<const float*>(arena_.ptr(b.dw_w)),
+                       static_cast<const float*>(arena_.ptr(b.dw_b)), M2, se_mean, 2.0 * nc * b.mid * (Pi * b.c1.cin + Po * 9),
+                       4.0 * nc * (Pi * b.c1.cin + Po * b.mid) + 4.0 * b.mid * (b.c1.cin + 11.0), s, ws_report(), 2, nh, nw,
+                       qt, ql);
         } else if (FUSABLE && b.stride == 2 && ir_fused_ && ir_fused_s2_supported(oh, ow, b.c1.cs_in, cs, SPL) &&
                    nh * nw <= 64) {
           const double Pi = (double)oh * ow, Po = (double)nh * nw, es = SPL ? 4.0 : 2.0;

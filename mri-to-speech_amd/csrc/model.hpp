@@ -100,6 +100,7 @@ class Acoustic {
   int chunk = 1920;  // = m2s.config.CNN_CHUNK (the benched pass size)
   bool ir_fused_ = true;  // bf16: fused conv_pw + conv_dw + SE squeeze (env M2S_IR_FUSED=0 disables)
   bool ir_ws_ = true;     // split fp32: the persistent warp-specialised form of it (env M2S_IR_WS=0 disables)
+  bool ir_ws_s2_ = true;  // ... also for the stride-2 block at 16x16 (env M2S_IR_WS_S2=0: ir_pwdw_s2)
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
   bool f8_er_ = true;            // fp8: EdgeResidual blocks.1.1/.2 on e4m3 (env M2S_F8_ER=0: bf16 er_fused)
   bool se_y8_ = true;            // fp8: the SE GEMM also stores the next expand's e4m3 operand (env M2S_SE_Y8=0:

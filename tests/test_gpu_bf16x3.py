@@ -131,6 +131,28 @@ def test_ir_ws_matches_grid_kernel(rt, ac_state, monkeypatch, hw, n):
     assert _rel(ws.effnet(fr).cpu().numpy(), grid.effnet(fr).cpu().numpy()) <= 1e-4
 
 
+@pytest.mark.parametrize("n", [3, 300])
+def test_ir_ws_stride2_matches_grid_kernel_and_oracle(rt, ac_state, monkeypatch, n):
+    """blocks.5.0 (the stride-2 IR block at 16x16 -> 8x8) on the persistent ir_ws kernel (ir_ws_kernel<16, 4, 2>)
+    against the one-slice-per-workgroup ir_pwdw_s2 kernel it replaces (M2S_IR_WS_S2=0) and, at 3 frames, the fp32
+    oracle's tap; 300 frames = more images than workgroups.  Same split fp32 arithmetic up to the squeeze's
+    summation order: the 1e-4 parity bar."""
+    sd = {k: torch.from_numpy(v) for k, v in ac_state.items()}
+    fr = torch.from_numpy(synth.synth_frames(1, n, seed=23)[0])
+    ws = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    monkeypatch.setenv("M2S_IR_WS_S2", "0")
+    grid = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    x = fr.to(DEV)
+    for i in (19, 20):  # after blocks.5.0 (stride 2) and blocks.5.1 (its SE-gated output feeds it)
+        a, b = ws.probe(x, i).cpu().numpy(), grid.probe(x, i).cpu().numpy()
+        assert np.isfinite(a).all() and _rel(a, b) <= 1e-4, (i, _rel(a, b))
+    if n <= 3:
+        taps = []
+        effnet.effnet_features(sd, fr, taps=taps)
+        assert _rel(ws.probe(x, 19).cpu().numpy(), taps[19].numpy()) <= 1e-4
+    assert _rel(ws.effnet(x).cpu().numpy(), grid.effnet(x).cpu().numpy()) <= 1e-4
+
+
 @pytest.mark.parametrize("n", [3, 37])
 def test_ir_s2band_matches_unfused(rt, ac_state, monkeypatch, n):
     """blocks.3.0 as one banded kernel (ir_s2band.hip: conv_pw + stride-2 depthwise on 4-row bands, squeeze

@@ -13,7 +13,7 @@ sys.path.insert(0, sys.argv[1])
 from m2s import runtime as rt, synth, _native
 dev = torch.device("cuda", 0)
 x = torch.rand(1920, 256, 256, device=dev)
-eng = rt.AcousticEngine(synth.synth_acoustic_state(1), dtype="bf16x3", device=dev)
+eng = rt.AcousticEngine(synth.synth_acoustic_state(1), dtype=os.environ.get("AB_DTYPE", "bf16x3"), device=dev)
 for _ in range(3):
     eng.effnet(x)
 torch.cuda.synchronize()

@@ -9,7 +9,7 @@ for spec in "$@"; do
   B=mri-to-speech_amd/csrc/build_variant_$NAME
   rm -rf variants/$NAME $B && mkdir -p variants/$NAME/m2s $B
   cp mri-to-speech_amd/m2s/*.py variants/$NAME/m2s/
-  for o in mri-to-speech_amd/csrc/build/*.o; do [ "$(basename $o)" = ir_ws.hip.o ] || cp -p $o $B/; done
+  for o in mri-to-speech_amd/csrc/build/*.o; do [ "$(basename $o)" = "${SRC:-ir_ws.hip}.o" ] || cp -p $o $B/; done
   make -s -C mri-to-speech_amd/csrc -j8 OUT=$ROOT/variants/$NAME/m2s/libm2s.so TOUT=$ROOT/variants/$NAME/m2s/libm2s_torch.so \
     BUILD=build_variant_$NAME TLIBDIR=$ROOT/variants/$NAME/m2s EXTRA="$FL"
 done
