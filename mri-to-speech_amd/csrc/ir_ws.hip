@@ -109,6 +109,9 @@ __host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mi
 #ifndef IRWS_PF_DEEP
 #define IRWS_PF_DEEP 1
 #endif
+#ifndef IRWS_PAIR
+#define IRWS_PAIR 1  // 16x16: a consumer lane's two pixels vertically adjacent (shared tap rows)
+#endif
 #ifndef IRWS_TAPS_AHEAD
 #define IRWS_TAPS_AHEAD 1
 #endif
@@ -404,8 +407,9 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     TR(f, 4);
     const uint32_t pbase = (uint32_t)(d.img * PO + (r0 / S) * OWS);  // uniform
-    const uint32_t yoff0 = __builtin_amdgcn_readfirstlane(4u * (uint32_t)c0) + 8u * (uint32_t)cg +
-                           (pbase + (uint32_t)cpl) * (4u * (uint32_t)cs_mid);  // launch_ir_ws: < 2^32
+    const uint32_t yoffb = __builtin_amdgcn_readfirstlane(4u * (uint32_t)c0) + 8u * (uint32_t)cg +
+                           pbase * (4u * (uint32_t)cs_mid);  // launch_ir_ws: < 2^32
+    const uint32_t yoff0 = yoffb + (uint32_t)cpl * (4u * (uint32_t)cs_mid);
     // lane = (4-channel plane cg, pixels cpl + 64 k): the plane's 9 taps stay in registers
     const float* wd = wdl + (f % 3) * 320 + 4 * cg;
     float w[9][4], b[4];
@@ -442,8 +446,48 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       *reinterpret_cast<uint2*>(u) = hi;
       *reinterpret_cast<uint2*>(u + 64) = lo;
     };
+    // W = 16, full band: the lane's two pixels are vertically adjacent, (2 a, c) and (2 a + 1, c) for cpl =
+    // 16 a + c, so their windows share two tap rows: 12 tile reads for both instead of 18
+    auto pixel_pair = [&]() {
+      const int pa = cpl >> 4, pc = cpl & 15;
+      const char* tp = tpl + ((2 * pa) * WT + pc) * 16;
+      float a0[4] = {b[0], b[1], b[2], b[3]}, a1[4] = {b[0], b[1], b[2], b[3]};
+#pragma unroll
+      for (int ry = 0; ry < 4; ++ry) {
+#pragma unroll
+        for (int rx = 0; rx < 3; ++rx) {
+          const float4 u = *reinterpret_cast<const float4*>(tp + (ry * WT + rx) * 16);
+          if (ry < 3) {
+            const int t = ry * 3 + rx;
+            a0[0] += w[t][0] * u.x; a0[1] += w[t][1] * u.y; a0[2] += w[t][2] * u.z; a0[3] += w[t][3] * u.w;
+          }
+          if (ry > 0) {
+            const int t = (ry - 1) * 3 + rx;
+            a1[0] += w[t][0] * u.x; a1[1] += w[t][1] * u.y; a1[2] += w[t][2] * u.z; a1[3] += w[t][3] * u.w;
+          }
+        }
+        if (ry == 1) asm volatile("" ::: "memory");  // two rows of loads in flight (registers)
+      }
+      const uint32_t po = (uint32_t)(32 * pa + pc);  // band position of the upper pixel
+      auto out = [&](float* a, uint32_t pos) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = silu(a[j]);
+          s[j] += a[j];
+        }
+        uint2 hi, lo;
+        split4(a, hi, lo);
+        char* u = reinterpret_cast<char*>(y) + (yoffb + pos * (4u * (uint32_t)cs_mid));
+        *reinterpret_cast<uint2*>(u) = hi;
+        *reinterpret_cast<uint2*>(u + 64) = lo;
+      };
+      out(a0, po);
+      out(a1, po + 16u);
+    };
     if constexpr (S == 2) {
       if (cpl < OPB) pixel(0);  // (the bands of a 16-row map are full)
+    } else if (IRWS_PAIR && W == 16 && br == WS_BR) {
+      pixel_pair();
     } else if (br == WS_BR) {  // a full band: every lane's pixels exist, so their chains interleave
 #pragma unroll
       for (int k = 0; k < WS_PXL; ++k) pixel(k);
