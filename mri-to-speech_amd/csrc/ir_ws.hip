@@ -699,9 +699,9 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
     M2S_HIP(hipGetLastError());                                                                         \
     return;                                                                                             \
   }
-  // (the stride-1 kernels keep their two-argument names in profiles and the launch log)
-  M2S_IRWS(8, 4, 1, "ir_ws_kernel<8, 4>") M2S_IRWS(8, 7, 1, "ir_ws_kernel<8, 7>") M2S_IRWS(16, 4, 1, "ir_ws_kernel<16, 4>")
-  M2S_IRWS(16, 4, 2, "ir_ws_kernel<16, 4, 2>")
+  // (the launch log's names are rocprof's symbols, so the event and PMC records of a kernel share a key)
+  M2S_IRWS(8, 4, 1, "ir_ws_kernel<8, 4, 1>") M2S_IRWS(8, 7, 1, "ir_ws_kernel<8, 7, 1>")
+  M2S_IRWS(16, 4, 1, "ir_ws_kernel<16, 4, 1>") M2S_IRWS(16, 4, 2, "ir_ws_kernel<16, 4, 2>")
 #undef M2S_IRWS
 #undef M2S_IRWS_DUMP
   M2S_CHECK(false, "ir_ws: no variant for this shape");
