@@ -79,7 +79,9 @@ struct WsLayout {
 };
 
 __host__ __device__ inline int ws_cpp(int cs_in) { return (cs_in * 2 + 255) / 256 * 16; }  // chunks per plane
-__host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mid) {
+// S = 2: the tile planes lie TROWS = 5 (mod 16) 16-byte units apart (any odd residue: with the stride-2 consumers'
+// pixel order below, conflict-free reads; stride 1 keeps TROWS = 4 (mod 16))
+__host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mid, int S = 1) {
   WsLayout L;
   const int cpp = ws_cpp(cs_in), xp = 2 * cpp * 16;
   L.XR = 0;  // input rows a band needs (its rows and the in-image halo rows)
@@ -88,7 +90,7 @@ __host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mi
     L.XR = b - a > L.XR ? b - a : L.XR;
   }
   const int tr = ((H < WS_BR ? H : WS_BR) + 2) * (W + 2);
-  L.TROWS = tr + (20 - tr % 16) % 16;
+  L.TROWS = S == 1 ? tr + (20 - tr % 16) % 16 : tr + (21 - tr % 16) % 16;
   L.x_bytes = L.XR * W * xp;
   L.tile_bytes = 2 * 8 * L.TROWS * 16;
   L.w_bytes = 2 * (cs_in / 32) * 4096;
@@ -135,7 +137,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   constexpr int WT = W + 2;     // tile row (with the zero halo columns)
   constexpr int WS_PXL = WS_BR * W / 64;  // output pixels per consumer lane per slice
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const WsLayout Lg = ws_layout(H, W, CS, cs_mid);
+  const WsLayout Lg = ws_layout(H, W, CS, cs_mid, S);
   const int NB = (H + WS_BR - 1) / WS_BR, NS = cs_mid / WS_SL, P = H * W;
   const int PO = S == 1 ? P : ((H + 1) / 2) * OWS;  // output pixels of an image (TF-SAME)
   const int PLT = Lg.TROWS * 16;
@@ -398,10 +400,19 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   // (il_st4: position p, channel c -> element p * 2 cs + 2 (c & ~31) + (c & 31)) 64 positions apart.
   // The byte offset of a store is one 24-bit multiply-add on the band's scalar position base; the
   // per-pixel 64-bit position arithmetic (two v_mul_lo_u32 a pixel) was a fifth of the consumer VALU.
-  // (S = 2: output pixel cpl = (row oy, col ox) of the band's 4 rows; its window's top-left tile row and column
-  // are 2 oy - pad_t + 1 and 2 ox - pad_l + 1 (tile row = input row - r0 + 1, column = input column + 1))
-  const int toff0 = S == 1 ? ((cpl / W) * WT + cpl % W) * 16
-                           : ((2 * (cpl / OWS) - pad_t + 1) * WT + 2 * (cpl % OWS) - pad_l + 1) * 16;
+  // S = 2: pixel lane cpl = 4 k + i takes output pixel (oy, ox) of the band's 4 x 8, row 2 (k & 1) + (i & 1), column
+  // (c_(i & 1) + 4 (i >> 1)) & 7 with c_0 = (k >> 1) + 4 (k & 1), c_1 = c_0 + 6: the four pixel lanes of a
+  // ds_read_b128 lane group then sit at 16-byte offsets (c, c, c + 8, c + 8) mod 16, which with the planes an odd
+  // number (mod 16) of units apart fill all 16 bank quads in both lane-group patterns (stride-2 columns in pixel order were 2-way conflicted: 0.36 conflict
+  // cycles per LDS instruction, profiles/r05fin2_sq_mfma.txt).  Its window's top-left tile row and column are
+  // 2 oy - pad_t + 1 and 2 ox - pad_l + 1 (tile row = input row - r0 + 1, column = input column + 1).
+  int cpo = cpl, toff0 = ((cpl / W) * WT + cpl % W) * 16;
+  if constexpr (S == 2) {
+    const int k = cpl >> 2, i = cpl & 3, c0 = (k >> 1) + 4 * (k & 1);
+    const int oy = 2 * (k & 1) + (i & 1), ox = (((i & 1) ? c0 + 6 : c0) + 4 * (i >> 1)) & 7;
+    cpo = oy * OWS + ox;
+    toff0 = ((2 * oy - pad_t + 1) * WT + 2 * ox - pad_l + 1) * 16;
+  }
   auto consume = [&](int f, Step d) {
     const int c0 = d.sl * WS_SL, r0 = d.band * WS_BR, br = min(WS_BR, H - r0);
     float s[4] = {0.f, 0.f, 0.f, 0.f};
@@ -409,7 +420,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     const uint32_t pbase = (uint32_t)(d.img * PO + (r0 / S) * OWS);  // uniform
     const uint32_t yoffb = __builtin_amdgcn_readfirstlane(4u * (uint32_t)c0) + 8u * (uint32_t)cg +
                            pbase * (4u * (uint32_t)cs_mid);  // launch_ir_ws: < 2^32
-    const uint32_t yoff0 = yoffb + (uint32_t)cpl * (4u * (uint32_t)cs_mid);
+    const uint32_t yoff0 = yoffb + (uint32_t)cpo * (4u * (uint32_t)cs_mid);
     // lane = (4-channel plane cg, pixels cpl + 64 k): the plane's 9 taps stay in registers
     const float* wd = wdl + (f % 3) * 320 + 4 * cg;
     float w[9][4], b[4];
@@ -650,7 +661,7 @@ static void dump_trace(unsigned long long* tr, hipStream_t s, const char* tag) {
 
 bool ir_ws_s2_supported(int H, int W, int cs_in, int kp, int cs_mid, int OH, int OW, int pad_t, int pad_l) {
   return H == 16 && W == 16 && OH == 8 && OW == 8 && pad_t >= 0 && pad_t <= 1 && pad_l >= 0 && pad_l <= 1 &&
-         ir_ws_supported(H, W, cs_in, kp, cs_mid);
+         ir_ws_supported(H, W, cs_in, kp, cs_mid) && ws_layout(H, W, cs_in, cs_mid, 2).total <= 160 * 1024;
 }
 
 bool ir_ws_supported(int H, int W, int cs_in, int kp, int cs_mid) {
@@ -670,7 +681,7 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
             "ir_ws: unsupported shape");
   M2S_CHECK(N > 0, "ir_ws: no images");
   M2S_CHECK((double)N * H * W * cs_mid * 4.0 < 4294967296.0, "ir_ws: output map too large for 32-bit offsets");
-  const WsLayout L = ws_layout(H, W, cs_in, cs_mid);
+  const WsLayout L = ws_layout(H, W, cs_in, cs_mid, stride);
   const int n_cu = device_cus();
   const dim3 grid(std::min(N, n_cu));
 #ifdef IRWS_TRACE

@@ -249,10 +249,19 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
               hi.y = pack_bf16x2(v[2], v[3]);
             }
           }
-          // channels ni * 16 + 4 g .. : plane 2 ni + g / 2, the (g & 1) half of its 16 bytes
-          char* d = sS + (2 * ni + (g >> 1)) * SPLANE + px * 16 + (g & 1) * 8;
-          *reinterpret_cast<uint2*>(d) = hi;
-          if constexpr (SP) *reinterpret_cast<uint2*>(d + SLO) = lo;
+          // channels ni * 16 + 4 g .. : plane 2 ni + g / 2, the (g & 1) half of its 16 bytes.  The odd lane rows
+          // hand their halves to the even rows (v_permlane16_swap), which store whole 16-byte chunks: 8-byte
+          // stores of the halves were 2-way bank-conflicted (16 lanes 16 bytes apart; 0.36 conflict cycles per
+          // LDS instruction over the kernel, profiles/r05fin2_sq_mfma.txt)
+          auto up = [](uint32_t v) { return __builtin_amdgcn_permlane16_swap(v, v, false, false)[1]; };
+          const uint4 hq = make_uint4(hi.x, hi.y, up(hi.x), up(hi.y));
+          uint4 lq = make_uint4(0u, 0u, 0u, 0u);
+          if constexpr (SP) lq = make_uint4(lo.x, lo.y, up(lo.x), up(lo.y));
+          if ((g & 1) == 0) {
+            char* d = sS + (2 * ni + (g >> 1)) * SPLANE + px * 16;
+            *reinterpret_cast<uint4*>(d) = hq;
+            if constexpr (SP) *reinterpret_cast<uint4*>(d + SLO) = lq;
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
       }

@@ -143,6 +143,16 @@ def test_ir_ws_stride2_matches_grid_kernel_and_oracle(rt, ac_state, monkeypatch,
     monkeypatch.setenv("M2S_IR_WS_S2", "0")
     grid = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
     x = fr.to(DEV)
+    from m2s import _native
+    names = {}
+    for key, eng in (("ws", ws), ("grid", grid)):  # the kernel each engine runs for blocks.5.0
+        _native.prof_enable(True)
+        eng.probe(x, 19)
+        torch.cuda.synchronize()
+        names[key] = {r["name"] for r in _native.prof_launches()}
+        _native.prof_enable(False)
+    assert "ir_ws_kernel<16, 4, 2>" in names["ws"] and "ir_pwdw_s2_kernel<1>" not in names["ws"], names["ws"]
+    assert "ir_pwdw_s2_kernel<1>" in names["grid"], names["grid"]
     for i in (19, 20):  # after blocks.5.0 (stride 2) and blocks.5.1 (its SE-gated output feeds it)
         a, b = ws.probe(x, i).cpu().numpy(), grid.probe(x, i).cpu().numpy()
         assert np.isfinite(a).all() and _rel(a, b) <= 1e-4, (i, _rel(a, b))
