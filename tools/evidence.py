@@ -56,19 +56,20 @@ def dispatch_stages(d):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 names[int(r["Dispatch_Id"])] = r["Kernel_Name"]
-    disp = sorted(names)
-    out, j, matched = {}, 0, 0
-    i = 0
-    while i < len(disp) and j < len(launches):
+    # the trace also holds the dispatches before the log was switched on (weight packing, the engines' set-up, which
+    # can run the same kernels), and the logged steps are the process's last work: walk both sequences from the end
+    disp = sorted(names, reverse=True)
+    out, j, matched, i = {}, len(launches) - 1, 0, 0
+    while i < len(disp) and j >= 0:
         want = _base(launches[j][0])
-        # the next dispatch of this kernel within a short window (a launch may be preceded by fills / copies)
+        # the previous dispatch of this kernel within a short window (fills / copies may sit between launches)
         hit = next((q for q in range(i, min(i + 8, len(disp))) if _base(names[disp[q]]) == want), None)
         if hit is None:  # this launch was not traced as named: skip it
-            j += 1
+            j -= 1
             continue
         out[disp[hit]] = launches[j][1]
         matched += 1
-        i, j = hit + 1, j + 1
+        i, j = hit + 1, j - 1
     return out, rec["steps"], matched, len(launches)
 
 
