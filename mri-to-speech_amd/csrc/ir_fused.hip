@@ -45,6 +45,10 @@ constexpr int ROWS_MAX_SP = 400;  // SP: fp32 rows (1 x 18x18, 4 x 10x10)
 constexpr int POS_MAX = 256;   // positions per workgroup
 // One slice per workgroup: a slice loop per workgroup (more reuse of the input) measured slower,
 // occupancy 4 -> 2.
+#ifndef IRPW_CG8
+#define IRPW_CG8 1  // bf16 / fp8 depthwise on 8 groups of 4 channels (0: 4 groups of 8)
+#endif
+
 
 __device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float acc) {
   return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x), __builtin_bit_cast(bf16x2_t, w), acc,
@@ -118,8 +122,13 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
 
   const bf16_t* xi = x + (size_t)n0 * P * cs_in * R;
   const int mw = wave * MT * 16;
-  const int cg = tid % CG, pl = tid / CG;
-  const int lpi = PL / G, g = pl / lpi, q = pl - g * lpi;  // phase-2 image and lane within it
+  // phase 2: CGX channel groups of NCH channels x PLX pixel lanes.  bf16 tiles (SP = 0): 8 groups of 4 channels
+  // (IRPW_CG8=0: 4 x 8), half the taps per lane in registers (36 dwords) and twice the pixel lanes: same-box A/B
+  // (gpurun_out/r05ai) fp8 16x16 385 -> 361 us, bf16 16x16 478 -> 474 us, 8x8 within +-2 %; asking the compiler
+  // for five workgroups per CU instead of four (96 VGPRs, spills) was no faster for fp8 and 6 % slower for bf16
+  constexpr int CGX = (!SP && IRPW_CG8) ? 8 : CG, NCH = SL / CGX, PLX = 256 / CGX;
+  const int cg = tid % CGX, pl = tid / CGX;
+  const int lpi = PLX / G, g = pl / lpi, q = pl - g * lpi;  // phase-2 image and lane within it
   int off[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) off[t] = ((t / 3 - 1) * WR + (t % 3 - 1)) * (SP ? MROWF : MROW);
@@ -273,8 +282,10 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
     __syncthreads();
 
     // ---- phase 2: depthwise 3x3 (stride 1, pad 1) from the haloed tile ------------------------
-    const int c = c0 + cg * 8;
-    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int c = c0 + cg * NCH;
+    float s[NCH];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) s[j] = 0.f;
     if (SP && g < gi && c < cs_mid) {
       float w[9][8], b[8];
 #pragma unroll
@@ -322,18 +333,20 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
         il_st8(ys, (long)(n0 + g) * PO + p, cs_mid, c, a);  // the SE GEMM's interleaved operand
       }
     } else if (!SP && g < gi && c < cs_mid) {
-      uint32_t w[9][8];
-      float b[8];
+      constexpr int NW2 = NCH / 2;  // tap dwords per lane and tap: (w_c, 0) / (0, w_c+1) pairs
+      uint32_t w[9][NCH];
+      float b[NCH];
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const uint4 lo = wdw_lds[t][2 * cg], hi = wdw_lds[t][2 * cg + 1];
-        w[t][0] = lo.x; w[t][1] = lo.y; w[t][2] = lo.z; w[t][3] = lo.w;
-        w[t][4] = hi.x; w[t][5] = hi.y; w[t][6] = hi.z; w[t][7] = hi.w;
-      }
-      {
-        const float4 lo = bdw_lds[2 * cg], hi = bdw_lds[2 * cg + 1];
-        b[0] = lo.x; b[1] = lo.y; b[2] = lo.z; b[3] = lo.w;
-        b[4] = hi.x; b[5] = hi.y; b[6] = hi.z; b[7] = hi.w;
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int k = 0; k < NCH / 4; ++k) {
+          const uint4 v = wdw_lds[t][(NCH / 4) * cg + k];
+          w[t][4 * k] = v.x; w[t][4 * k + 1] = v.y; w[t][4 * k + 2] = v.z; w[t][4 * k + 3] = v.w;
+        }
+#pragma unroll
+      for (int k = 0; k < NCH / 4; ++k) {
+        const float4 v = bdw_lds[(NCH / 4) * cg + k];
+        b[4 * k] = v.x; b[4 * k + 1] = v.y; b[4 * k + 2] = v.z; b[4 * k + 3] = v.w;
       }
       bf16_t* yi = y + (size_t)(n0 + g) * PO * cs_mid + c;
       for (int p = q; p < PO; p += lpi) {
@@ -344,49 +357,60 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
           const int oy = p / SOW, ox = p - (p / SOW) * SOW;
           trow = g * IR + (S * oy - pad_t + 2) * WR + S * ox - pad_l + 2;
         }
-        const bf16_t* base = tile + trow * MROW + cg * 8;
-        uint4 in[9];
-#pragma unroll
-        for (int t = 0; t < 9; ++t) in[t] = *reinterpret_cast<const uint4*>(base + off[t]);
-        float a[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = b[j];
+        const bf16_t* base = tile + trow * MROW + cg * NCH;
+        uint32_t in[9][NW2];
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
-          const uint32_t u[4] = {in[t].x, in[t].y, in[t].z, in[t].w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            a[2 * j] = dot2(u[j], w[t][2 * j], a[2 * j]);
-            a[2 * j + 1] = dot2(u[j], w[t][2 * j + 1], a[2 * j + 1]);
+          if constexpr (NW2 == 4) {
+            const uint4 v = *reinterpret_cast<const uint4*>(base + off[t]);
+            in[t][0] = v.x; in[t][NW2 > 1 ? 1 : 0] = v.y; in[t][NW2 > 2 ? 2 : 0] = v.z; in[t][NW2 > 3 ? 3 : 0] = v.w;
+          } else {
+            const uint2 v = *reinterpret_cast<const uint2*>(base + off[t]);
+            in[t][0] = v.x; in[t][NW2 > 1 ? 1 : 0] = v.y;
           }
         }
-        uint4 o;
-        uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
-        float v[8];
+        float a[NCH];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < NCH; ++j) a[j] = b[j];
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int j = 0; j < NW2; ++j) {
+            a[2 * j] = dot2(in[t][j], w[t][2 * j], a[2 * j]);
+            a[2 * j + 1] = dot2(in[t][j], w[t][2 * j + 1], a[2 * j + 1]);
+          }
+        float v[NCH];
+        uint32_t ow[NW2];
+#pragma unroll
+        for (int j = 0; j < NW2; ++j) {
           v[2 * j] = silu(a[2 * j]);
           v[2 * j + 1] = silu(a[2 * j + 1]);
           s[2 * j] += v[2 * j];  // the squeeze sums the unrounded values
           s[2 * j + 1] += v[2 * j + 1];
           ow[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
         }
-        if constexpr (F8) {  // 8 channels -> 8 bytes at byte (n, p, c) of the e4m3 map
-          reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(y) + ((size_t)(n0 + g) * PO + p) * cs_mid + c)[0] = e4m3x8(v);
+        uint8_t* y8 = reinterpret_cast<uint8_t*>(y) + ((size_t)(n0 + g) * PO + p) * cs_mid + c;
+        if constexpr (F8 && NCH == 8) {  // 8 channels -> 8 bytes at byte (n, p, c) of the e4m3 map
+          reinterpret_cast<uint2*>(y8)[0] = e4m3x8(v);
+        } else if constexpr (F8) {  // 4 channels -> 4 bytes (the first half of e4m3x8: the same bytes)
+          const int r = __builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v[0]), sat_e4m3(v[1]), 0, false);
+          reinterpret_cast<uint32_t*>(y8)[0] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v[2]), sat_e4m3(v[3]), r, true);
+        } else if constexpr (NCH == 8) {
+          *reinterpret_cast<uint4*>(yi + (size_t)p * cs_mid) = make_uint4(ow[0], ow[NW2 > 1 ? 1 : 0], ow[NW2 > 2 ? 2 : 0], ow[NW2 > 3 ? 3 : 0]);
         } else {
-          *reinterpret_cast<uint4*>(yi + (size_t)p * cs_mid) = o;
+          *reinterpret_cast<uint2*>(yi + (size_t)p * cs_mid) = make_uint2(ow[0], ow[NW2 > 1 ? 1 : 0]);
         }
       }
     }
-    // ---- squeeze: the wave's 16 pixel lanes (lane / CG) share cg = lane % CG; one image per wave
+    // ---- squeeze: the wave's pixel lanes (lane / CGX) share cg = lane % CGX; one image per wave
     // when G = 4, else the image spans 4/G waves.
 #pragma unroll
-    for (int msk = CG; msk < 64; msk <<= 1)
+    for (int msk = CGX; msk < 64; msk <<= 1)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s[j] += __shfl_xor(s[j], msk);
-    if (lane < CG)
+      for (int j = 0; j < NCH; ++j) s[j] += __shfl_xor(s[j], msk);
+    if (lane < CGX)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = s[j];
+      for (int j = 0; j < NCH; ++j) red[wave][lane * NCH + j] = s[j];
     __syncthreads();
     if (tid < G * SL) {
       const int gg = tid / SL, cl = tid - gg * SL, wpi = 4 / G;
