@@ -29,6 +29,7 @@
 // per workgroup at two per CU.  Tiles are dealt per XCD in contiguous ranges, so the workgroups of
 // one XCD work on neighbouring tiles of the same frames at any time (shared halos stay in its L2).
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -39,6 +40,9 @@
 namespace m2s {
 namespace {
 
+#ifndef STEM_P2_DB
+#define STEM_P2_DB 0  // phase 2's B fragments double-buffered across taps (spills at 256 VGPRs: off)
+#endif
 constexpr int SB_TW = 16;           // output tile width (one MFMA position subtile per tile row)
 constexpr int SB_SW = SB_TW + 4;    // S row width
 constexpr int SB_AV = SB_TW + 2;    // A row width (valid pixels)
@@ -286,17 +290,58 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
       f32x4 acc[AMS];
 #pragma unroll
       for (int i = 0; i < AMS; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // the wave's subtiles (a uniform count: 5 or 6 with the 23-subtile A map) as a straight-line body: every
+      // B fragment of a tap read at once and the next tap's issued before this tap's MFMAs (the per-subtile
+      // guarded form waited out a full LDS round trip for each of its 54 (tap, subtile) pairs: ~8.5 k cycles)
+      const int nsub = (ASUB - sub0 - wave + 3) / 4;
+      auto body = [&](auto nic) {
+        constexpr int NI = decltype(nic)::value;
+        constexpr int NB = STEM_P2_DB ? 2 : 1;  // tap buffers: 2 = the next tap's reads ahead of this tap's MFMAs
+        bf16x8 bh[NB][NI], bl[NB][SP ? NI : 1];
+        auto ld = [&](int k, int buf) {
+          const int toff = ((k / 3) * SB_SW + (k % 3)) * 16;
 #pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const int toff = ((k / 3) * SB_SW + (k % 3)) * 16;
+          for (int i = 0; i < NI; ++i) {
+            bh[buf][i] = frag(sS + sbase[i] + toff);
+            if constexpr (SP) bl[buf][i] = frag(sS + SLO + sbase[i] + toff);
+          }
+        };
+        if (NB == 2) ld(0, 0);
 #pragma unroll
-        for (int i = 0; i < AMS; ++i) {
-          if (sub0 + wave + 4 * i < ASUB) {
-            const bf16x8 b = frag(sS + sbase[i] + toff);
+        for (int k = 0; k < 9; ++k) {
+          const int cb = NB == 2 ? (k & 1) : 0;
+          if (NB == 1) ld(k, 0);
+          else if (k + 1 < 9) ld(k + 1, (k + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < NI; ++i) {
             if constexpr (SP)
-              acc[i] = mma3(wf0[k], wl0[k], b, frag(sS + SLO + sbase[i] + toff), acc[i]);
+              acc[i] = mma3(wf0[k], wl0[k], bh[cb][i], bl[cb][i], acc[i]);
             else
-              acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[k], b, acc[i], 0, 0, 0);
+              acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[k], bh[cb][i], acc[i], 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      static_assert(AMS == 6, "the straight-line bodies cover 5 and 6 subtiles");
+      // (split only: the bf16 kernel's three workgroups per CU leave 168 VGPRs, and the bodies spilled there)
+      if (SP && nsub == 6) {
+        body(std::integral_constant<int, 6>());
+      } else if (SP && nsub == 5) {
+        body(std::integral_constant<int, 5>());
+      } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const int toff = ((k / 3) * SB_SW + (k % 3)) * 16;
+#pragma unroll
+          for (int i = 0; i < AMS; ++i) {
+            if (sub0 + wave + 4 * i < ASUB) {
+              const bf16x8 b = frag(sS + sbase[i] + toff);
+              if constexpr (SP)
+                acc[i] = mma3(wf0[k], wl0[k], b, frag(sS + SLO + sbase[i] + toff), acc[i]);
+              else
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0[k], b, acc[i], 0, 0, 0);
+            }
           }
         }
       }
