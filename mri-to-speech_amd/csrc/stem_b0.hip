@@ -166,20 +166,23 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
     wf1[k] = *reinterpret_cast<const bf16x8*>(w);
     if constexpr (SP) wl1[k] = *reinterpret_cast<const bf16x8*>(w + a.kp1);
   }
-  // the stem's weights in LDS as the lanes' A-fragment values: [channel tile][lane (g, r16)] 4 floats = taps
-  // (ky = g, kx = 0..2) of channel ni * 16 + r16 and 0 (g = 3: zeros), and the biases; a subtile reads its
-  // two fragments (split there) and biases instead of keeping them in registers, which phase 2's resident
-  // weights leave none of
-  __shared__ __attribute__((aligned(16))) float sw9[2 * 64 * 4 + 32];
-  for (int i = tid; i < 2 * 64 * 4 + 32; i += 256) {
-    float v = 0.f;
-    if (i < 512) {
-      const int ni = i >> 8, ln = (i >> 2) & 63, kx = i & 3, gg = ln >> 4;
-      if (gg < 3 && kx < 3) v = a.w9[(ni * 16 + (ln & 15)) * 9 + 3 * gg + kx];
+  // the stem's weights in LDS as the lanes' A-fragments, split once here: [channel tile][lane (g, r16)] the
+  // bf16 hi and lo halves of the taps (ky = g, kx = 0..2) of channel ni * 16 + r16 and 0 (g = 3: zeros) in one
+  // 16-byte entry, then the fp32 biases; a subtile reads its two fragments and biases instead of keeping them
+  // in registers, which phase 2's resident weights leave none of
+  __shared__ __attribute__((aligned(16))) uint32_t sw9[2 * 64 * 4 + 32];
+  for (int i = tid; i < 2 * 64 + 32; i += 256) {
+    if (i < 128) {
+      const int ni = i >> 6, ln = i & 63, gg = ln >> 4;
+      float wv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (gg < 3)
+        for (int kx = 0; kx < 3; ++kx) wv[kx] = a.w9[(ni * 16 + (ln & 15)) * 9 + 3 * gg + kx];
+      uint2 wh, wl;
+      split4(wv, wh, wl);
+      *reinterpret_cast<uint4*>(&sw9[i * 4]) = make_uint4(wh.x, wh.y, wl.x, wl.y);
     } else {
-      v = a.b9[i - 512];
+      sw9[512 + i - 128] = __float_as_uint(a.b9[i - 128]);
     }
-    sw9[i] = v;
   }
   const float4 bb0 = *reinterpret_cast<const float4*>(a.b0 + 4 * g);
   const float4 bb1 = *reinterpret_cast<const float4*>(a.b1 + 4 * g);
@@ -235,13 +238,10 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
         const bool ok = oy >= 0 && oy < a.OH && ox >= 0 && ox < a.OW;
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni) {
-          const float4 w4 = *reinterpret_cast<const float4*>(&sw9[(ni * 64 + ln) * 4]);
+          const uint4 w4 = *reinterpret_cast<const uint4*>(&sw9[(ni * 64 + ln) * 4]);
           const float4 b4 = *reinterpret_cast<const float4*>(&sw9[512 + ni * 16 + 4 * (ln >> 4)]);
-          const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-          uint2 wh, wl;
-          split4(wv, wh, wl);
-          const bf16x8 wsh = __builtin_bit_cast(bf16x8, make_uint4(wh.x, wh.y, 0u, 0u));
-          const bf16x8 wsl = __builtin_bit_cast(bf16x8, make_uint4(wl.x, wl.y, 0u, 0u));
+          const bf16x8 wsh = __builtin_bit_cast(bf16x8, make_uint4(w4.x, w4.y, 0u, 0u));
+          const bf16x8 wsl = __builtin_bit_cast(bf16x8, make_uint4(w4.z, w4.w, 0u, 0u));
           const f32x4 acc = mma3(wsh, wsl, bh, bl, f32x4{b4.x, b4.y, b4.z, b4.w});
           const float v[4] = {silu(acc[0]), silu(acc[1]), silu(acc[2]), silu(acc[3])};
           uint2 hi = make_uint2(0u, 0u), lo = make_uint2(0u, 0u);
