@@ -117,6 +117,13 @@ __host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mi
 #ifndef IRWS_TAPS_AHEAD
 #define IRWS_TAPS_AHEAD 1
 #endif
+// JOINT (hand-off right after the MFMAs): the wait for every producer's slice-f MFMAs and the wait for the consumers'
+// release of the tile buffer poll both counters in one LDS round trip (W(f + 2) is issued as soon as the first is met).
+// 1 = the stride-2 kernel only, 2 = every shape.  Same-box A/B (gpurun_out/ab_joint.txt, us per launch): <16,4,2>
+// 656-665 -> 632-637, <16,4,1> 642-645 -> 670-673
+#ifndef IRWS_JOINT
+#define IRWS_JOINT 1
+#endif
 // S = depthwise stride.  S = 2 (blocks.5.0, 16x16 -> 8x8, TF-SAME pads pad_t / pad_l): the producers expand the
 // same input bands; a band's output rows are its 4 stride-2 rows, one pixel a consumer lane (lanes of consumer
 // waves 0-3; waves 4-7 only take part in the hand-offs and the squeeze count).
@@ -130,6 +137,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   constexpr int OWS = W / S;                      // output row width
   constexpr int OPB = (WS_BR / S) * OWS;          // output pixels of a full band
   constexpr bool HAND_END = IRWS_HAND_END == 2 ? W == 8 : IRWS_HAND_END, TAPS_AHEAD = IRWS_TAPS_AHEAD;
+  constexpr bool JOINT = IRWS_JOINT && !HAND_END && (IRWS_JOINT == 2 || S == 2);
   constexpr int CS = KS * 32;  // input channel stride = expand K
   constexpr int CPP = (CS * 2 + 255) / 256 * 16;
   constexpr int CPR = 2 * CPP;  // 16-byte chunks per LDS x row
@@ -291,14 +299,43 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   // the hand-off latency, ~800 cycles a slice, on every producer's critical path; in-kernel stamps r05k.)
   const bool tap_wave = wave >= WS_NP - 2;  // issue_wd's two waves
   const int npw = (wave < 4 * KS ? (4 * KS - 1 - wave) / WS_NP + 1 : 0) + (wave == 0 ? 1 : 0);  // W pieces a slice
+  // (JOINT) every producer done with slice f's MFMAs -> W(f + 2) issued; every consumer done with slice f - 2 -> return.
+  // One lane polls pdone and lanes 0..WS_NC-1 the consumer words, one ds_read pair and one lgkmcnt wait a poll
+  auto wait_pd_tf = [&](int f, Step d2) {
+    const unsigned pd_t = f + 1 < T ? (unsigned)(WS_NP * (f + 1)) : 0u, tf_t = f >= 2 ? (unsigned)(f - 1) : 0u;
+    bool wdone = !(f + 2 < T);
+    const uint32_t ap = (uint32_t)(uintptr_t)pdone, at = (uint32_t)(uintptr_t)(tfree + (lane < WS_NC ? lane : 0));
+    for (unsigned n = 0; n < spin_max; ++n) {
+      unsigned vp, vt;
+      asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)" : "=&v"(vp), "=&v"(vt) : "v"(ap), "v"(at) : "memory");
+      const bool pok = __builtin_amdgcn_readfirstlane(vp) >= pd_t;
+      const bool tok = __builtin_amdgcn_ballot_w64(lane < WS_NC && vt < tf_t) == 0;
+      if (pok && !wdone) {
+        TR(f, 14);
+        issue_w(f + 2, d2);
+        wdone = true;
+      }
+      if (pok && tok) return;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    report_async(err, M2S_ASYNC_WS, lane);
+    if (lane == 0) asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)poison), "v"(1u) : "memory");
+    if (!wdone) issue_w(f + 2, d2);
+  };
   auto after_mfma = [&](int f, Step d2) {
     if (HAND_END) {
       bump(pdone);
     } else {  // W(f + 1) of this wave landed (younger: only the tap waves' slice-f taps), then every producer's
       if (tap_wave) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
       else wait_vm0();
+      TR(f, 13);
       bump(pdone);
+      if (JOINT) {
+        wait_pd_tf(f, d2);
+        return;
+      }
       if (f + 1 < T) wait_ge(pdone, (unsigned)(WS_NP * (f + 1)));
+      TR(f, 14);
       if (f + 2 < T) issue_w(f + 2, d2);
     }
   };
@@ -363,7 +400,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       TR(f, 6);
       after_mfma(f, d2);
       TR(f, 8);
-      if (f >= 2) wait_all(tfree, (unsigned)(f - 1));  // every consumer is done with tile f - 2 (same buffer)
+      if (!JOINT && f >= 2) wait_all(tfree, (unsigned)(f - 1));  // every consumer is done with tile f - 2 (same buffer)
       TR(f, 9);
       // bias + SiLU -> tile[f % 2]; lane holds channels 4g..4g+3 (of 16-channel tile nt) of position r16
 #pragma unroll
@@ -382,7 +419,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     else if (nu == 1) units(std::integral_constant<int, 1>());
     else {
       after_mfma(f, d2);
-      if (f >= 2) wait_all(tfree, (unsigned)(f - 1));
+      if (!JOINT && f >= 2) wait_all(tfree, (unsigned)(f - 1));
     }
     // halo rows outside the image (above the first band, below the last) hold zeros
     if (tid < 8 * W) {
@@ -649,6 +686,20 @@ static void dump_trace(unsigned long long* tr, hipStream_t s, const char* tag) {
     for (int w = 0; w < 8; ++w) {
       fprintf(stderr, " w%d", w);
       for (int k : {0, 2, 6, 9, 12, 3}) fprintf(stderr, "%c%lld", k ? '/' : ' ', at(i, 0, k, w) - at(i, 0, 0));
+    }
+    fprintf(stderr, "]");
+  }
+  fprintf(stderr, "\n");
+  // consumer waves' px start / tfree bump / end of slices i - 2 .. i, relative to producer wave 0's slice i start
+  fprintf(stderr, "TRACEC %s:", tag);
+  for (int i = 4; i < 7; ++i) {
+    fprintf(stderr, " [s%d P0 mfma_end %lld vm0 %lld pdone %lld after %lld tf %lld tfull %lld |", i, at(i, 0, 6) - at(i, 0, 0),
+            at(i, 0, 13) - at(i, 0, 0), at(i, 0, 14) - at(i, 0, 0), at(i, 0, 8) - at(i, 0, 0), at(i, 0, 9) - at(i, 0, 0),
+            at(i, 0, 12) - at(i, 0, 0));
+    for (int j = i - 2; j <= i; ++j) {
+      fprintf(stderr, " c%d:", j);
+      for (int w = 0; w < 8; ++w)
+        fprintf(stderr, " %lld/%lld/%lld", at(j, 1, 4, w) - at(i, 0, 0), at(j, 1, 10, w) - at(i, 0, 0), at(j, 1, 7, w) - at(i, 0, 0));
     }
     fprintf(stderr, "]");
   }
