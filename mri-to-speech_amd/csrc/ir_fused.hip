@@ -39,7 +39,6 @@ constexpr int MROW = SL + 8;   // bf16 LDS row stride in bf16 (80 B)
 constexpr int MROWF = SL + 4;  // fp32 (SP) LDS row stride in floats (144 B)
 constexpr int NT = SL / 16;    // 16-channel MFMA subtiles
 constexpr int CG = SL / 8;     // phase-2 channel groups (8 channels = one 16-byte vector)
-constexpr int PL = 256 / CG;   // phase-2 pixel lanes (64; 16 per wave)
 constexpr int ROWS_MAX = 400;  // haloed pixel rows per workgroup (4 x 10x10, 1 x 18x18)
 constexpr int ROWS_MAX_SP = 400;  // SP: fp32 rows (1 x 18x18, 4 x 10x10)
 constexpr int POS_MAX = 256;   // positions per workgroup
@@ -48,11 +47,27 @@ constexpr int POS_MAX = 256;   // positions per workgroup
 #ifndef IRPW_CG8
 #define IRPW_CG8 1  // bf16 / fp8 depthwise on 8 groups of 4 channels (0: 4 groups of 8)
 #endif
+#ifndef IRPW_F16
+#define IRPW_F16 1  // e4m3-output modes: f16 tile + v_pk_fma_f16 depthwise, packed-f32 SiLU (0: the bf16 dot2 form)
+#endif
 
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float dot2(uint32_t x, uint32_t w, float acc) {
   return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x), __builtin_bit_cast(bf16x2_t, w), acc,
                                          false);
+}
+// the sigmoid of two values: v_pk_mul_f32 / v_pk_add_f32 around the two transcendentals of each (the file builds
+// without SLP packing, so the packed forms are spelled out as vector ops)
+__device__ __forceinline__ f32x2 sigmoid2(f32x2 z) {
+  const f32x2 t = z * -1.4426950408889634f;
+  const f32x2 d = f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + 1.0f;
+  return f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+// a (w_c, 0) / (0, w_c+1) bf16 tap dword pair -> the f16 pair (w_c, w_c+1)
+__device__ __forceinline__ h16x2 taps_f16(uint32_t lo, uint32_t hi) {
+  return __builtin_convertvector((f32x2{__uint_as_float(lo << 16), __uint_as_float(hi & 0xffff0000u)}), h16x2);
 }
 
 // S = depthwise stride.  OH x OW is the conv_pw (input) map; with S = 2 the depthwise writes the
@@ -72,6 +87,10 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
   // SPM = 3: the expand on e4m3 too: x = e4m3 rows of kp bytes (launch_se_*_f8 y8), wpw = e4m3 [rows][kp] with
   // per-channel scales wsc (pack_gemm_f8), one v_mfma_scale_f32_16x16x128_f8f6f4 per 128 k
   constexpr bool F8I = SPM == 3;
+  // e4m3 output: the tile holds f16 (11-bit significand against the output's 4), the depthwise accumulates in f16
+  // on v_pk_fma_f16 (two channels an instruction instead of one v_dot2 per channel); with 4 channels a lane.
+  // One image a workgroup only: same-box A/B (gpurun_out/f16dw) fp8 16x16 363 -> 335 us, 8x8 (G = 4) 227 -> 231 us
+  constexpr bool F16 = F8 && IRPW_F16 && IRPW_CG8 && G == 1;
   // the haloed tile: dynamic LDS sized for this launch's G images (ir_tile_bytes)
   extern __shared__ __attribute__((aligned(16))) char tile_raw[];
   bf16_t* tile = reinterpret_cast<bf16_t*>(tile_raw);
@@ -253,6 +272,29 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
     for (int ni = 0; ni < NT; ++ni) {
       const int cl = ni * 16 + 4 * g16;  // slice-local channel of acc[ni][.][0]
       const float4 bb = *reinterpret_cast<const float4*>(bpw + c0 + cl);
+      if constexpr (F16) {  // (scale,) bias, SiLU on packed f32, f16 pairs into the tile
+        f32x2 sc01 = f32x2{1.f, 1.f}, sc23 = f32x2{1.f, 1.f};
+        if constexpr (F8I) {
+          const float4 sc = *reinterpret_cast<const float4*>(wsc + c0 + cl);
+          sc01 = f32x2{sc.x, sc.y};
+          sc23 = f32x2{sc.z, sc.w};
+        }
+        const f32x2 b01 = f32x2{bb.x, bb.y}, b23 = f32x2{bb.z, bb.w};
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi) {
+          const int m = mw + mi * 16 + r16;
+          if (m >= MP) continue;
+          const f32x2 z01 = F8I ? __builtin_elementwise_fma(f32x2{acc[ni][mi][0], acc[ni][mi][1]}, sc01, b01)
+                                : f32x2{acc[ni][mi][0], acc[ni][mi][1]} + b01;
+          const f32x2 z23 = F8I ? __builtin_elementwise_fma(f32x2{acc[ni][mi][2], acc[ni][mi][3]}, sc23, b23)
+                                : f32x2{acc[ni][mi][2], acc[ni][mi][3]} + b23;
+          const h16x2 y01 = __builtin_convertvector(z01 * sigmoid2(z01), h16x2);
+          const h16x2 y23 = __builtin_convertvector(z23 * sigmoid2(z23), h16x2);
+          *reinterpret_cast<uint2*>(tile + lut[m] * MROW + cl) =
+              make_uint2(__builtin_bit_cast(uint32_t, y01), __builtin_bit_cast(uint32_t, y23));
+        }
+        continue;
+      }
       if constexpr (F8I) {  // the e4m3 weights' per-channel scales
         const float4 sc = *reinterpret_cast<const float4*>(wsc + c0 + cl);
 #pragma unroll
@@ -332,6 +374,51 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
         }
         il_st8(ys, (long)(n0 + g) * PO + p, cs_mid, c, a);  // the SE GEMM's interleaved operand
       }
+    } else if (F16 && g < gi && c < cs_mid) {
+      static_assert(!F16 || NCH == 4, "f16 depthwise: 4 channels a lane");
+      h16x2 w[9][2], b2[2];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const uint4 v = wdw_lds[t][cg];
+        w[t][0] = taps_f16(v.x, v.y);
+        w[t][1] = taps_f16(v.z, v.w);
+      }
+      {
+        const float4 v = bdw_lds[cg];
+        b2[0] = __builtin_convertvector((f32x2{v.x, v.y}), h16x2);
+        b2[1] = __builtin_convertvector((f32x2{v.z, v.w}), h16x2);
+      }
+      f32x2 s01 = f32x2{0.f, 0.f}, s23 = f32x2{0.f, 0.f};
+      for (int p = q; p < PO; p += lpi) {
+        int trow;  // haloed tile row of the tap-(1, 1) input pixel
+        if constexpr (S == 1) {
+          trow = lut[g * P + p];
+        } else {
+          const int oy = p / SOW, ox = p - (p / SOW) * SOW;
+          trow = g * IR + (S * oy - pad_t + 2) * WR + S * ox - pad_l + 2;
+        }
+        const bf16_t* base = tile + trow * MROW + cg * NCH;
+        uint2 in[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) in[t] = *reinterpret_cast<const uint2*>(base + off[t]);
+        h16x2 a0 = b2[0], a1 = b2[1];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          a0 = __builtin_elementwise_fma(__builtin_bit_cast(h16x2, in[t].x), w[t][0], a0);
+          a1 = __builtin_elementwise_fma(__builtin_bit_cast(h16x2, in[t].y), w[t][1], a1);
+        }
+        const f32x2 x01 = __builtin_convertvector(a0, f32x2), x23 = __builtin_convertvector(a1, f32x2);
+        const f32x2 g01 = sigmoid2(x01), g23 = sigmoid2(x23);
+        s01 += x01 * g01;  // the squeeze sums the unsaturated values
+        s23 += x23 * g23;
+        // min(x, 448) * sigmoid(x): saturated for e4m3 (SiLU >= -0.28), a NaN x stays NaN through the sigmoid
+        const f32x2 o01 = f32x2{fminf(x01.x, 448.f), fminf(x01.y, 448.f)} * g01;
+        const f32x2 o23 = f32x2{fminf(x23.x, 448.f), fminf(x23.y, 448.f)} * g23;
+        const int r = __builtin_amdgcn_cvt_pk_fp8_f32(o01.x, o01.y, 0, false);
+        uint8_t* y8 = reinterpret_cast<uint8_t*>(y) + ((size_t)(n0 + g) * PO + p) * cs_mid + c;
+        reinterpret_cast<uint32_t*>(y8)[0] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(o23.x, o23.y, r, true);
+      }
+      s[0] = s01.x; s[1] = s01.y; s[2 % NCH] = s23.x; s[3 % NCH] = s23.y;
     } else if (!SP && g < gi && c < cs_mid) {
       constexpr int NW2 = NCH / 2;  // tap dwords per lane and tap: (w_c, 0) / (0, w_c+1) pairs
       uint32_t w[9][NCH];
@@ -440,8 +527,8 @@ __global__ void __launch_bounds__(256, SP == 1 ? 3 : 4)
     ir_pwdw_s2_kernel(const bf16_t* __restrict__ x, int cs_in, int kp, const bf16_t* __restrict__ wpw,
                       const float* __restrict__ bpw, const uint32_t* __restrict__ wdw2, const float* __restrict__ bdw,
                       int N, int IH, int IW, int cs_mid, bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, int OH,
-                      int OW, int pad_t, int pad_l) {
-  ir_pwdw_body<4, 1, 2, SP>(x, cs_in, kp, wpw, bpw, wdw2, bdw, N, IH, IW, cs_mid, y, se_mean, OH, OW, pad_t, pad_l);
+                      int OW, int pad_t, int pad_l, const float* __restrict__ wsc) {
+  ir_pwdw_body<4, 1, 2, SP>(x, cs_in, kp, wpw, bpw, wdw2, bdw, N, IH, IW, cs_mid, y, se_mean, OH, OW, pad_t, pad_l, wsc);
 }
 
 // images per workgroup: up to 4 small images (measured on the 8x8 maps of blocks.5 in split fp32:
@@ -538,26 +625,37 @@ bool ir_fused_s2_supported(int IH, int IW, int cs_in, int cs_mid, bool split) {
 
 void launch_ir_pwdw_s2(const void* x, int N, int cs_in, int kp, const void* wpw, const float* bpw, const void* wdw,
                        const float* bdw, int IH, int IW, int OH, int OW, int pad_t, int pad_l, int cs_mid, void* y,
-                       void* se_mean, bool split, double flops, double bytes, hipStream_t s) {
+                       void* se_mean, bool split, double flops, double bytes, hipStream_t s, bool f8_out, const void* x8,
+                       const void* w8, const float* wsc, int kp8) {
   M2S_CHECK(ir_fused_s2_supported(IH, IW, cs_in, cs_mid, split) && kp % 32 == 0 && kp >= cs_in,
             "ir_pwdw_s2: unsupported shape");
   M2S_CHECK(OH == (IH + 1) / 2 && OW == (IW + 1) / 2 && OH * OW <= 64 && pad_t >= 0 && pad_t <= 1 && pad_l >= 0 &&
                 pad_l <= 1,
             "ir_pwdw_s2: geometry");
+  M2S_CHECK(!(split && f8_out), "ir_pwdw_s2: e4m3 output is a bf16-path variant");
+  const bool f8_in = x8 != nullptr;
+  M2S_CHECK(!f8_in || (f8_out && w8 && wsc && kp8 % 128 == 0 && kp8 >= cs_in), "ir_pwdw_s2: e4m3 expand operands");
+  if (f8_in) {  // the e4m3 operands replace the bf16 ones
+    x = x8;
+    wpw = w8;
+    kp = kp8;
+  }
+  const int mode = split ? 1 : f8_in ? 3 : f8_out ? 2 : 0;
   const dim3 grid(ceil_div(cs_mid, SL) * N);
   const bf16_t* xb = static_cast<const bf16_t*>(x);
   const bf16_t* wb = static_cast<const bf16_t*>(wpw);
   const uint32_t* wd = static_cast<const uint32_t*>(wdw);
-  if (split) {
-    ProfScope ps("ir_pwdw_s2_kernel<1>", flops, bytes, s);
-    hipLaunchKernelGGL(ir_pwdw_s2_kernel<1>, grid, dim3(256), ir_tile_bytes(IH, IW, 1, true), s, xb, cs_in, kp, wb, bpw, wd, bdw, N, IH, IW, cs_mid,
-                       static_cast<bf16_t*>(y), static_cast<bf16_t*>(se_mean), OH, OW, pad_t, pad_l);
-  } else {
-    ProfScope ps("ir_pwdw_s2_kernel<0>", flops, bytes, s);
-    hipLaunchKernelGGL(ir_pwdw_s2_kernel<0>, grid, dim3(256), ir_tile_bytes(IH, IW, 1, false), s, xb, cs_in, kp, wb, bpw, wd, bdw, N, IH, IW, cs_mid,
-                       static_cast<bf16_t*>(y), static_cast<bf16_t*>(se_mean), OH, OW, pad_t, pad_l);
+#define M2S_IRS2(SP_)                                                                                            \
+  if (mode == SP_) {                                                                                             \
+    ProfScope ps("ir_pwdw_s2_kernel<" #SP_ ">", flops, bytes, s);                                               \
+    hipLaunchKernelGGL(ir_pwdw_s2_kernel<SP_>, grid, dim3(256), ir_tile_bytes(IH, IW, 1, split), s, xb, cs_in, kp, wb, \
+                       bpw, wd, bdw, N, IH, IW, cs_mid, static_cast<bf16_t*>(y), static_cast<bf16_t*>(se_mean), OH, OW,  \
+                       pad_t, pad_l, wsc);                                                                       \
+    M2S_HIP(hipGetLastError());                                                                                  \
+    return;                                                                                                      \
   }
-  M2S_HIP(hipGetLastError());
+  M2S_IRS2(0) M2S_IRS2(1) M2S_IRS2(2) M2S_IRS2(3)
+#undef M2S_IRS2
 }
 
 }  // namespace m2s

@@ -2,7 +2,8 @@
 //   conv_pw (1x1 expand, MFMA) + bn1 + SiLU -> fp32 LDS band -> conv_dw 3x3/s2 (TF-SAME) + bn2 + SiLU -> the
 //   SE GEMM's operand, + the SE squeeze's per-band partial sums.
 // SP = 1: split fp32 (three-term MFMA on hi/lo input and weights, output the interleaved [hi 32 | lo 32]
-// operand); SP = 0: bf16 input / weights / output (the bf16 and fp8 engines), one MFMA term.
+// operand); SP = 0: bf16 input / weights / output (the bf16 engine), one MFMA term; SP = 2: the same with the
+// depthwise output stored as OCP e4m3 bytes (fp8 engines: the operand of the e4m3 SE GEMM, gemm128 KIND_F8_SE).
 // (timm InvertedResidual conv_pw/bn1/conv_dw/bn2/se; mri_acoustic_model.py:28-34.)
 //
 // Unfused, conv_pw wrote the 224-channel expanded map at 32x32 as hi/lo pairs (1.76 GB per 1920 frames)
@@ -37,12 +38,13 @@ constexpr int SB_MT = 5;                 // 16-position tiles per wave at most: 
 
 size_t sb_tile_bytes(int IW) { return (size_t)SB_ROWS * (IW + 2) * SB_MROW * sizeof(float); }
 
-template <int KSN, int SP>  // expand k-steps (kp / 32), split fp32
+template <int KSN, int SPM>  // expand k-steps (kp / 32), 0 bf16 / 1 split fp32 / 2 bf16 with e4m3 output
 __global__ void __launch_bounds__(256, 3)
     ir_s2band_kernel(const bf16_t* __restrict__ x, int IH, int IW, const bf16_t* __restrict__ wpw,
                      const float* __restrict__ bpw, const float* __restrict__ wdw, const float* __restrict__ bdw,
                      int OH, int OW, int pad_t, int pad_l, int cs_mid, bf16_t* __restrict__ y,
                      float* __restrict__ psum) {
+  constexpr bool SP = SPM == 1, F8 = SPM == 2;
   constexpr int CS = KSN * 32;  // input channel stride = expand K
   constexpr int R = SP ? 2 : 1;  // bf16 planes per row (hi, lo)
   extern __shared__ __attribute__((aligned(16))) float tile[];  // [SB_ROWS][IW + 2][SB_MROW]
@@ -163,6 +165,8 @@ __global__ void __launch_bounds__(256, 3)
       const long pix = ((long)n * OH + oy0 + oyl) * OW + ox;
       if constexpr (SP) {
         il_st8(ys, pix, cs_mid, c0 + cg * 8, a);
+      } else if constexpr (F8) {  // 8 channels -> 8 e4m3 bytes at byte (pix, c) of the (N, OH*OW, cs_mid) map
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(y) + pix * cs_mid + c0 + cg * 8) = e4m3x8(a);
       } else {
         *reinterpret_cast<uint4*>(y + pix * cs_mid + c0 + cg * 8) =
             make_uint4(pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(a[4], a[5]), pack_bf16x2(a[6], a[7]));
@@ -192,8 +196,10 @@ bool ir_s2band_supported(int IH, int IW, int OH, int OW, int cs_in, int kp, int 
 
 void launch_ir_s2band(const void* x, int N, int IH, int IW, int cs_in, int kp, const void* wpw, const float* bpw,
                       const float* wdw, const float* bdw, int OH, int OW, int pad_t, int pad_l, int cs_mid, void* y,
-                      float* psum, bool split, double flops, double bytes, hipStream_t s) {
+                      float* psum, bool split, double flops, double bytes, hipStream_t s, bool f8_out) {
   M2S_CHECK(N > 0 && ir_s2band_supported(IH, IW, OH, OW, cs_in, kp, cs_mid), "ir_s2band: unsupported shape");
+  M2S_CHECK(!(split && f8_out), "ir_s2band: e4m3 output is a bf16-path variant");
+  const int mode = split ? 1 : f8_out ? 2 : 0;
   M2S_CHECK(pad_t >= 0 && pad_t <= 1 && pad_l >= 0 && pad_l <= 1 && 2 * (OW - 1) - pad_l + 2 <= IW &&
                 2 * (OH - 1) - pad_t + 2 <= IH,
             "ir_s2band: geometry");
@@ -203,12 +209,12 @@ void launch_ir_s2band(const void* x, int N, int IH, int IW, int cs_in, int kp, c
   const bf16_t* wb = static_cast<const bf16_t*>(wpw);
   bf16_t* yb = static_cast<bf16_t*>(y);
 #define M2S_SB(KSN_, SP_)                                                                                   \
-  if (kp == KSN_ * 32 && split == (SP_ == 1)) {                                                              \
+  if (kp == KSN_ * 32 && mode == SP_) {                                                                      \
     ProfScope ps("ir_s2band_kernel<" #KSN_ ", " #SP_ ">", flops, bytes, s);                                  \
     hipLaunchKernelGGL((ir_s2band_kernel<KSN_, SP_>), grid, dim3(256), lds, s, xb, IH, IW, wb, bpw, wdw, bdw, OH, OW, \
                        pad_t, pad_l, cs_mid, yb, psum);                                                       \
   }
-  M2S_SB(2, 1) M2S_SB(1, 1) M2S_SB(2, 0) M2S_SB(1, 0)
+  M2S_SB(2, 1) M2S_SB(1, 1) M2S_SB(2, 0) M2S_SB(1, 0) M2S_SB(2, 2) M2S_SB(1, 2)
 #undef M2S_SB
   M2S_HIP(hipGetLastError());
 }

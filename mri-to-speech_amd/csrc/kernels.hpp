@@ -112,11 +112,12 @@ int ir_s2band_bands(int OH);
 bool ir_s2band_supported(int IH, int IW, int OH, int OW, int cs_in, int kp, int cs_mid);
 void launch_ir_s2band(const void* x, int N, int IH, int IW, int cs_in, int kp, const void* wpw, const float* bpw,
                       const float* wdw, const float* bdw, int OH, int OW, int pad_t, int pad_l, int cs_mid, void* y,
-                      float* psum, bool split, double flops, double bytes, hipStream_t s);
+                      float* psum, bool split, double flops, double bytes, hipStream_t s, bool f8_out = false);
 bool ir_fused_s2_supported(int IH, int IW, int cs_in, int cs_mid, bool split);
 void launch_ir_pwdw_s2(const void* x, int N, int cs_in, int kp, const void* wpw, const float* bpw, const void* wdw,
                        const float* bdw, int IH, int IW, int OH, int OW, int pad_t, int pad_l, int cs_mid, void* y,
-                       void* se_mean, bool split, double flops, double bytes, hipStream_t s);
+                       void* se_mean, bool split, double flops, double bytes, hipStream_t s, bool f8_out = false,
+                       const void* x8 = nullptr, const void* w8 = nullptr, const float* wsc = nullptr, int kp8 = 0);
 
 // Fused HiFi-GAN ResBlock1 (all (c1, c2) pairs of one resblock + the MRF running sum), bf16 for C in
 // {32, 64} or split fp32 (split: x, S as [hi C | lo C] per position) for C = 32:

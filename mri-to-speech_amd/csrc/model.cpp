@@ -85,6 +85,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_IR_WS_S2")) ir_ws_s2_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_EXPAND")) f8_expand_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_F8_S2")) f8_s2_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_ER")) f8_er_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_ER8_X8")) er8_x8_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_ER2")) f8_er2_ = std::strcmp(e, "0") != 0;
@@ -394,7 +395,8 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
         const int m = b.mid, cs = chan_stride(m);
         max_mid_cs_ = std::max(max_mid_cs_, cs);
         conv1x1(b.c1, q + "conv_pw.weight", cin, m, fold_bn(sd, q + "bn1", m));
-        if (dtype == M2S_DT_FP8 && b.stride == 1 && chan_stride(cin) <= 256) {  // the e4m3 expand (ir_pwdw x8)
+        // the e4m3 expand (ir_pwdw / ir_pwdw_s2 x8; the stride-2 blocks' copy is used where ir_pwdw_s2 runs, blocks.5.0)
+        if (dtype == M2S_DT_FP8 && chan_stride(cin) <= 256) {
           const float* wq = need(sd, q + "conv_pw.weight", {m, cin, 1, 1}).data;
           const BN bn1 = fold_bn(sd, q + "bn1", m);
           size_t boff = 0;
@@ -437,7 +439,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
         pack_conv(arena_, se_dt, b.se2, [&](int, int n, int, int c) { return w2[(size_t)n * rd + c]; },
                   [&](int n) { return b2[n]; });
         conv1x1(b.c2, q + "conv_pwl.weight", m, b.cout, fold_bn(sd, q + "bn3", b.cout));
-        if (dtype == M2S_DT_FP8 && b.stride == 1 && chan_stride(b.cout) <= 224) {
+        if (dtype == M2S_DT_FP8 && chan_stride(b.cout) <= 224) {  // (stride 2: used with ir_pwdw_s2's e4m3 output)
           const float* wq = need(sd, q + "conv_pwl.weight", {b.cout, m, 1, 1}).data;
           const BN bn3 = fold_bn(sd, q + "bn3", b.cout);
           b.f8_kp = round_up(cs, 128);
@@ -536,7 +538,7 @@ size_t Acoustic::effnet_x8(int H, int W) const {
     int nh, nw;
     same_pad(oh, 3, b.stride, &nh, &ph);
     same_pad(ow, 3, b.stride, &nw, &pw);
-    if (b.f8_pw && f8_expand_) mx = std::max(mx, (size_t)nh * nw * b.f8x_kp);  // stride 1: the block input's map
+    if (b.f8_pw && f8_expand_) mx = std::max(mx, (size_t)oh * ow * b.f8x_kp);  // the block input's map
     if (b.er8 && f8_er_) mx = std::max(mx, (size_t)nh * nw * 32);              // er8_fused x8 / y8 (N, H, W, 32)
     if (b.er8w && f8_er_) mx = std::max(mx, (size_t)nh * nw * 64);             // er8w_fused x8 / y8 (N, H, W, 64)
     oh = nh;
@@ -655,8 +657,14 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
     for (size_t k = front ? 2 : 0; k < blocks_.size(); ++k) {
       const Block& b = blocks_[k];
       uint8_t* next8 = nullptr;  // the e4m3 copy of this block's output, if its SE GEMM wrote one
-      // the next block takes an e4m3 expand operand (fp8 engines, stride-1 IR blocks)
-      const bool want8 = X8[0] && f8_expand_ && k + 1 < blocks_.size() && blocks_[k + 1].f8_pw && blocks_[k + 1].stride == 1;
+      int nh, nw, qt, ql;
+      same_pad(oh, 3, b.stride, &nh, &qt);
+      same_pad(ow, 3, b.stride, &nw, &ql);
+      // the next block takes an e4m3 expand operand (fp8 engines: stride-1 IR blocks, and the stride-2 one on
+      // ir_pwdw_s2, whose input map is this block's nh x nw output)
+      const bool want8 = X8[0] && f8_expand_ && k + 1 < blocks_.size() && blocks_[k + 1].f8_pw &&
+                         (blocks_[k + 1].stride == 1 ||
+                          (f8_s2_ && ir_fused_s2_supported(nh, nw, blocks_[k + 1].c1.cs_in, chan_stride(blocks_[k + 1].mid), false)));
       // the next block is an e4m3 EdgeResidual (er8_fused): this block also stores its output as e4m3 bytes
       // (er8w_fused, blocks.2.1/.2, always takes its e4m3 operand from the producer; M2S_ER8_X8=0 switches only
       // er8_fused to its in-kernel conversion)
@@ -664,9 +672,6 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                                         ((er8_x8_ && blocks_[k + 1].er8) || (f8_er2_ && blocks_[k + 1].er8w))
                                     ? (cur8 == X8[0] ? X8[1] : X8[0])
                                     : nullptr;
-      int nh, nw, qt, ql;
-      same_pad(oh, 3, b.stride, &nh, &qt);
-      same_pad(ow, 3, b.stride, &nw, &ql);
       auto a2d = [&](const PConv& pc, const void* x, void* y) {
         ConvArgs a = conv_args(pc);
         a.x = x;
@@ -792,15 +797,27 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         } else if (FUSABLE && b.stride == 2 && ir_fused_ && ir_fused_s2_supported(oh, ow, b.c1.cs_in, cs, SPL) &&
                    nh * nw <= 64) {
           const double Pi = (double)oh * ow, Po = (double)nh * nw, es = SPL ? 4.0 : 2.0;
+          // fp8 engines (blocks.5.0): e4m3 depthwise output for the e4m3 SE GEMM, the expand on e4m3 as for stride 1
+          f8 = f8_s2_ && b.f8_pwl && se_gemm_f8_supported(nh * nw, cs, chan_stride(b.cout));
+          const bool f8x = f8 && f8_expand_ && b.f8_pw && X8[0];
+          if (f8x && !cur8) {  // no e4m3 producer wrote this input: convert it
+            cur8 = X8[0];
+            launch_rows_e4m3(cur, (long)nc * oh * ow, b.c1.cs_in, cur8, b.f8x_kp, s);
+          }
           launch_ir_pwdw_s2(cur, nc, b.c1.cs_in, b.c1.kp, b.c1.w, b.c1.b, wdw, static_cast<const float*>(arena_.ptr(b.dw_b)),
                             oh, ow, nh, nw, qt, ql, cs, M2, se_mean, SPL, 2.0 * nc * b.mid * (Pi * b.c1.cin + Po * 9),
-                            es * nc * (Pi * b.c1.cs_in + Po * cs), s);
+                            nc * ((f8x ? 1.0 : es) * Pi * b.c1.cin + (f8 ? 1.0 : es) * Po * b.mid), s, f8,
+                            f8x ? cur8 : nullptr, f8x ? arena_.ptr(b.f8x_w) : nullptr,
+                            f8x ? static_cast<const float*>(arena_.ptr(b.f8x_s)) : nullptr, b.f8x_kp);
         } else if (FUSABLE && b.stride == 2 && ir_fused_ && ir_s2band_ &&
                    ir_s2band_supported(oh, ow, nh, nw, b.c1.cs_in, b.c1.kp, cs)) {
           const double Pi = (double)oh * ow, Po = (double)nh * nw, es = SPL ? 4.0 : 2.0;
+          // fp8 engines (blocks.3.0): e4m3 depthwise output for the e4m3 SE GEMM (the expand stays bf16)
+          f8 = f8_s2_ && b.f8_pwl && se_gemm_f8_supported(nh * nw, cs, chan_stride(b.cout));
           launch_ir_s2band(cur, nc, oh, ow, b.c1.cs_in, b.c1.kp, b.c1.w, b.c1.b, static_cast<const float*>(arena_.ptr(b.dw_w)),
                            static_cast<const float*>(arena_.ptr(b.dw_b)), nh, nw, qt, ql, cs, M2, sums, SPL,
-                           2.0 * nc * b.mid * (Pi * 1.125 * b.c1.cin + Po * 9), es * nc * (Pi * b.c1.cs_in + Po * cs), s);
+                           2.0 * nc * b.mid * (Pi * 1.125 * b.c1.cin + Po * 9),
+                           nc * (es * Pi * b.c1.cs_in + (f8 ? 1.0 : es) * Po * cs), s, f8);
           ProfScope ps(tname<T>("se_mean_kernel"), 0.0, 4.0 * nc * cs * ir_s2band_bands(nh) + es * nc * cs, s);
           launch_se_mean<T>(sums, nc, ir_s2band_bands(nh), cs, 1.0f / (float)(nh * nw), se_mean, s);
         } else {
@@ -982,12 +999,13 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
     : h_(h), dtype_(dtype), device_(device) {
   M2S_CHECK(dtype == M2S_DT_F32 || dtype == M2S_DT_BF16 || dtype == M2S_DT_BF16X3 || dtype == M2S_DT_FP8, "bad dtype");
   M2S_CHECK(h.resblock == 1 || h.resblock == 2, "resblock must be 1 or 2");
-  // fp8 engines: e4m3 resblock (MRF) convs at C = 128 / 256; conv_pre, the upsamplers and the fused
-  // C = 32 / 64 ResBlock1 kernels stay bf16
+  // fp8 engines: e4m3 resblock (MRF) convs at C = 64 / 128 / 256; conv_pre, the upsamplers and the fused
+  // C = 32 ResBlock1 kernel stay bf16
   const int io_dt = dtype == M2S_DT_FP8 ? M2S_DT_BF16 : dtype;
   if (const char* e = std::getenv("M2S_MRF_FUSED")) mrf_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_MRF_BATCH")) mrf_batch_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_MRF_HALO")) mrf_halo_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_F8_MRF64")) f8_mrf64_ = std::strcmp(e, "0") != 0;
   M2S_CHECK(h.n_up >= 1 && h.n_up <= 8 && h.n_kernels >= 1 && h.n_kernels <= 8, "bad generator config");
   const int c0 = h.upsample_initial_channel;
   {  // conv_pre: Conv1d(num_mels, c0, 7), no weight norm (models.py:94)
@@ -1075,14 +1093,16 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
                   }
         return arena_.add_vec(f);
       };
-      // fp8: the C = 128 / 256 resblock convs as e4m3 bytes for conv1d_f8 (K = 128 block-scaled MFMA)
-      const bool q8 = dtype == M2S_DT_FP8 && h.resblock == 1 && !frag && conv1d_f8_supported(co, kk);
+      // fp8: the C = 128 / 256 (and, f8_mrf64_, C = 64) resblock convs as e4m3 bytes for conv1d_f8 (K = 128
+      // block-scaled MFMA; C = 64: two taps a K step)
+      const bool q8 = dtype == M2S_DT_FP8 && h.resblock == 1 && (!frag || (co == 64 && f8_mrf64_)) &&
+                      conv1d_f8_supported(co, kk);
       auto mk_q8 = [&](const std::string& name) {
         std::vector<float> wv = fold_wn(sd, name, {co, co, kk});
         const HostTensor& bv = need(sd, name + ".bias", {co});
         RB::F8 f;
         pack_gemm_f8(
-            arena_, kk * co, co, co, kk * co,
+            arena_, kk * co, co, co, round_up(kk * co, 128),
             [&](int n, int kx) { return wv[((size_t)n * co + kx % co) * kk + kx / co]; },  // K = tap-major t C + c
             [&](int n) { return bv.data[n]; }, &f.w, &f.s, &f.b);
         return f;

@@ -109,6 +109,8 @@ class Acoustic {
   bool er8_x8_ = true;           // ... their input as e4m3 bytes from the producer (env M2S_ER8_X8=0: converted
                                  // in er8_fused; the same bytes, test_fp8_er8_e4m3_handoff_is_exact)
   bool f8_expand_ = true;        // fp8: the stride-1 IR expand on e4m3 (env M2S_F8_EXPAND=0: bf16 expand)
+  bool f8_s2_ = true;            // fp8: the stride-2 IR blocks (blocks.3.0 ir_s2band, blocks.5.0 ir_pwdw_s2) with e4m3
+                                 // depthwise output + e4m3 SE GEMM (env M2S_F8_S2=0: bf16)
   bool se_fused_ = true;    // bf16: SE excitation in one kernel (env M2S_SE_FUSED=0: two GEMMs)
   bool er_fused_ = true;    // bf16: EdgeResidual 32->128->32 in one kernel (env M2S_ER_FUSED=0 disables)
   bool se_sp_ = false;      // split: SE-gated conv_pwl on gemm128.hip (env M2S_SE_SP=1; default conv_gemm's in-LDS
@@ -191,6 +193,7 @@ class Vocoder {
   size_t act_elems(int B, int T) const;
   bool mrf_fused_ = true;
   bool mrf_halo_ = true;   // split: C = 64 MRF convs with once-staged input rows (env M2S_MRF_HALO=0: conv_gemm)
+  bool f8_mrf64_ = true;   // fp8: the C = 64 MRF convs on e4m3 (conv1d_f8; env M2S_F8_MRF64=0: fused bf16 ResBlock1)
   bool mrf_batch_ = true;  // split: resblocks of a conv_gemm MRF stage batched per launch (env M2S_MRF_BATCH=0 disables)  // bf16: fused ResBlock1 kernel for C in {32, 64} (env M2S_MRF_FUSED=0 disables)
 
  private:

@@ -256,3 +256,75 @@ def test_fp8_se_y8_e4m3_handoff_is_exact(rt, monkeypatch):
     for i in (10, 12, 14, 18, 20, 28):
         assert torch.equal(ey.probe(fr, i), ec.probe(fr, i)), i
     assert torch.equal(ey.effnet(fr), ec.effnet(fr))
+
+
+@pytest.mark.parametrize("n", [5, 300])
+def test_fp8_e4m3_stride2_block(rt, monkeypatch, n):
+    """The stride-2 IR blocks on e4m3 in the fp8 engine: blocks.5.0 (16x16 -> 8x8) on ir_pwdw_s2 mode 3 (the expand
+    on the e4m3 block input written by blocks.4.5's SE GEMM, the f16 depthwise, e4m3 output) and the e4m3 SE-gated
+    conv_pwl (se_ws f8); blocks.3.0 (32x32 -> 16x16) on ir_s2band mode 2 (bf16 expand, e4m3 depthwise output) and
+    the e4m3 SE GEMM (gemm128), against the bf16 blocks (M2S_F8_S2=0) and the fp32 oracle.  The launch log shows
+    which kernels ran.  Bars as for the stride-1 e4m3 expand: taps >= 0.995 against the bf16 blocks, pooled
+    features per frame >= 0.995 against the oracle (0.99 end to end)."""
+    from m2s import _native
+    st = synth.synth_acoustic_state(8)
+    fr = torch.from_numpy(synth.synth_frames(1, n, seed=49)[0]).to(DEV)
+    monkeypatch.setenv("M2S_F8_S2", "1")
+    e8 = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    monkeypatch.setenv("M2S_F8_S2", "0")
+    eb = rt.AcousticEngine(st, dtype="fp8", device=DEV)
+    names = {}
+    for key, eng in (("f8", e8), ("bf16", eb)):
+        _native.prof_enable(True)
+        eng.probe(fr, 19)
+        torch.cuda.synchronize()
+        names[key] = {r["name"] for r in _native.prof_launches()}
+        _native.prof_enable(False)
+    assert "ir_pwdw_s2_kernel<3>" in names["f8"] and "ir_pwdw_s2_kernel<0>" not in names["f8"], names["f8"]
+    assert "ir_s2band_kernel<2, 2>" in names["f8"] and "ir_s2band_kernel<2, 0>" not in names["f8"], names["f8"]
+    assert "ir_pwdw_s2_kernel<0>" in names["bf16"] and "ir_s2band_kernel<2, 0>" in names["bf16"], names["bf16"]
+    # after blocks.3.0, 3.1 (its e4m3 input now from 3.0's SE GEMM), 5.0, 5.1, 5.9
+    for i in (9, 10, 19, 20, 28):
+        a, b = e8.probe(fr, i).cpu().numpy(), eb.probe(fr, i).cpu().numpy()
+        assert np.isfinite(a).all()
+        c = _cos(a.ravel(), b.ravel())
+        print(f"tap {i}: cos(e4m3 blocks.5.0, bf16 blocks.5.0) {c:.6f}")
+        assert c >= 0.995, (i, c)
+    if n == 5:
+        sd = {k: torch.from_numpy(v) for k, v in st.items()}
+        ref = effnet.effnet_gap(sd, fr.cpu()).numpy()
+        f = e8.effnet(fr).cpu().numpy()
+        cmin = min(_cos(f[i], ref[i]) for i in range(n))
+        print(f"features vs oracle: min per-frame cos {cmin:.6f}")
+        assert cmin >= 0.995
+
+
+@pytest.mark.parametrize("frames", [37, 300])
+def test_fp8_mrf64_e4m3(rt, monkeypatch, frames):
+    """The C = 64 MRF stage on e4m3 in the fp8 vocoder (conv1d_f8 with two taps per 128-byte K step, the odd tap
+    count ending on a zero tap; gemm128_kernel<1, 4, 1, 4, 3>) against the fused bf16 ResBlock1 (M2S_F8_MRF64=0)
+    and the fp32 oracle: wav cosine >= 0.999 between the two engines and >= 0.99 against the
+    oracle, the launch log showing which kernel ran.  Ragged: 3 clips, stage lengths not multiples of any tile."""
+    from m2s import _native
+    sd = synth.synth_generator_state(5, HIFIGAN_H)
+    mel = synth.synth_mel_log(3, 64, frames, seed=12)
+    monkeypatch.setenv("M2S_F8_MRF64", "1")
+    v8 = rt.VocoderEngine(sd, HIFIGAN_H, dtype="fp8", device=DEV)
+    monkeypatch.setenv("M2S_F8_MRF64", "0")
+    vb = rt.VocoderEngine(sd, HIFIGAN_H, dtype="fp8", device=DEV)
+    x = torch.from_numpy(mel).to(DEV)
+    out, names = {}, {}
+    for key, v in (("f8", v8), ("bf16", vb)):
+        _native.prof_enable(True)
+        out[key] = v.forward(x).cpu().numpy().reshape(3, -1)
+        torch.cuda.synchronize()
+        names[key] = {r["name"] for r in _native.prof_launches()}
+        _native.prof_enable(False)
+    assert "gemm128_kernel<1, 4, 1, 4, 3>" in names["f8"] and not any("rb1_fused_kernel<64" in n for n in names["f8"]), names["f8"]
+    assert any("rb1_fused_kernel<64" in n for n in names["bf16"]), names["bf16"]
+    ref = hifigan.generator({k: torch.from_numpy(v) for k, v in sd.items()}, HIFIGAN_H, torch.from_numpy(mel)).numpy()
+    for b in range(3):
+        c2, cr = _cos(out["f8"][b], out["bf16"][b]), _cos(out["f8"][b], ref[b])
+        print(f"clip {b}: wav cos(e4m3 C=64, bf16 C=64) {c2:.6f}, vs oracle {cr:.6f}")
+        assert np.isfinite(out["f8"][b]).all()
+        assert c2 >= 0.999 and cr >= COS_MIN, (b, c2, cr)
