@@ -6,8 +6,8 @@
 //   K step = 128 e4m3 channels:
 //   y[m][n] = wscale[n] * sum_k W8[n][k] * e4m3(gate[img(m)][k] * X8[m][k]) + bias[n] (+ res[m][n])
 // KIND_F8_C1D (fp8 engines, the HiFi-GAN MRF convs at C = 64 / 128 / 256, models.py:11-49: causal dilated
-//   Conv1d, the operand already LeakyReLU'd by its producer), same MFMA (C = 64: a K step holds two taps, the
-//   row's first four 16-byte chunks tap 2 st and the last four tap 2 st + 1; an odd tap count ends on a zero tap):
+//   Conv1d, the operand already LeakyReLU'd by its producer), same MFMA (C = 64 / 32: a K step holds 128 / C taps,
+//   C / 16 of the row's 16-byte chunks each, in tap order; a tap count not a multiple ends on zero taps):
 //   v[m][n] = wscale[n] * sum_{t,c} W8[n][t C + c] * X8[b, l + t dil - (k - 1) dil][c] + bias[n] (+ res[m][n])
 //   y (bf16) = v, or the MRF running sum (y + v) [/ nk]; y8 (e4m3) = lrelu(v) for the next conv's operand.
 // KIND_SP_SE (bf16x3 engines, the same SE-gated conv_pwl in split fp32), K step = 32 channels as
@@ -79,7 +79,7 @@ struct G128Args {
   int M, P, cs_in, kp, cs_out, n_tiles, nimg;  // P: SE rows per image, C1D sequence length L
   int ld8;                                      // F8 SE: y8 row bytes
   int dil, pad_left, accum;                     // C1D: tap dilation, causal left pad, MRF sum mode (0 / 1 / 2)
-  int ntap;                                     // C1D: taps (C = 64: K steps hold two)
+  int ntap;                                     // C1D: taps (C < 128: a K step holds 128 / C)
   float accum_div, slope8;
 };
 
@@ -127,12 +127,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) gemm128_kernel(const G128Args
   asm volatile("" : "+s"(zp));
   // SE: K step st = input channels [128 st, 128 st + 128) of the row.  C1D: tap t = st / gpt, channels
   // 128 (st % gpt) .. of input position l + t dil - pad_left of the row's sequence (zero outside [0, L)).
-  const bool two = !SE && a.cs_in == 64;               // C1D, C = 64: two taps a K step
-  const int gpt = two ? 1 : a.cs_in / F8_ROW;          // C1D: K steps per tap
+  const int tpk = !SE && a.cs_in < F8_ROW ? F8_ROW / a.cs_in : 1;  // C1D: taps a K step (C = 64: 2, C = 32: 4)
+  const int cpt = 8 / tpk;                                        // ... and 16-byte chunks a tap
+  const bool two = tpk > 1;
+  const int gpt = two ? 1 : a.cs_in / F8_ROW;                      // C1D: K steps per tap
   const uint8_t* srow[PER];  // row base (+ logical chunk offset; C1D: at tap 0 with the pad), or null
   int cofs[PER];             // SE: logical chunk byte offset within the K step
   int lpos[PER];             // C1D: position of tap 0 within the sequence (l - pad_left)
-  int thalf[PER];            // C1D, C = 64: the chunk's tap within the K step's pair
+  int thalf[PER];            // C1D, C < 128: the chunk's tap within the K step
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int blk = wave + NW * j;
@@ -140,7 +142,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) gemm128_kernel(const G128Args
     const int c = pch ^ swz128<SP>(lr & 15);
     cofs[j] = c * 16;
     lpos[j] = 0;
-    thalf[j] = two ? c >> 2 : 0;
+    thalf[j] = two ? c / cpt : 0;
     if (blk < A_BLK) {  // SP: hi chunks 0-3 from the row's hi half, lo chunks 4-7 from its lo half
       srow[j] = SP ? a.w + (size_t)(n0 + lr) * a.kp * 4 + (c < 4 ? c * 16 : a.kp * 2 + (c - 4) * 16)
                    : a.w + (size_t)(n0 + lr) * a.kp + c * 16;
@@ -151,7 +153,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) gemm128_kernel(const G128Args
       } else {
         const int l = m - (m / a.P) * a.P;
         lpos[j] = l - a.pad_left;
-        srow[j] = m < a.M ? a.x + ((long)m - a.pad_left) * a.cs_in + (two ? (c & 3) : c) * 16 : nullptr;
+        srow[j] = m < a.M ? a.x + ((long)m - a.pad_left) * a.cs_in + (two ? c % cpt : c) * 16 : nullptr;
       }
     }
   }
@@ -169,8 +171,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) gemm128_kernel(const G128Args
       } else if constexpr (SE) {
         src = srow[j] && st * F8_ROW + cofs[j] < a.cs_in ? static_cast<const void*>(srow[j] + st * F8_ROW) : zp;
       } else if (two) {
-        const int tt = 2 * st + thalf[j], lp = lpos[j] + tt * a.dil;
-        src = srow[j] && tt < a.ntap && lp >= 0 && lp < a.P ? static_cast<const void*>(srow[j] + (long)tt * a.dil * 64)
+        const int tt = tpk * st + thalf[j], lp = lpos[j] + tt * a.dil;
+        src = srow[j] && tt < a.ntap && lp >= 0 && lp < a.P ? static_cast<const void*>(srow[j] + (long)tt * a.dil * a.cs_in)
                                                              : static_cast<const void*>(zp);
       } else {
         const int lp = lpos[j] + t * a.dil;
@@ -474,7 +476,7 @@ void launch_se_gemm_f8(const void* x8, int M, int P, int cs_in, const void* w8, 
   }
 }
 
-bool conv1d_f8_supported(int C, int k) { return (C == 64 || C == 128 || C == 256) && k >= 1 && k <= 31; }
+bool conv1d_f8_supported(int C, int k) { return (C == 32 || C == 64 || C == 128 || C == 256) && k >= 1 && k <= 31; }
 
 void launch_conv1d_f8(const void* x8, int B, int L, int C, int k, int dil, const void* w8, const float* wscale,
                       const float* bias, const void* res, void* y, void* y8, float slope8, int accum, float accum_div,
@@ -495,14 +497,16 @@ void launch_conv1d_f8(const void* x8, int B, int L, int C, int k, int dil, const
   a.M = B * L;
   a.P = L;
   a.cs_in = a.cs_out = C;
-  a.kp = round_up(k * C, F8_ROW);  // C = 64, odd k: the last K step's second tap is a zero tap
+  a.kp = round_up(k * C, F8_ROW);  // C < 128: the last K step may end on zero taps
   a.ntap = k;
   a.dil = dil;
   a.pad_left = (k - 1) * dil;
   a.accum = accum;
   a.accum_div = accum_div;
   a.slope8 = slope8;
-  if (C == 64)
+  if (C == 32)
+    launch_tile<KIND_F8_C1D, 4, 1, 2>(a, s, flops, bytes);  // 256 positions x 32 channels
+  else if (C == 64)
     launch_tile<KIND_F8_C1D, 4, 1, 4>(a, s, flops, bytes);  // 256 positions x 64 channels
   else if (C == 128)
     launch_tile<KIND_F8_C1D, 4, 1, 8>(a, s, flops, bytes);  // 256 positions x 128 channels

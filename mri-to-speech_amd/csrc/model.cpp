@@ -1006,6 +1006,7 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
   if (const char* e = std::getenv("M2S_MRF_BATCH")) mrf_batch_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_MRF_HALO")) mrf_halo_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_MRF64")) f8_mrf64_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_F8_MRF32")) f8_mrf32_ = std::strcmp(e, "0") != 0;
   M2S_CHECK(h.n_up >= 1 && h.n_up <= 8 && h.n_kernels >= 1 && h.n_kernels <= 8, "bad generator config");
   const int c0 = h.upsample_initial_channel;
   {  // conv_pre: Conv1d(num_mels, c0, 7), no weight norm (models.py:94)
@@ -1095,7 +1096,8 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
       };
       // fp8: the C = 128 / 256 (and, f8_mrf64_, C = 64) resblock convs as e4m3 bytes for conv1d_f8 (K = 128
       // block-scaled MFMA; C = 64: two taps a K step)
-      const bool q8 = dtype == M2S_DT_FP8 && h.resblock == 1 && (!frag || (co == 64 && f8_mrf64_)) &&
+      const bool q8 = dtype == M2S_DT_FP8 && h.resblock == 1 &&
+                      (!frag || (co == 64 && f8_mrf64_) || (co == 32 && f8_mrf32_)) &&
                       conv1d_f8_supported(co, kk);
       auto mk_q8 = [&](const std::string& name) {
         std::vector<float> wv = fold_wn(sd, name, {co, co, kk});

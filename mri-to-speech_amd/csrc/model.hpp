@@ -193,7 +193,11 @@ class Vocoder {
   size_t act_elems(int B, int T) const;
   bool mrf_fused_ = true;
   bool mrf_halo_ = true;   // split: C = 64 MRF convs with once-staged input rows (env M2S_MRF_HALO=0: conv_gemm)
-  bool f8_mrf64_ = true;   // fp8: the C = 64 MRF convs on e4m3 (conv1d_f8; env M2S_F8_MRF64=0: fused bf16 ResBlock1)
+  // fp8: the C = 64 / 32 MRF convs on e4m3 (conv1d_f8, 128 / C taps a K step; env M2S_F8_MRF64=1 / M2S_F8_MRF32=1).
+  // Off: the fused bf16 ResBlock1 keeps a resblock's intermediates on chip and is faster at configs[4] (8 x 1000
+  // frames, same box, gpurun_out/f8s2: fp8 step 74.8 ms with both fused, 79.7 with C = 64 on e4m3, 85.1 with both)
+  bool f8_mrf64_ = false;
+  bool f8_mrf32_ = false;
   bool mrf_batch_ = true;  // split: resblocks of a conv_gemm MRF stage batched per launch (env M2S_MRF_BATCH=0 disables)  // bf16: fused ResBlock1 kernel for C in {32, 64} (env M2S_MRF_FUSED=0 disables)
 
  private:

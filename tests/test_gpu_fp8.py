@@ -300,17 +300,20 @@ def test_fp8_e4m3_stride2_block(rt, monkeypatch, n):
 
 
 @pytest.mark.parametrize("frames", [37, 300])
-def test_fp8_mrf64_e4m3(rt, monkeypatch, frames):
-    """The C = 64 MRF stage on e4m3 in the fp8 vocoder (conv1d_f8 with two taps per 128-byte K step, the odd tap
-    count ending on a zero tap; gemm128_kernel<1, 4, 1, 4, 3>) against the fused bf16 ResBlock1 (M2S_F8_MRF64=0)
-    and the fp32 oracle: wav cosine >= 0.999 between the two engines and >= 0.99 against the
-    oracle, the launch log showing which kernel ran.  Ragged: 3 clips, stage lengths not multiples of any tile."""
+@pytest.mark.parametrize("var,C,kern", [("M2S_F8_MRF64", 64, "gemm128_kernel<1, 4, 1, 4, 3>"),
+                                        ("M2S_F8_MRF32", 32, "gemm128_kernel<1, 4, 1, 2, 3>")])
+def test_fp8_mrf_narrow_e4m3(rt, monkeypatch, frames, var, C, kern):
+    """The C = 64 (M2S_F8_MRF64=1) and C = 32 (M2S_F8_MRF32=1) MRF stages on e4m3 in the fp8 vocoder (conv1d_f8 with
+    128 / C taps per 128-byte K step, a tap count not a multiple ending on zero taps) against the fused bf16
+    ResBlock1 (switch off, the default: faster at configs[4]) and the fp32 oracle: wav cosine >= 0.999 between the two engines and >= 0.99
+     against the oracle, the launch log showing which kernel ran.  Ragged: 3 clips, stage lengths
+    not multiples of any tile."""
     from m2s import _native
     sd = synth.synth_generator_state(5, HIFIGAN_H)
     mel = synth.synth_mel_log(3, 64, frames, seed=12)
-    monkeypatch.setenv("M2S_F8_MRF64", "1")
+    monkeypatch.setenv(var, "1")
     v8 = rt.VocoderEngine(sd, HIFIGAN_H, dtype="fp8", device=DEV)
-    monkeypatch.setenv("M2S_F8_MRF64", "0")
+    monkeypatch.setenv(var, "0")
     vb = rt.VocoderEngine(sd, HIFIGAN_H, dtype="fp8", device=DEV)
     x = torch.from_numpy(mel).to(DEV)
     out, names = {}, {}
@@ -320,11 +323,12 @@ def test_fp8_mrf64_e4m3(rt, monkeypatch, frames):
         torch.cuda.synchronize()
         names[key] = {r["name"] for r in _native.prof_launches()}
         _native.prof_enable(False)
-    assert "gemm128_kernel<1, 4, 1, 4, 3>" in names["f8"] and not any("rb1_fused_kernel<64" in n for n in names["f8"]), names["f8"]
-    assert any("rb1_fused_kernel<64" in n for n in names["bf16"]), names["bf16"]
+    fused = f"rb1_fused_kernel<{C},"
+    assert kern in names["f8"] and not any(fused in n for n in names["f8"]), names["f8"]
+    assert any(fused in n for n in names["bf16"]) and kern not in names["bf16"], names["bf16"]
     ref = hifigan.generator({k: torch.from_numpy(v) for k, v in sd.items()}, HIFIGAN_H, torch.from_numpy(mel)).numpy()
     for b in range(3):
         c2, cr = _cos(out["f8"][b], out["bf16"][b]), _cos(out["f8"][b], ref[b])
-        print(f"clip {b}: wav cos(e4m3 C=64, bf16 C=64) {c2:.6f}, vs oracle {cr:.6f}")
+        print(f"clip {b}: wav cos(e4m3 C={C}, bf16 C={C}) {c2:.6f}, vs oracle {cr:.6f}")
         assert np.isfinite(out["f8"][b]).all()
         assert c2 >= 0.999 and cr >= COS_MIN, (b, c2, cr)

@@ -8,7 +8,7 @@ VAR=${2:-variants/f16off}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_fp8.py -m gpu -x -v -s --timeout 200 --timeout-method thread -k "stride2 or mrf64" > "$OUT/pytest_new.log" 2>&1 \
+timeout -k 10 400 python -u -m pytest tests/test_gpu_fp8.py -m gpu -x -v -s --timeout 200 --timeout-method thread -k "stride2 or mrf_narrow" > "$OUT/pytest_new.log" 2>&1 \
   || { tail -40 "$OUT/pytest_new.log"; exit 1; }
 grep -E "passed|failed|cos" "$OUT/pytest_new.log" | tail -20 | cut -c1-200
 AB_DTYPE=fp8 AB_KERN=ir_pwdw AB_ROUNDS=2 timeout -k 10 300 python -u tools/ab_kern.py mri-to-speech_amd "$VAR" > "$OUT/ab.txt" 2>&1 \
@@ -20,7 +20,7 @@ bl() {  # bl <name> <dtype> [env...]
     --no-cpu-baseline --no-long > "$OUT/bench_$n.json" 2> "$OUT/bench_$n.err" || { tail -20 "$OUT/bench_$n.err"; return 1; }
   echo "$n $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['ms_per_step'], 'ms', d.get('parity'))" "$OUT/bench_$n.json" | cut -c1-300)"
 }
-bl fp8 fp8 && bl fp8_nos2 fp8 M2S_F8_S2=0 && bl fp8_nomrf64 fp8 M2S_F8_MRF64=0 && bl bf16 bf16 || exit 1
+bl fp8 fp8 && bl fp8_nos2 fp8 M2S_F8_S2=0 && bl fp8_nomrf64 fp8 M2S_F8_MRF64=0 && bl fp8_mrf32 fp8 M2S_F8_MRF32=1 && bl bf16 bf16 || exit 1
 timeout -k 10 500 python -u -m pytest tests/test_gpu_fp8.py tests/test_gpu_configs4.py -m gpu -x -v -s --timeout 200 --timeout-method thread -k "fp8" > "$OUT/pytest.log" 2>&1 \
   || { tail -40 "$OUT/pytest.log"; exit 1; }
 grep -E "passed|failed" "$OUT/pytest.log" | tail -3 | cut -c1-200
