@@ -466,6 +466,22 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
             a[2 * j] = dot2(in[t][j], w[t][2 * j], a[2 * j]);
             a[2 * j + 1] = dot2(in[t][j], w[t][2 * j + 1], a[2 * j + 1]);
           }
+        uint8_t* y8 = reinterpret_cast<uint8_t*>(y) + ((size_t)(n0 + g) * PO + p) * cs_mid + c;
+        if constexpr (F8) {  // saturated as silu_e4m3: min(x, 448) * sigmoid(x), NaN kept; the squeeze sums x * sigmoid(x)
+          float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int j = 0; j < NCH; ++j) {
+            const float gs = sigmoidf_(a[j]);
+            s[j] += a[j] * gs;
+            o[j] = fminf(a[j], 448.f) * gs;
+          }
+          const uint2 q = e4m3x8_nosat(o);  // 8 channels -> 8 bytes at byte (n, p, c) of the e4m3 map; 4 -> the first 4
+          if constexpr (NCH == 8)
+            reinterpret_cast<uint2*>(y8)[0] = q;
+          else
+            reinterpret_cast<uint32_t*>(y8)[0] = q.x;
+          continue;
+        }
         float v[NCH];
         uint32_t ow[NW2];
 #pragma unroll
@@ -476,13 +492,7 @@ __device__ __forceinline__ void ir_pwdw_body(const bf16_t* __restrict__ x, int c
           s[2 * j + 1] += v[2 * j + 1];
           ow[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
         }
-        uint8_t* y8 = reinterpret_cast<uint8_t*>(y) + ((size_t)(n0 + g) * PO + p) * cs_mid + c;
-        if constexpr (F8 && NCH == 8) {  // 8 channels -> 8 bytes at byte (n, p, c) of the e4m3 map
-          reinterpret_cast<uint2*>(y8)[0] = e4m3x8(v);
-        } else if constexpr (F8) {  // 4 channels -> 4 bytes (the first half of e4m3x8: the same bytes)
-          const int r = __builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v[0]), sat_e4m3(v[1]), 0, false);
-          reinterpret_cast<uint32_t*>(y8)[0] = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v[2]), sat_e4m3(v[3]), r, true);
-        } else if constexpr (NCH == 8) {
+        if constexpr (NCH == 8) {
           *reinterpret_cast<uint4*>(yi + (size_t)p * cs_mid) = make_uint4(ow[0], ow[NW2 > 1 ? 1 : 0], ow[NW2 > 2 ? 2 : 0], ow[NW2 > 3 ? 3 : 0]);
         } else {
           *reinterpret_cast<uint2*>(yi + (size_t)p * cs_mid) = make_uint2(ow[0], ow[NW2 > 1 ? 1 : 0]);

@@ -157,16 +157,25 @@ __global__ void __launch_bounds__(256, 3)
         a[0] += w[t][0] * u0.x; a[1] += w[t][1] * u0.y; a[2] += w[t][2] * u0.z; a[3] += w[t][3] * u0.w;
         a[4] += w[t][4] * u1.x; a[5] += w[t][5] * u1.y; a[6] += w[t][6] * u1.z; a[7] += w[t][7] * u1.w;
       }
+      const long pix = ((long)n * OH + oy0 + oyl) * OW + ox;
+      if constexpr (F8) {  // 8 channels -> 8 e4m3 bytes at byte (pix, c) of the (N, OH*OW, cs_mid) map
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {  // saturated as silu_e4m3: min(x, 448) * sigmoid(x), NaN kept
+          const float g = sigmoidf_(a[j]);
+          s[j] += a[j] * g;  // the squeeze sums the unsaturated values
+          o[j] = fminf(a[j], 448.f) * g;
+        }
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(y) + pix * cs_mid + c0 + cg * 8) = e4m3x8_nosat(o);
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         a[j] = silu(a[j]);
         s[j] += a[j];
       }
-      const long pix = ((long)n * OH + oy0 + oyl) * OW + ox;
       if constexpr (SP) {
         il_st8(ys, pix, cs_mid, c0 + cg * 8, a);
-      } else if constexpr (F8) {  // 8 channels -> 8 e4m3 bytes at byte (pix, c) of the (N, OH*OW, cs_mid) map
-        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(y) + pix * cs_mid + c0 + cg * 8) = e4m3x8(a);
       } else {
         *reinterpret_cast<uint4*>(y + pix * cs_mid + c0 + cg * 8) =
             make_uint4(pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(a[4], a[5]), pack_bf16x2(a[6], a[7]));

@@ -547,11 +547,21 @@ size_t Acoustic::effnet_x8(int H, int W) const {
   return round_up((int)mx, 256);
 }
 
+// Frames per CNN pass: `chunk`, or, where one pass fewer of at most chunk + chunk / 16 frames covers N, that
+// (8 x 1000 frames: 4 passes of 2000 instead of 4 x 1920 + a 320-frame tail, which fills the persistent
+// kernels' one-workgroup-per-CU grids for under two of their rounds).  Every pass is exact (per-frame work), so
+// the split never changes a result (test_effnet_chunking_is_exact).
+int Acoustic::pass_frames(int N) const {
+  if (N <= chunk) return N;
+  const int n = ceil_div(N, chunk), even = ceil_div(N, n - 1);
+  return even <= chunk + chunk / 16 ? even : chunk;
+}
+
 size_t Acoustic::effnet_ws(int N, int H, int W) const {
   size_t io, mid, se;
   effnet_dims(H, W, &io, &mid, &se);
   const size_t es = act_bytes(dtype_);
-  const size_t nc = std::min(N, chunk);
+  const size_t nc = pass_frames(N);
   Workspace ws(nullptr, 0);
   ws.take<char>(nc * io * es);
   ws.take<char>(nc * io * es);
@@ -595,7 +605,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
   M2S_CHECK(N > 0 && H >= 32 && W >= 32, "effnet: bad input size");
   size_t io, mid, se;
   effnet_dims(H, W, &io, &mid, &se);
-  const int nc_max = std::min(N, chunk);
+  const int nc_max = pass_frames(N);
   constexpr int R = Elem<T>::R;  // split fp32: hi + lo planes
   T* A = ws.take<T>((size_t)nc_max * io * R);
   T* Bb = ws.take<T>((size_t)nc_max * io * R);

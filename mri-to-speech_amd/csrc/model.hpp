@@ -164,6 +164,7 @@ class Acoustic {
   void effnet_t(const float* frames, int N, int H, int W, float* feats, int stop_after, float* probe, int* probe_dims,
                 Workspace& ws, hipStream_t s);
   size_t effnet_ws(int N, int H, int W) const;
+  int pass_frames(int N) const;
   size_t effnet_x8(int H, int W) const;  // fp8 engines: bytes per image of an e4m3 expand-operand buffer
   void effnet_dims(int H, int W, size_t* io_elems, size_t* mid_elems, size_t* se_elems) const;
 

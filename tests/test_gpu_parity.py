@@ -164,6 +164,10 @@ def test_effnet_chunking_is_exact(rt, ac_state):
     ref_eng = rt.AcousticEngine(ac_state[1], dtype="fp32", device=DEV, chunk=256)
     fr = torch.from_numpy(synth.synth_frames(1, 5, seed=12)[0]).to(DEV)
     assert torch.equal(eng.effnet(fr), ref_eng.effnet(fr))
+    # 33 frames at chunk 16: two passes of 17 (one pass fewer of <= chunk + chunk / 16 frames) instead of 16, 16, 1
+    eng16 = rt.AcousticEngine(ac_state[1], dtype="fp32", device=DEV, chunk=16)
+    fr = torch.from_numpy(synth.synth_frames(1, 33, seed=13)[0]).to(DEV)
+    assert torch.equal(eng16.effnet(fr), ref_eng.effnet(fr))
 
 
 def test_effnet_bf16_close(ac_bf16, ac_state):

@@ -7,7 +7,7 @@ VAR=${2:-variants/f16off}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-AB_DTYPE=fp8 AB_KERN=ir_pwdw AB_ROUNDS=2 timeout -k 10 300 python -u tools/ab_kern.py mri-to-speech_amd "$VAR" > "$OUT/ab.txt" 2>&1 \
+AB_DTYPE=fp8 AB_KERN=${AB_KERN:-ir_pwdw} AB_ROUNDS=2 timeout -k 10 300 python -u tools/ab_kern.py mri-to-speech_amd "$VAR" > "$OUT/ab.txt" 2>&1 \
   || { tail -30 "$OUT/ab.txt"; exit 1; }
 cat "$OUT/ab.txt" | cut -c1-400
 timeout -k 10 500 python -u -m pytest tests/test_gpu_fp8.py tests/test_gpu_configs4.py -m gpu -x -v -s --timeout 200 --timeout-method thread -k "fp8" > "$OUT/pytest.log" 2>&1 \
