@@ -58,10 +58,11 @@ PRECISION = {
     "bf16": "bf16 storage and operands, fp32 accumulate; BiLSTM recurrence 3-term split products (B > 4), "
             "input projection/head/glue fp32",
     "fp8": "e4m3 storage + block-scaled e4m3 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, per-output-channel "
-           "weight scales) for the stride-1 IR blocks' expand, expanded maps and SE-gated conv_pwl GEMMs, the "
-           "EdgeResidual blocks.1.1/.2 and blocks.2.1/.2 (conv_exp + conv_pwl) and the C=128/256 MRF convs; the other "
-           "convs (stem, stride-2 EdgeResidual blocks.1.0/2.0 and IR blocks.3.0/5.0, IR depthwise, C=32/64 MRF, "
-           "upsamplers) bf16; BiLSTM recurrence 3-term split products (B > 4), input projection/head/glue fp32",
+           "weight scales) for the IR blocks' expand (stride 1 and blocks.5.0), expanded maps and SE-gated conv_pwl "
+           "GEMMs (all IR blocks), the EdgeResidual blocks.1.1/.2 and blocks.2.1/.2 (conv_exp + conv_pwl) and the "
+           "C=128/256 MRF convs; the other convs (stem, stride-2 EdgeResidual blocks.1.0/2.0, blocks.3.0 expand, IR "
+           "depthwise on f16 / fp32 accumulation, C=32/64 MRF, upsamplers) bf16; BiLSTM recurrence 3-term split "
+           "products (B > 4), input projection/head/glue fp32",
 }
 
 MFMA_KERNELS = ("conv_gemm_kernel", "gemm128_kernel", "conv_halo_kernel", "conv1d_halo", "conv_igemm_kernel", "ir_pwdw",

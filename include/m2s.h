@@ -53,12 +53,14 @@ enum m2s_status { M2S_OK = 0, M2S_E_ARG = 1, M2S_E_HIP = 2, M2S_E_STATE = 3, M2S
  *                 accumulation; meets the fp32 tolerances of the parity tests
  *   M2S_DT_FP8    configs[4]: OCP e4m3 storage and block-scaled e4m3 MFMA
  *                 (v_mfma_scale_f32_16x16x128_f8f6f4, unit E8M0 block scales, per-output-channel
- *                 fp32 weight scales applied in the epilogue) for: the stride-1 IR blocks' conv_pw
- *                 expand, expanded maps and SE-gated conv_pwl GEMMs; the EdgeResidual blocks.1.1/.2
- *                 and blocks.2.1/.2 (conv_exp + conv_pwl); the C = 128 / 256 MRF convs.  The stem,
- *                 the stride-2 blocks (EdgeResidual blocks.1.0 / 2.0, IR blocks.3.0 / 5.0), the IR
- *                 depthwise convs (fp32 accumulation of a bf16 tile), the C = 32 / 64 MRF convs and
- *                 the upsamplers run the bf16 path */
+ *                 fp32 weight scales applied in the epilogue) for: the IR blocks' conv_pw expand
+ *                 (stride 1 and blocks.5.0), expanded maps and SE-gated conv_pwl GEMMs (every IR
+ *                 block, blocks.3.0 / 5.0 included); the EdgeResidual blocks.1.1/.2 and blocks.2.1/.2
+ *                 (conv_exp + conv_pwl); the C = 128 / 256 MRF convs (C = 64 / 32 on request:
+ *                 M2S_F8_MRF64 / M2S_F8_MRF32, slower than the fused bf16 ResBlock1).  The stem, the
+ *                 stride-2 EdgeResidual blocks.1.0 / 2.0, the blocks.3.0 expand, the IR depthwise convs
+ *                 (f16 or fp32 accumulation of a 16-bit tile), the C = 32 / 64 MRF convs and the
+ *                 upsamplers run the bf16 path */
 enum m2s_dtype { M2S_DT_F32 = 0, M2S_DT_BF16 = 1, M2S_DT_BF16X3 = 2, M2S_DT_FP8 = 3 };
 /* host tensor element types */
 enum m2s_elem { M2S_ELEM_F32 = 0, M2S_ELEM_I64 = 1 };
