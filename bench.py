@@ -48,9 +48,9 @@ PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "bf16x3": 2500.0 / 3,
                # e4m3 on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4: 2x bf16 (MI355X_MICROARCH.md)
                "fp8": 5000.0}
 PEAK_HBM_GBS = 8000.0
-FP32_TOL = {"mel_norm": 1e-4, "mel_log": 5e-4, "wav": 2e-4}  # tests/test_gpu_configs.py
+FP32_TOL = {"mel_norm": 1e-4, "mel_log": 5e-4, "wav": 1e-4}  # tests/test_gpu_configs.py; wav: SURVEY.md §8(c)
 # 1000-frame clips: fp32 summation order over 1000 recurrent steps (tests/test_gpu_configs4.py)
-LONG_TOL = {"mel_norm": 2e-4, "mel_log": 1e-3, "wav": 2e-4}
+LONG_TOL = {"mel_norm": 2e-4, "mel_log": 1e-3, "wav": 1e-4}
 PRECISION = {
     "bf16x3": "split fp32: bf16 hi+lo pairs (17-bit), 3 bf16 MFMA terms per product, fp32 accumulate; "
               "BiLSTM recurrence 3-term split products (lstm_x3, B > 4), input projection/head/glue fp32",
@@ -552,6 +552,10 @@ def roofline(launches, dtype, steps, fps, frames_per_step, stages=False):
         "kernel": dom["name"], "arith": ar, "launches_per_step": dom["launches"] // steps,
         "avg_launch_us": round(1000.0 * dom["ms"] / dom["launches"], 2),
         "algorithmic_bytes_per_launch": round(dom["bytes"] / dom["launches"]),
+        # an intermediate the kernel writes only for the next kernel of the same operation to read back (ir_ws: the
+        # IR block's expanded depthwise map, read by the SE-gated conv_pwl; include/m2s.h spill_bytes): HBM traffic
+        # the PMC record sees, not compulsory bytes, so not in `achieved` nor in the roof choice
+        "spill_bytes_per_launch": round(dom.get("spill_bytes", 0.0) / dom["launches"]),
         "algorithmic_flop_per_launch": round(dom["flops"] / dom["launches"]),
         "kernel_share_of_gpu_time": round(dom["ms"] / tot_ms, 3),
         "all_mfma_kernels_tflops": round(mm_fl / (mm_ms * 1e-3) / 1e12, 2),
@@ -561,8 +565,12 @@ def roofline(launches, dtype, steps, fps, frames_per_step, stages=False):
     }
     r["traffic_source"] = tsrc or f"no PMC record of source {sha} in profiles/ (tools/gpu_evidence.sh)"
     r["src_sha"] = sha
-    r["bytes_note"] = ("algorithmic bytes on the real channel counts (block input + output + weights, 4 B an element in "
-                       "split fp32), not the padded channel strides of the layout")
+    r["bytes_note"] = ("algorithmic bytes on the real channel counts (compulsory: the operation's input + output + weights, "
+                       "4 B an element in split fp32), not the padded channel strides of the layout; spilled intermediates "
+                       "are spill_bytes_per_launch; bound = the roof the algorithmic intensity (flop / compulsory byte) meets "
+                       "first")
+    if traffic:
+        r["traffic_over_compulsory_plus_spill"] = round(traffic / max(r["algorithmic_bytes_per_launch"] + r["spill_bytes_per_launch"], 1), 3)
     if stages:
         r.update(stage_table(launches, steps))
     return r

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define M2S_ABI_VERSION 5
+#define M2S_ABI_VERSION 6
 
 enum m2s_status { M2S_OK = 0, M2S_E_ARG = 1, M2S_E_HIP = 2, M2S_E_STATE = 3, M2S_E_NODEV = 4, M2S_E_INTERNAL = 5 };
 /* compute dtype of the convolution stacks.  The BiLSTM input projection, head and glue run in fp32 in every
@@ -89,7 +89,9 @@ typedef struct m2s_acoustic m2s_acoustic;
 int m2s_acoustic_create(const m2s_tensor* sd, int n, int n_mels, int rnn_hidden, int dtype, int device,
                         m2s_acoustic** out);
 void m2s_acoustic_destroy(m2s_acoustic* m);
-/* frames per CNN pass (bounds the CNN workspace); default 1920 (= m2s.config.CNN_CHUNK, the size bench.py times) */
+/* frames per CNN pass (bounds the CNN workspace); default 1920 (= m2s.config.CNN_CHUNK, the size bench.py times).
+ * A pass may hold up to chunk + chunk / 16 frames where one pass fewer then covers N (no short tail pass), so
+ * the workspace and the kernels' size checks see up to ~6 % more frames than `frames`. */
 int m2s_acoustic_set_chunk(m2s_acoustic* m, int frames);
 /* Asynchronous failure report.  The persistent BiLSTM waits at a grid barrier once per time step, and
  * the persistent CNN kernels (ir_ws, se_ws) at LDS flags between their producer and consumer waves;
@@ -218,13 +220,17 @@ int m2s_prof_enable(int on);
 int m2s_prof_collect(m2s_prof_stat* out, int max, int* n_out);
 /* One recorded launch, in launch order: its kernel name, the stage of the path it belongs to
  * ("cnn", "bilstm", "head", "glue", "voc_pre", "ups_c<C>", "mrf_c<C>", "voc_post"; bench.py's
- * roofline.stages), event time, algorithmic FLOPs and bytes. */
+ * roofline.stages), event time, algorithmic FLOPs and bytes (compulsory in + out + weights of the
+ * operation the kernel implements), and spill_bytes: an intermediate map the kernel writes only for a
+ * later kernel of the same operation to read back (ir_ws: the IR block's expanded depthwise map, which
+ * the SE-gated conv_pwl reads; ABI 6), counted once, not part of `bytes`. */
 typedef struct m2s_prof_launch {
   char name[96];
   char stage[24];
   double ms;
   double flops;
   double bytes;
+  double spill_bytes;
 } m2s_prof_launch;
 /* Synchronises on the recorded events, writes up to `max` launches in launch order (*n_out = all of
  * them), clears the record.  out == NULL: *n_out = the number recorded, the record stays. */

@@ -16,6 +16,8 @@
 #include "conv_igemm.hpp"
 
 #include <cstring>
+#include <map>
+#include <mutex>
 
 #include "prof.hpp"
 
@@ -151,7 +153,8 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * ROW + ((ch
 // hi*hi + hi*lo + lo*hi (the dropped lo*lo term is below 2^-16 of the product).
 // SP = 2: e4m3 operands over bf16 storage (conv_igemm.hpp launch_conv_gemm, a.wscale).
 template <int BM, int BN, int MT, int NT, int S, int KIND, int XF, int SP>
-__global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 2 : 1)) conv_gemm_kernel(const ConvBatch ab, int n_tiles, int se_imgs) {
+__global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 2 : 1)) conv_gemm_kernel(const ConvBatch ab, int n_tiles, int se_imgs,
+                                                                                                      float* __restrict__ kpart) {
   // KIND_CONV1D launches may batch convs of one shape over grid.z (launch_conv_gemm_batch)
   const ConvArgs a = ab.a[KIND == KIND_CONV1D ? blockIdx.z : 0];  // a copy: fields land in SGPRs once, not re-loaded per K step
   constexpr int WN = BN / (NT * 16);
@@ -184,7 +187,11 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
   const bf16_t* __restrict__ X = static_cast<const bf16_t*>(a.x);
   const bf16_t* __restrict__ W = static_cast<const bf16_t*>(a.w) + (size_t)phase * a.n_pad * a.kp * R;
   const int xs = a.cs_in * R;  // elements per input position
-  const int nsteps = a.kp / 32;
+  // split K (grid.y > 1, small grids: launch_tile): this workgroup runs K steps [kb, kb + nsteps) of its tile and
+  // stores fp32 partial sums to kpart; conv_gemm_ksum_kernel adds them in split order and runs the epilogue
+  const int nks = gridDim.y, ks = blockIdx.y;
+  const int kb = (a.kp / 32) * ks / nks;
+  const int nsteps = (a.kp / 32) * (ks + 1) / nks - kb;
 
   // ---- DMA roles: lane -> (row within a 16-row block, physical chunk) -------------------------
   // Per A row the geometry is resolved once: `rbase` = element offset of the row's tap-0 input
@@ -235,7 +242,8 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
     rmask[j] = ok ? msk : 0u;
   }
   // this lane's tap and channel within the current K step, and the tap's input offset
-  int s_tap = (q * 8) / a.cs_in, s_c = (q * 8) % a.cs_in;
+  // (K step kb's element offset: cs_in >= 32 is a multiple of 32, smaller cs_in divide 32)
+  int s_tap = (kb * 32 + q * 8) / a.cs_in, s_c = (kb * 32 + q * 8) % a.cs_in;
   const int row_stride = a.IW * xs;  // CONV2D: one input row
   auto tap_off = [&](int t) -> int {
     if constexpr (KIND == KIND_CONV2D) return (t / 3) * row_stride + (t - (t / 3) * 3) * xs;
@@ -397,7 +405,7 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
       for (int ni = 0; ni < NT; ++ni) {
         const int m = m0 + wm * MT * 16 + mi * 16 + r16, n4 = n0 + wn * NT * 16 + ni * 16 + 4 * g;
         pres[mi][ni][0] = pres[mi][ni][1] = make_uint2(0u, 0u);
-        if (R0 && m < a.M && n4 < a.cs_out) {
+        if (R0 && nks == 1 && m < a.M && n4 < a.cs_out) {
           const size_t orow = (size_t)m * a.cs_out * 2;
           pres[mi][ni][0] = *reinterpret_cast<const uint2*>(R0 + orow + n4);
           pres[mi][ni][1] = *reinterpret_cast<const uint2*>(R0 + orow + a.cs_out + n4);
@@ -454,34 +462,51 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // visible at the next barrier
     };
-    issue(0, 0);
+    if (nsteps > 0) issue(kb, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the SE table stores
-    for (int st = 0; st < nsteps; ++st) {
+    for (int i = 0; i < nsteps; ++i) {
       wait_vm<0>();
-      __builtin_amdgcn_s_barrier();  // st landed everywhere; slot (st + 1) % 2 free
-      if (st + 1 < nsteps) issue(st + 1, (st + 1) % 2);
-      scale_slot(st, st % 2);
+      __builtin_amdgcn_s_barrier();  // step i landed everywhere; slot (i + 1) % 2 free
+      if (i + 1 < nsteps) issue(kb + i + 1, (i + 1) % 2);
+      scale_slot(kb + i, i % 2);
       __builtin_amdgcn_s_barrier();
-      compute(st, st % 2);
+      compute(kb + i, i % 2);
     }
   } else {
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
-    if (s < nsteps) issue(s, s);
+    if (s < nsteps) issue(kb + s, s);
 
-  for (int st = 0; st < nsteps; ++st) {
-    // stage st has landed once at most min(S-2, nsteps-1-st) younger stages are outstanding
-    const int younger = min(S - 2, nsteps - 1 - st);
+  for (int i = 0; i < nsteps; ++i) {
+    // step i has landed once at most min(S-2, nsteps-1-i) younger steps are outstanding
+    const int younger = min(S - 2, nsteps - 1 - i);
     if (younger >= 2)
       wait_vm<2 * PER_STAGE>();
     else if (younger == 1)
       wait_vm<PER_STAGE>();
     else
       wait_vm<0>();
-    __builtin_amdgcn_s_barrier();  // every wave's DMA for `st` landed; slot (st-1)%S is free
-    if (st + S - 1 < nsteps) issue(st + S - 1, (st + S - 1) % S);
-    compute(st, st % S);
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for step i landed; slot (i-1)%S is free
+    if (i + S - 1 < nsteps) issue(kb + i + S - 1, (i + S - 1) % S);
+    compute(kb + i, i % S);
   }
+  }
+
+  if (nks > 1) {  // split K: raw fp32 partial sums [z][ks][M][cs_out], the epilogue runs in conv_gemm_ksum_kernel
+    float* __restrict__ P = kpart + ((size_t)blockIdx.z * nks + ks) * a.M * a.cs_out;
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) {
+      const int m = m0 + wm * MT * 16 + mi * 16 + r16;
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) {
+        const int n4 = n0 + wn * NT * 16 + ni * 16 + 4 * g;
+        if (n4 < a.cs_out)
+          *reinterpret_cast<float4*>(P + (size_t)m * a.cs_out + n4) =
+              make_float4(acc[ni][mi][0], acc[ni][mi][1], acc[ni][mi][2], acc[ni][mi][3]);
+      }
+    }
+    return;
   }
 
   // ---- epilogue: 4 consecutive channels of one position per lane ------------------------------
@@ -581,6 +606,124 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
   }
 }
 
+// Split-K epilogue: the partial sums of the nks K ranges added in split order (deterministic), then the main
+// kernel's epilogue (bias / e4m3 weight scale, activation, residual, MRF accumulation, bf16 or split store);
+// lane = 4 consecutive channels of one output position, grid.z = the main launch's grid.z.
+template <int KIND, int SP>
+__global__ void __launch_bounds__(256) conv_gemm_ksum_kernel(const ConvBatch ab, const float* __restrict__ kpart, int nks) {
+  const ConvArgs a = ab.a[KIND == KIND_CONV1D ? blockIdx.z : 0];
+  constexpr int R = SP == 1 ? 2 : 1;
+  const int nq = a.cs_out / 4;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)a.M * nq) return;
+  const int m = (int)(i / nq), n4 = (int)(i - (long)m * nq) * 4;
+  const size_t plane = (size_t)a.M * a.cs_out;
+  const float* p = kpart + (size_t)blockIdx.z * nks * plane + (size_t)m * a.cs_out + n4;
+  float4 acc = *reinterpret_cast<const float4*>(p);
+  for (int k = 1; k < nks; ++k) {
+    const float4 t = *reinterpret_cast<const float4*>(p + k * plane);
+    acc.x += t.x;
+    acc.y += t.y;
+    acc.z += t.z;
+    acc.w += t.w;
+  }
+  long orow = m;
+  if constexpr (KIND == KIND_CONVT) {
+    const int b = m / a.L_in, qq = m - (m / a.L_in) * a.L_in;
+    orow = (long)b * a.L_out + (long)qq * a.ct_u + blockIdx.z;
+  }
+  orow *= (long)a.cs_out * R;
+  const float4 bb = *reinterpret_cast<const float4*>(a.bias + n4);
+  float v[4] = {acc.x + bb.x, acc.y + bb.y, acc.z + bb.z, acc.w + bb.w};
+  if constexpr (SP == 2) {
+    const float4 ws = *reinterpret_cast<const float4*>(a.wscale + n4);
+    v[0] = fmaf(acc.x, ws.x, bb.x);
+    v[1] = fmaf(acc.y, ws.y, bb.y);
+    v[2] = fmaf(acc.z, ws.z, bb.z);
+    v[3] = fmaf(acc.w, ws.w, bb.w);
+  }
+  auto apply_act = [&]() {
+    if (a.act == ACT_SILU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = silu(v[j]);
+    } else if (a.act == ACT_LRELU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * a.act_slope;
+    } else if (a.act == ACT_SIGMOID) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = sigmoidf_(v[j]);
+    }
+  };
+  if (!a.act_after_res) apply_act();
+  bf16_t* __restrict__ Y = static_cast<bf16_t*>(a.y);
+  const bf16_t* __restrict__ Rs = static_cast<const bf16_t*>(a.res);
+  if (Rs) {
+    float r[4];
+    ld4f(Rs + orow + n4, r);
+    if constexpr (SP == 1) {
+      float rl[4];
+      ld4f(Rs + orow + a.cs_out + n4, rl);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] += rl[j];
+    }
+    if (a.res_unslope != 0.f) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = r[j] > 0.f ? r[j] : r[j] * a.res_unslope;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += r[j];
+  }
+  if (a.accum) {
+    float pv[4];
+    ld4f(Y + orow + n4, pv);
+    if constexpr (SP == 1) {
+      float pl[4];
+      ld4f(Y + orow + a.cs_out + n4, pl);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pv[j] += pl[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = pv[j] + v[j];
+    if (a.accum == 2) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = v[j] / a.accum_div;
+    }
+  }
+  if (a.act_after_res) apply_act();
+  if constexpr (SP == 1) {
+    uint2 hi, lo;
+    split4(v, hi, lo);
+    *reinterpret_cast<uint2*>(Y + orow + n4) = hi;
+    *reinterpret_cast<uint2*>(Y + orow + a.cs_out + n4) = lo;
+  } else {
+    uint2 u;
+    u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    *reinterpret_cast<uint2*>(Y + orow + n4) = u;
+  }
+}
+
+// Split-K partial sums live in one device buffer per (device, stream), grown on demand (only small grids split,
+// so it stays a few MB); launches on one stream are ordered, so one buffer per stream is race-free.
+float* ksplit_scratch(hipStream_t s, size_t bytes) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> bufs;
+  int dev = 0;
+  M2S_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(mu);
+  auto& b = bufs[{dev, s}];
+  if (b.second < bytes) {
+    if (b.first) {
+      M2S_HIP(hipStreamSynchronize(s));  // the old buffer may still be read by queued launches
+      M2S_HIP(hipFree(b.first));
+    }
+    const size_t sz = (bytes + (16u << 20) - 1) / (16u << 20) * (16u << 20);
+    M2S_HIP(hipMalloc(&b.first, sz));
+    b.second = sz;
+  }
+  return static_cast<float*>(b.first);
+}
+
 const char* kname(int k) {
   switch (k) {
     case KIND_CONV2D: return "conv2d";
@@ -609,15 +752,42 @@ void launch_tile(const ConvBatch& b, hipStream_t s, int phases, double flops, do
   }
   const size_t lds = (size_t)S * (R * (BM + BN) + 16) * ROW + (size_t)se_imgs * a.cs_in * sizeof(float);
   M2S_CHECK(lds <= 160 * 1024, "conv_gemm: LDS budget");
-  dim3 grid(m_tiles * n_tiles, 1, phases);
+  // Split K where the tiles fill under half a round of the chip's workgroup slots (one clip, the 8 x 4 acoustic
+  // batch: a few dozen tiles walking 20..88 K steps each): nks K ranges of >= 4 steps, up to a full round.
+  // M2S_KSPLIT=n forces n ranges (A/B, tests; 1 = never split).
+  int nst = 0;
+  for (int i = 0; i < (KIND == KIND_CONV1D ? phases : 1); ++i) nst = std::max(nst, b.a[i].kp / 32);
+  const int tiles = m_tiles * n_tiles * phases;
+  const int slots = device_cus() * std::max(1, std::min(2, (int)(160 * 1024 / lds)));
+  const char* fe = getenv("M2S_KSPLIT");  // read per launch: tests switch it between engines of one process
+  const int force = fe ? atoi(fe) : 0;
+  int nks = 1;
+  if (force > 0)
+    nks = std::min(force, std::max(1, nst));
+  else if (2 * tiles <= slots && nst >= 8)
+    nks = std::max(1, std::min({slots / tiles, nst / 4, 16}));
+  const size_t part_bytes = (size_t)phases * nks * a.M * a.cs_out * sizeof(float);
+  if (nks > 1 && part_bytes > ((size_t)256 << 20)) nks = 1;
+  float* kpart = nks > 1 ? ksplit_scratch(s, part_bytes) : nullptr;
+  dim3 grid(m_tiles * n_tiles, nks, phases);
   char name[96];
   static const bool detail = getenv("M2S_PROF_DETAIL") != nullptr;
   if (detail)  // per-layer records for analysis: K x N and rows per launch
     snprintf(name, sizeof(name), "conv_gemm<%s,%dx%d%s> K%d N%d M%d", kname(KIND), BM, BN, SP == 1 ? ",x3" : SP == 2 ? ",e4m3" : "", a.kp, a.cs_out, a.M);
   else
     snprintf(name, sizeof(name), "conv_gemm_kernel<%d, %d, %d, %d, %d, %d, %d, %d>", BM, BN, MT, NT, S, KIND, XF, SP);
-  ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF, SP>), grid, dim3(256), lds, s, b, n_tiles, se_imgs);
+  {
+    ProfScope ps(name, flops, bytes, s);
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF, SP>), grid, dim3(256), lds, s, b, n_tiles, se_imgs, kpart);
+  }
+  if (nks > 1) {
+    // the partial sums are a spill (written and read back once), not compulsory bytes
+    snprintf(name, sizeof(name), "conv_gemm_ksum_kernel<%d, %d>", KIND, SP);
+    ProfScope ps(name, 0.0, 0.0, s, 2.0 * part_bytes);
+    const long threads = (long)a.M * (a.cs_out / 4);
+    hipLaunchKernelGGL((conv_gemm_ksum_kernel<KIND, SP>), dim3((unsigned)((threads + 255) / 256), 1, phases), dim3(256), 0, s, b,
+                       kpart, nks);
+  }
 }
 
 template <int KIND, int XF, int SP>

@@ -94,8 +94,9 @@ __host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mi
   L.x_bytes = L.XR * W * xp;
   L.tile_bytes = 2 * 8 * L.TROWS * 16;
   L.w_bytes = 2 * (cs_in / 32) * 4096;
-  // taps + biases, the squeeze's fixed-point channel sums [cs_mid] (u64) and arrival counts [cs_mid / 32], counters
-  L.total = L.x_bytes + L.tile_bytes + L.w_bytes + (3 * 320 + 2 * 32) * 4 + cs_mid * 8 + (cs_mid / WS_SL) * 4 + 128;
+  // taps + biases, the squeeze's fixed-point channel sums [cs_mid] (u64), arrival counts and NaN flags [cs_mid / 32],
+  // counters
+  L.total = L.x_bytes + L.tile_bytes + L.w_bytes + (3 * 320 + 2 * 32) * 4 + cs_mid * 8 + 2 * (cs_mid / WS_SL) * 4 + 128;
   return L;
 }
 
@@ -161,6 +162,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   // number of (band, wave) arrivals, whose last one turns the sums into the slice's SE means
   unsigned long long* sq = reinterpret_cast<unsigned long long*>(bpl + 2 * 32);  // [cs_mid]
   unsigned* sq_n = reinterpret_cast<unsigned*>(sq + cs_mid);                      // [NS]
+  unsigned* sq_nan = sq_n + cs_mid / WS_SL;  // [NS] a non-finite partial reached the slice's sums: its means are NaN
   // The hand-offs that replace the per-slice barrier, in LDS.  Producer events are shared monotonic counters
   // (one add per producer wave and event): a producer adds slice f + 1's count only after a wait that needed
   // every producer's slice-f add, so "counter >= NP x k" cannot be met by one wave running ahead.  Consumers are
@@ -210,7 +212,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
 
   if (tid < 32) ctr[tid] = 0u;  // ordered before any use by the kernel's one barrier
   for (int i = tid; i < cs_mid; i += 64 * (WS_NP + WS_NC)) sq[i] = 0ull;
-  for (int i = tid; i < NS; i += 64 * (WS_NP + WS_NC)) sq_n[i] = 0u;
+  for (int i = tid; i < 2 * NS; i += 64 * (WS_NP + WS_NC)) sq_n[i] = 0u;  // counts and NaN flags
   // the tiles' halo columns are zero for good (the producers write only interior columns)
   for (int i = tid; i < 2 * 8 * Lg.TROWS; i += 64 * (WS_NP + WS_NC)) {
     const int pl = i / Lg.TROWS, r = i - pl * Lg.TROWS, c = r % WT;
@@ -568,18 +570,29 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     {
       const int j = (lane >> 3) & 3;
       const float v = j == 0 ? s[0] : j == 1 ? s[1] : j == 2 ? s[2] : s[3];
+      // a non-finite partial (an upstream NaN, or |v| >= 2^31 where the 32.32 conversion is undefined) cannot be
+      // carried in fixed point: it flags the image's slice, whose SE means the last arriver stores as NaN (as the
+      // float sum propagated it)
+      if (lane < WS_SL && !(__builtin_fabsf(v) < 2147483648.0f))
+        asm volatile("ds_write_b32 %0, %1" ::"v"((uint32_t)(uintptr_t)(sq_nan + d.sl)), "v"(1u) : "memory");
       if (lane < WS_SL)
-        __hip_atomic_fetch_add(sq + c0 + sc, (unsigned long long)(long long)(v * 4294967296.0f), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(sq + c0 + sc, (unsigned long long)(long long)(__builtin_fabsf(v) < 2147483648.0f ? v * 4294967296.0f : 0.f),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    // the arrival count is release (this wave's sum adds and poison write are ordered before it) and acquire (the last
+    // arriver sees every other wave's adds before it reads the sums): the memory model's ordering, not LDS's in-order
+    // execution of one wave's operations
     unsigned arrived = 0;
-    if (lane == 0) arrived = __hip_atomic_fetch_add(sq_n + d.sl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) arrived = __hip_atomic_fetch_add(sq_n + d.sl, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (__builtin_amdgcn_readfirstlane(arrived) == (unsigned)(NB * WS_NC - 1) && lane < WS_SL) {
       const unsigned long long t = __hip_atomic_exchange(sq + c0 + sc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       // 32.32 -> float: integer part (arithmetic high word) + fraction (low word)
       const float m = __fmaf_rn((float)(unsigned)t, 2.3283064365386963e-10f, (float)(int)(t >> 32)) / (float)PO;
-      act_st<sp_t>(reinterpret_cast<sp_t*>(se_mean), d.img, cs_mid, c0 + sc, *poison ? __builtin_nanf("") : m);
-      if (lane == 0) sq_n[d.sl] = 0u;
+      act_st<sp_t>(reinterpret_cast<sp_t*>(se_mean), d.img, cs_mid, c0 + sc, (*poison || sq_nan[d.sl]) ? __builtin_nanf("") : m);
+      if (lane == 0) {
+        sq_n[d.sl] = 0u;
+        sq_nan[d.sl] = 0u;
+      }
     }
   };
 
@@ -717,7 +730,9 @@ bool ir_ws_s2_supported(int H, int W, int cs_in, int kp, int cs_mid, int OH, int
 
 bool ir_ws_supported(int H, int W, int cs_in, int kp, int cs_mid) {
   if (!((W == 8 && (kp == 128 || kp == 224)) || (W == 16 && kp == 128)) || H < 1 || H > 64 || cs_in != kp) return false;
-  if (cs_mid % WS_SL != 0 || cs_mid < WS_SL) return false;
+  // the atomic squeeze keeps one sums / count set per workgroup, reused across bands and images: consumer waves
+  // may run two slices apart, so a slice index must not recur within three steps (NS = cs_mid / 32 >= 3)
+  if (cs_mid % WS_SL != 0 || cs_mid < 3 * WS_SL) return false;
   const WsLayout L = ws_layout(H, W, cs_in, cs_mid);
   const int cpr = 2 * ws_cpp(cs_in);
   return L.total <= 160 * 1024 && (L.XR * W * cpr) % 64 == 0 && L.XR * W * cpr / 64 / WS_NP + 1 <= 60 &&
@@ -726,7 +741,7 @@ bool ir_ws_supported(int H, int W, int cs_in, int kp, int cs_mid) {
 
 void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_mid, const void* wpw, const float* bpw,
                   const float* wdw, const float* bdw, void* y, void* se_mean, double flops, double bytes,
-                  hipStream_t s, AsyncReport rep, int stride, int OH, int OW, int pad_t, int pad_l) {
+                  hipStream_t s, AsyncReport rep, int stride, int OH, int OW, int pad_t, int pad_l, double spill) {
   M2S_CHECK(stride == 1 ? ir_ws_supported(H, W, cs_in, kp, cs_mid)
                         : stride == 2 && ir_ws_s2_supported(H, W, cs_in, kp, cs_mid, OH, OW, pad_t, pad_l),
             "ir_ws: unsupported shape");
@@ -754,7 +769,7 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
 #define M2S_IRWS(W_, KS_, S_, NAME_)                                                                    \
   if (W == W_ && kp == KS_ * 32 && stride == S_) {                                                      \
     allow_lds(reinterpret_cast<const void*>(&ir_ws_kernel<W_, KS_, S_>));                             \
-    ProfScope ps(NAME_, flops, bytes, s);                                                               \
+    ProfScope ps(NAME_, flops, bytes, s, spill);                                                        \
     hipLaunchKernelGGL((ir_ws_kernel<W_, KS_, S_>), grid, dim3(64 * (WS_NP + WS_NC)), L.total, s, xb, N, H, cs_mid, wb, \
                        bpw, wdw, bdw, yb, mb, tr, rep.spin_max, rep.err, pad_t, pad_l);                  \
     M2S_IRWS_DUMP(NAME_)                                                                                \

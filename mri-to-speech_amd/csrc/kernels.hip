@@ -169,22 +169,33 @@ __global__ void __launch_bounds__(256) lstm_step_kernel(const float* __restrict_
 __global__ void __launch_bounds__(256) mel_head_kernel(const float* __restrict__ hs, int rows, int H,
                                                        const float* __restrict__ wt, const float* __restrict__ b,
                                                        int n_mels, float* __restrict__ out) {
-  extern __shared__ float ys[];  // [4][H]
-  const int r0 = blockIdx.x * 4;
+  // one output row (frame) per workgroup: y = h_fwd + h_bwd staged in LDS, lane = mel (n_mels <= 64), the
+  // four waves take a quarter of K each with four independent FMA chains, the quarters added in a fixed order
+  // (a 640-long dependent FMA chain per thread made a 30-frame clip's head a 26 us launch)
+  extern __shared__ float ys[];  // [H] + [4][64] partial sums
+  float* part = ys + H;
+  const int row = blockIdx.x;
   const long plane = (long)rows * H;
-  for (int i = threadIdx.x; i < 4 * H; i += 256) {
-    const int r = i / H, k = i - r * H;
-    const int row = r0 + r;
-    ys[i] = row < rows ? hs[(long)row * H + k] + hs[plane + (long)row * H + k] : 0.f;
-  }
+  for (int k = threadIdx.x; k < H; k += 256) ys[k] = hs[(long)row * H + k] + hs[plane + (long)row * H + k];
   __syncthreads();
-  const int r = threadIdx.x >> 6, nl = threadIdx.x & 63;
-  const int row = r0 + r;
-  if (row >= rows) return;
-  for (int n = nl; n < n_mels; n += 64) {
-    float acc = 0.f;
-    for (int k = 0; k < H; ++k) acc += ys[r * H + k] * wt[(long)k * n_mels + n];
-    out[(long)row * n_mels + n] = acc + b[n];
+  const int q = threadIdx.x >> 6;
+  const int k0 = q * H / 4, k1 = (q + 1) * H / 4;
+  for (int nb = 0; nb < n_mels; nb += 64) {  // 64 mels a pass (the reference's n_mels = 64: one pass)
+    const int n = nb + (threadIdx.x & 63);
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (n < n_mels) {
+      int k = k0;
+      for (; k + 4 <= k1; k += 4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = fmaf(ys[k + j], wt[(long)(k + j) * n_mels + n], a[j]);
+      }
+      for (; k < k1; ++k) a[0] = fmaf(ys[k], wt[(long)k * n_mels + n], a[0]);
+    }
+    if (nb > 0) __syncthreads();  // the previous pass's partials were read
+    part[threadIdx.x] = (a[0] + a[1]) + (a[2] + a[3]);
+    __syncthreads();
+    const int l = threadIdx.x & 63;
+    if (q == 0 && n < n_mels) out[(long)row * n_mels + n] = ((part[l] + part[64 + l]) + (part[128 + l] + part[192 + l])) + b[n];
   }
 }
 
@@ -361,8 +372,8 @@ void launch_lstm_step(const float* pre, const float* whh, float* hs, float* cst,
 
 void launch_mel_head(const float* hs, int rows, int H, const float* wt, const float* b, int n_mels, float* out,
                      hipStream_t s) {
-  hipLaunchKernelGGL(mel_head_kernel, dim3(ceil_div(rows, 4)), dim3(256), 4 * H * sizeof(float), s, hs, rows, H, wt, b,
-                     n_mels, out);
+  M2S_CHECK(n_mels >= 1 && H >= 4, "mel_head: shape");
+  hipLaunchKernelGGL(mel_head_kernel, dim3(rows), dim3(256), (H + 4 * 64) * sizeof(float), s, hs, rows, H, wt, b, n_mels, out);
   M2S_HIP(hipGetLastError());
 }
 

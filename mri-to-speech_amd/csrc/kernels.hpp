@@ -104,7 +104,7 @@ bool ir_ws_s2_supported(int H, int W, int cs_in, int kp, int cs_mid, int OH, int
 void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_mid, const void* wpw, const float* bpw,
                   const float* wdw, const float* bdw, void* y, void* se_mean, double flops, double bytes,
                   hipStream_t s, AsyncReport rep = {}, int stride = 1, int OH = 0, int OW = 0, int pad_t = 0,
-                  int pad_l = 0);
+                  int pad_l = 0, double spill = 0.0);
 // Stride-2 IR front half on bands of 4 output rows (blocks.3.0: 32x32 -> 16x16), split fp32 or bf16: y =
 // the SE GEMM's operand (N, OH*OW, cs_mid; split: interleaved hi/lo), psum = squeeze partial sums
 // (N, OH / 4, cs_mid) for launch_se_mean.  wdw: fp32 tap-major [9][cs_mid].  (ir_s2band.hip)

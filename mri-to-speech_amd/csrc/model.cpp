@@ -83,6 +83,8 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_IR_FUSED")) ir_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_IR_WS")) ir_ws_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_IR_WS_S2")) ir_ws_s2_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_IRWS_MIN")) irws_min_ = std::atoi(e);
+  if (const char* e = std::getenv("M2S_SEWS_MIN")) sews_min_cus_ = std::atoi(e);
   if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_EXPAND")) f8_expand_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_S2")) f8_s2_ = std::strcmp(e, "0") != 0;
@@ -777,13 +779,16 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         bool f8 = false;  // fp8 engine: e4m3 depthwise output -> the e4m3 SE GEMM
         // bf16 feeds the fused kernel bf16 depthwise taps (dword halves), split fp32 the fp32 taps
         const void* wdw = arena_.ptr(SPL ? b.dw_w : b.dw_w2);
-        if (SPL && b.stride == 1 && ir_fused_ && ir_ws_ && ir_ws_supported(nh, nw, b.c1.cs_in, b.c1.kp, cs)) {
+        const bool big = nc >= irws_min_;  // persistent ir_ws only where its one-image workgroups fill the chip
+        if (SPL && b.stride == 1 && ir_fused_ && ir_ws_ && big && ir_ws_supported(nh, nw, b.c1.cs_in, b.c1.kp, cs)) {
           const double P = (double)nh * nw;
           launch_ir_ws(cur, nc, nh, nw, b.c1.cs_in, b.c1.kp, cs, b.c1.w, b.c1.b, static_cast<const float*>(arena_.ptr(b.dw_w)),
                        static_cast<const float*>(arena_.ptr(b.dw_b)), M2, se_mean, 2.0 * nc * P * b.mid * (b.c1.cin + 9),
-                       // algorithmic bytes on the real channel counts (split fp32: 4 B an element): the block input,
-                       // the depthwise output, the split expand weights, taps and biases
-                       4.0 * nc * P * (b.c1.cin + b.mid) + 4.0 * b.mid * (b.c1.cin + 11.0), s, ws_report());
+                       // algorithmic bytes on the real channel counts (split fp32: 4 B an element): compulsory = the
+                       // block input, the split expand weights, taps and biases, the SE means out; the depthwise output
+                       // map is a spill (written here only for the SE-gated conv_pwl to read back: m2s.h spill_bytes)
+                       4.0 * nc * P * b.c1.cin + 4.0 * b.mid * (b.c1.cin + 11.0) + 4.0 * nc * b.mid, s, ws_report(), 1, 0, 0,
+                       0, 0, 4.0 * nc * P * b.mid);
         } else if (FUSABLE && b.stride == 1 && ir_fused_ && ir_fused_supported(nh, nw, b.c1.cs_in, cs, SPL)) {
           const double P = (double)nh * nw, es = SPL ? 4.0 : 2.0;
           f8 = b.f8_pwl && se_gemm_f8_supported(nh * nw, cs, chan_stride(b.cout));
@@ -797,13 +802,13 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                          nc * P * ((f8x ? 1.0 : es) * b.c1.cin + (f8 ? 1.0 : es) * b.mid), s, f8, f8x ? cur8 : nullptr,
                          f8x ? arena_.ptr(b.f8x_w) : nullptr, f8x ? static_cast<const float*>(arena_.ptr(b.f8x_s)) : nullptr,
                          b.f8x_kp);
-        } else if (SPL && b.stride == 2 && ir_fused_ && ir_ws_ && ir_ws_s2_ &&
+        } else if (SPL && b.stride == 2 && ir_fused_ && ir_ws_ && ir_ws_s2_ && big &&
                    ir_ws_s2_supported(oh, ow, b.c1.cs_in, b.c1.kp, cs, nh, nw, qt, ql)) {
           const double Pi = (double)oh * ow, Po = (double)nh * nw;
           launch_ir_ws(cur, nc, oh, ow, b.c1.cs_in, b.c1.kp, cs, b.c1.w, b.c1.b, static_cast<const float*>(arena_.ptr(b.dw_w)),
                        static_cast<const float*>(arena_.ptr(b.dw_b)), M2, se_mean, 2.0 * nc * b.mid * (Pi * b.c1.cin + Po * 9),
-                       4.0 * nc * (Pi * b.c1.cin + Po * b.mid) + 4.0 * b.mid * (b.c1.cin + 11.0), s, ws_report(), 2, nh, nw,
-                       qt, ql);
+                       4.0 * nc * Pi * b.c1.cin + 4.0 * b.mid * (b.c1.cin + 11.0) + 4.0 * nc * b.mid, s, ws_report(), 2, nh, nw,
+                       qt, ql, 4.0 * nc * Po * b.mid);
         } else if (FUSABLE && b.stride == 2 && ir_fused_ && ir_fused_s2_supported(oh, ow, b.c1.cs_in, cs, SPL) &&
                    nh * nw <= 64) {
           const double Pi = (double)oh * ow, Po = (double)nh * nw, es = SPL ? 4.0 : 2.0;
@@ -886,7 +891,10 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                             rows * cs + 2.0 * rows * co * (b.skip ? 2.0 : 1.0) + (double)b.f8_npad * b.f8_kp +
                                 2.0 * nc * cs + (next8 ? rows * ld8 : 0.0),
                             next8, ld8);
-        } else if (SPL && se_ws_ && se_ws_supported(nh * nw, cs, chan_stride(b.cout))) {
+        } else if (SPL && se_ws_ && se_ws_supported(nh * nw, cs, chan_stride(b.cout)) &&
+                   // se_ws runs one persistent workgroup per tile (256 rows; 128 at 8 x 8) up to one per CU: below a
+                   // full round of tiles the split-K conv_gemm SE GEMM fills the chip instead
+                   ceil_div(nc * nh * nw, nh * nw == 64 ? 128 : 256) >= sews_min_cus_ * device_cus()) {
           const double rows = (double)nc * nh * nw;
           launch_se_ws(M2, nc * nh * nw, nh * nw, cs, b.c2.w, b.c2.n_pad, b.c2.b, scale, b.skip ? cur : nullptr, nxt,
                        chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
@@ -1107,7 +1115,7 @@ Vocoder::Vocoder(const StateDict& sd, const m2s_hifigan_h& h, int dtype, int dev
       // fp8: the C = 128 / 256 (and, f8_mrf64_, C = 64) resblock convs as e4m3 bytes for conv1d_f8 (K = 128
       // block-scaled MFMA; C = 64: two taps a K step)
       const bool q8 = dtype == M2S_DT_FP8 && h.resblock == 1 &&
-                      (!frag || (co == 64 && f8_mrf64_) || (co == 32 && f8_mrf32_)) &&
+                      ((co >= 128 && !frag) || (co == 64 && f8_mrf64_) || (co == 32 && f8_mrf32_)) &&
                       conv1d_f8_supported(co, kk);
       auto mk_q8 = [&](const std::string& name) {
         std::vector<float> wv = fold_wn(sd, name, {co, co, kk});

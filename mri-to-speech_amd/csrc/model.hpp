@@ -101,6 +101,12 @@ class Acoustic {
   bool ir_fused_ = true;  // bf16: fused conv_pw + conv_dw + SE squeeze (env M2S_IR_FUSED=0 disables)
   bool ir_ws_ = true;     // split fp32: the persistent warp-specialised form of it (env M2S_IR_WS=0 disables)
   bool ir_ws_s2_ = true;  // ... also for the stride-2 block at 16x16 (env M2S_IR_WS_S2=0: ir_pwdw_s2)
+  // Small passes (the reference CLI's one clip, configs[1]'s 8 x 4): the persistent one-workgroup-per-image (ir_ws)
+  // and one-tile-per-CU (se_ws) kernels fill a few dozen CUs there, so below these sizes the pass runs the grid forms
+  // (ir_pwdw / ir_pwdw_s2, the split-K conv_gemm SE GEMM).  Env M2S_IRWS_MIN (images per pass) / M2S_SEWS_MIN (se_ws
+  // tiles, in CUs: 1 = one full round) override.
+  int irws_min_ = 512;
+  int sews_min_cus_ = 1;
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
   bool f8_er_ = true;            // fp8: EdgeResidual blocks.1.1/.2 on e4m3 (env M2S_F8_ER=0: bf16 er_fused)
   bool se_y8_ = true;            // fp8: the SE GEMM also stores the next expand's e4m3 operand (env M2S_SE_Y8=0:

@@ -14,7 +14,7 @@ thread_local std::string g_stage = "other";
 
 struct Rec {
   std::string name, stage;
-  double flops, bytes;
+  double flops, bytes, spill;
   hipEvent_t a, b;
 };
 
@@ -50,11 +50,11 @@ bool prof_on() { return P().on; }
 StageTag::StageTag(const std::string& stage) : prev_(g_stage) { g_stage = stage; }
 StageTag::~StageTag() { g_stage = prev_; }
 
-ProfScope::ProfScope(const std::string& name, double flops, double bytes, hipStream_t s) : s_(s) {
+ProfScope::ProfScope(const std::string& name, double flops, double bytes, hipStream_t s, double spill) : s_(s) {
   Prof& p = P();
   if (!p.on) return;
   std::lock_guard<std::mutex> g(p.mu);
-  Rec r{name, g_stage, flops, bytes, p.get(), p.get()};
+  Rec r{name, g_stage, flops, bytes, spill, p.get(), p.get()};
   M2S_HIP(hipEventRecord(r.a, s));
   slot_ = (int)p.recs.size();
   p.recs.push_back(r);
@@ -123,6 +123,7 @@ extern "C" int m2s_prof_launches_impl(m2s_prof_launch* out, int max, int* n_out)
       l.ms = ms;
       l.flops = r.flops;
       l.bytes = r.bytes;
+      l.spill_bytes = r.spill;
     }
     ++n;
     p.pool.push_back(r.a);

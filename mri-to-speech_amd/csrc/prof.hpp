@@ -23,7 +23,8 @@ class StageTag {
 
 class ProfScope {
  public:
-  ProfScope(const std::string& name, double flops, double bytes, hipStream_t s);
+  // spill: bytes of an intermediate the kernel writes only for a later kernel to read back (not in `bytes`)
+  ProfScope(const std::string& name, double flops, double bytes, hipStream_t s, double spill = 0.0);
   ~ProfScope();
 
  private:

@@ -51,8 +51,10 @@ __device__ __forceinline__ void st4(bf16_t* u, int cs, const float* v) {
   }
 }
 
-template <int SP>
-__global__ void __launch_bounds__(256) se_excite_kernel(const bf16_t* __restrict__ mean, int N, int mid, int cs_mid,
+// NW waves a workgroup: 4, or 16 for small batches (the reduce's K chain split NW / RT ways instead of 4 / RT:
+// at one clip the 8 x 8 blocks' 39-step chain made a 16-workgroup launch ~23 us)
+template <int SP, int NW>
+__global__ void __launch_bounds__(64 * NW) se_excite_kernel(const bf16_t* __restrict__ mean, int N, int mid, int cs_mid,
                                                         const bf16_t* __restrict__ w1, int kp1,
                                                         const float* __restrict__ b1, int rd,
                                                         const bf16_t* __restrict__ w2, int kp2,
@@ -60,18 +62,18 @@ __global__ void __launch_bounds__(256) se_excite_kernel(const bf16_t* __restrict
   constexpr int R = SP ? 2 : 1;
   constexpr int UB = SP ? 4 : 8;  // k-steps of loads in flight per batch
   __shared__ __attribute__((aligned(16))) bf16_t hid[R][SE_IMG][SE_HROW];
-  __shared__ __attribute__((aligned(16))) f32x4 part[4][64];  // K-split partial sums
+  __shared__ __attribute__((aligned(16))) f32x4 part[NW][64];  // K-split partial sums
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const int n0 = blockIdx.x * SE_IMG;
   const bool img_ok = n0 + r16 < N;
 
-  // ---- conv_reduce + SiLU: RT = ceil(rd / 16) row tiles; the 4 waves split K 4 / RT ways --------
+  // ---- conv_reduce + SiLU: RT = ceil(rd / 16) row tiles; the NW waves split K NW / RT ways -------
   // (wave w: row tile w % RT, k-steps w / RT, w / RT + KSP, ...), partials summed in LDS in a fixed
   // order.  One wave per row tile walked all cs_mid / 32 k-steps alone with two or three waves idle.
   {
-    const int RT = (rd + 15) / 16, KSP = 4 / RT;
+    const int RT = (rd + 15) / 16, KSP = NW / RT;
     const int rt = wave % RT, kq = wave / RT;
     const int row = 16 * rt + r16;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -126,8 +128,8 @@ __global__ void __launch_bounds__(256) se_excite_kernel(const bf16_t* __restrict
   const int ntile = cs_mid / 16;
   // channel tiles dealt over the gridDim.y workgroups of these images and their 4 waves (tile
   // 4 * (y + gridDim.y * v) + wave); 4 tiles per batch, all their weight fragments loaded first
-  const int ts = 4 * gridDim.y;
-  for (int t0 = 4 * blockIdx.y + wave; t0 < ntile; t0 += 4 * ts) {
+  const int ts = NW * gridDim.y;
+  for (int t0 = NW * blockIdx.y + wave; t0 < ntile; t0 += 4 * ts) {
     bf16x8 a[4][SE_RDMAX / 32], al[4][SE_RDMAX / 32];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -166,15 +168,18 @@ void launch_se_excite(const void* mean, int N, int mid, int cs_mid, const void* 
                       int rd, const void* w2, int kp2, const float* b2, void* gate, bool split, hipStream_t s) {
   M2S_CHECK(se_excite_supported(rd, kp2, cs_mid) && kp1 >= cs_mid && N > 0, "se_excite: unsupported shape");
   const double es = split ? 4.0 : 2.0;
-  ProfScope ps(split ? "se_excite_kernel<1>" : "se_excite_kernel<0>", 2.0 * 2.0 * N * mid * rd,
-               es * (2.0 * N * cs_mid) + es * 2.0 * mid * rd, s);
-  auto k = split ? se_excite_kernel<1> : se_excite_kernel<0>;
   // expand tiles split over ES workgroups per 16 images (each recomputes the reduce) while the grid
   // stays within one workgroup per CU: 1920 images were 120 workgroups (0.67 ms per step); ES = 2
-  // gives 0.50, and ES = 3 / 4 / 8 (past one per CU) 0.64 / 0.61 / 0.87
+  // gives 0.50, and ES = 3 / 4 / 8 (past one per CU) 0.64 / 0.61 / 0.87.  Under a quarter of the CUs
+  // busy (a few dozen images) the workgroups run 16 waves
   const int cus = device_cus();
   const int nwg = ceil_div(N, SE_IMG), ES = std::max(1, std::min(std::min(cus / nwg, cs_mid / 64), 8));
-  hipLaunchKernelGGL(k, dim3(nwg, ES), dim3(256), 0, s, static_cast<const bf16_t*>(mean), N, mid, cs_mid,
+  const bool wide = nwg * ES * 4 <= cus;
+  static const char* const names[2][2] = {{"se_excite_kernel<0, 4>", "se_excite_kernel<1, 4>"},
+                                          {"se_excite_kernel<0, 16>", "se_excite_kernel<1, 16>"}};
+  ProfScope ps(names[wide][split], 2.0 * 2.0 * N * mid * rd, es * (2.0 * N * cs_mid) + es * 2.0 * mid * rd, s);
+  auto k = wide ? (split ? se_excite_kernel<1, 16> : se_excite_kernel<0, 16>) : (split ? se_excite_kernel<1, 4> : se_excite_kernel<0, 4>);
+  hipLaunchKernelGGL(k, dim3(nwg, ES), dim3(wide ? 1024 : 256), 0, s, static_cast<const bf16_t*>(mean), N, mid, cs_mid,
                      static_cast<const bf16_t*>(w1), kp1, b1, rd, static_cast<const bf16_t*>(w2), kp2, b2,
                      static_cast<bf16_t*>(gate));
   M2S_HIP(hipGetLastError());

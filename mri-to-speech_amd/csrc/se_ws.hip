@@ -122,12 +122,12 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
   const int gimg = (grow + 1023) / 1024 * 1024;     // ... in LDS
   char* gbuf = smem + NS * SLOT;                    // [2][nimg][gimg]
   unsigned* flags = reinterpret_cast<unsigned*>(gbuf + 2 * nimg * gimg);  // FULL[NS], FREE[NS]
-  const uint32_t full0 = lds_u32(flags), free0 = lds_u32(flags + NS);
+  const uint32_t full0 = lds_u32(flags), free0 = lds_u32(flags + NS), poison = lds_u32(flags + 2 * NS);
   const int nsteps = F8 ? a.kp / 128 : a.cs_in / 32;
   const int n_tiles = a.n_tiles_m;                  // one n tile: BN covers cs_out
   const int my_tiles = (int)blockIdx.x < n_tiles ? (n_tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
 
-  if (tid < 2 * NS) flags[tid] = 0u;
+  if (tid <= 2 * NS) flags[tid] = 0u;  // FULL, FREE and the loaders' poison word
   __syncthreads();  // the only workgroup barrier
 
   if (wave >= NC) {
@@ -146,7 +146,12 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
       const uint8_t* xt = a.x + (size_t)m0 * xrow_b;
       for (int st = 0; st < nsteps; ++st, ++s) {
         const int slot = s % NS, use = s / NS;
-        if (use > 0 && !wait_flag(free0 + 4 * slot, (unsigned)(NC * use), a.spin_max)) report_async(a.err, M2S_ASYNC_WS, lane);
+        if (use > 0 && !wait_flag(free0 + 4 * slot, (unsigned)(NC * use), a.spin_max)) {
+          // a FREE timeout: the refill below may overwrite a slot a consumer still reads, so the poison word makes
+          // every consumer store NaN from its next epilogue on (written and retired before the DMA is issued)
+          report_async(a.err, M2S_ASYNC_WS, lane);
+          if (lane == 0) asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(poison), "v"(1u) : "memory");
+        }
         if (st == 0 && l == 0) {  // the tile's gate rows: nimg x 2 cs_in bf16, 16 B a lane
           const int img0 = m0 / a.P, nb = grow / 16;
           char* gdst = gbuf + (it & 1) * nimg * gimg;
@@ -204,7 +209,7 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
   const uint32_t a_lds0 = sm0 + (uint32_t)((wn * NT * 16 + r16) * ROWB);
   const uint32_t b_lds0 = sm0 + (uint32_t)((BN + wm * 64 + r16) * ROWB);
   const uint32_t g_lds0 = lds_u32(gbuf) + (uint32_t)(g * (F8 ? 64 : 16));
-  bool bad = false;  // a FULL wait timed out: this wave's tiles are stored as NaN from then on
+  bool bad = false;  // a FULL wait (or a loader's FREE wait) timed out: this wave's tiles are stored as NaN from then on
   int s = 0;
   for (int it = 0; it < my_tiles; ++it) {
     const int tile = blockIdx.x + it * gridDim.x;
@@ -351,6 +356,11 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
       }
       }
     }
+    {  // a loader's FREE wait timed out (its refill may have overwritten a slot this wave read): NaN from here on
+      unsigned pz;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(pz) : "v"(poison) : "memory");
+      bad = bad || __builtin_amdgcn_readfirstlane(pz) != 0u;
+    }
 
     if constexpr (F8) {  // bf16 out = wscale * acc + bias (+ skip), skip rows fetched first
       uint2 rv[MT][NT];
@@ -443,7 +453,7 @@ void launch_cfg(SeWsArgs& a, hipStream_t s, double flops, double bytes) {
   allow_lds(fn);
   const int nimg = BM / a.P > 0 ? BM / a.P : 1;
   const int gimg = ((F8 ? a.cs_in * 2 : a.cs_in * 4) + 1023) / 1024 * 1024;
-  const size_t lds = (size_t)NS * (BN + BM) * ROWB + (size_t)2 * nimg * gimg + 2 * NS * sizeof(unsigned);
+  const size_t lds = (size_t)NS * (BN + BM) * ROWB + (size_t)2 * nimg * gimg + (2 * NS + 1) * sizeof(unsigned);
   M2S_CHECK(lds <= 160 * 1024, "se_ws: LDS budget");
   M2S_CHECK(BM % a.P == 0 || a.P % BM == 0, "se_ws: tile rows vs image size");
   M2S_CHECK(a.cs_out <= BN, "se_ws: one n tile covers the outputs");

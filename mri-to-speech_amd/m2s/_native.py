@@ -20,7 +20,7 @@ F32, BF16, BF16X3, FP8 = 0, 1, 2, 3
 DTYPES = {"fp32": F32, "float32": F32, "f32": F32, "bf16": BF16, "bfloat16": BF16, "bf16x3": BF16X3,
           "fp8": FP8, "e4m3": FP8}
 ELEM_F32, ELEM_I64 = 0, 1
-ABI_VERSION = 5  # include/m2s.h M2S_ABI_VERSION
+ABI_VERSION = 6  # include/m2s.h M2S_ABI_VERSION
 
 
 class M2SError(RuntimeError):
@@ -46,7 +46,7 @@ class ProfStat(C.Structure):
 
 class ProfLaunch(C.Structure):
     _fields_ = [("name", C.c_char * 96), ("stage", C.c_char * 24), ("ms", C.c_double), ("flops", C.c_double),
-                ("bytes", C.c_double)]
+                ("bytes", C.c_double), ("spill_bytes", C.c_double)]
 
 
 _lib = None
@@ -190,17 +190,17 @@ def prof_launches() -> List[dict]:
     buf = (ProfLaunch * cap)()
     check(lib().m2s_prof_launches(buf, cap, C.byref(n)))
     return [dict(name=buf[i].name.decode(), stage=buf[i].stage.decode(), ms=buf[i].ms, flops=buf[i].flops,
-                 bytes=buf[i].bytes) for i in range(min(n.value, cap))]
+                 bytes=buf[i].bytes, spill_bytes=buf[i].spill_bytes) for i in range(min(n.value, cap))]
 
 
 def aggregate(launches: List[dict], key: str = "name") -> List[dict]:
     """Per-kernel (key="name") or per-stage (key="stage") sums of prof_launches() records."""
     agg: Dict[str, dict] = {}
     for r in launches:
-        a = agg.setdefault(r[key], dict(name=r[key], launches=0, ms=0.0, flops=0.0, bytes=0.0))
+        a = agg.setdefault(r[key], dict(name=r[key], launches=0, ms=0.0, flops=0.0, bytes=0.0, spill_bytes=0.0))
         a["launches"] += 1
-        for f in ("ms", "flops", "bytes"):
-            a[f] += r[f]
+        for f in ("ms", "flops", "bytes", "spill_bytes"):
+            a[f] += r.get(f, 0.0)
     return list(agg.values())
 
 

@@ -38,6 +38,10 @@ def _as_f32(t: torch.Tensor, device: torch.device) -> torch.Tensor:
 
 
 class AcousticEngine:
+    """libm2s's acoustic model on one device.  ``chunk``: frames per CNN pass (include/m2s.h
+    m2s_acoustic_set_chunk); a pass may hold up to chunk + chunk // 16 frames when that saves a short tail
+    pass, so size limits chosen through ``chunk`` have ~6 % of headroom to leave."""
+
     def __init__(self, state_dict: Dict, n_mels: int = 64, rnn_hidden: int = 640, dtype: str = "bf16x3",
                  device=None, chunk: int = CNN_CHUNK):
         self.device = _device(device)

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(L, name), name
     assert sorted(N.exported_symbols()) == declared
-    assert L.m2s_abi_version() == N.ABI_VERSION == 5
+    assert L.m2s_abi_version() == N.ABI_VERSION == 6
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-device error path")

@@ -4,7 +4,7 @@ bf16x3 keeps every activation and weight as a bf16 pair hi + lo (17 significant 
 each product as the three exact bf16 MFMA terms hi*hi + hi*lo + lo*hi with fp32 accumulation
 (include/m2s.h M2S_DT_BF16X3).  It must pass the SAME bars as the exact-f32 path
 (tests/test_gpu_parity.py): wav max |d| <= 1e-4 vs the reference goldens, CNN taps <= 1e-4 of the
-tensor's scale, mel_norm <= 1e-4 and wav <= 2e-4 end to end.  GPU box only.
+tensor's scale, mel_norm <= 1e-4 and wav <= 1e-4 end to end.  GPU box only.
 """
 import json
 import os
@@ -111,7 +111,7 @@ def test_pipeline_bf16x3_end_to_end(rt, ac_state):
     np.testing.assert_allclose(out["mel_norm"], mn.numpy(), atol=1e-4, rtol=0)
     np.testing.assert_allclose(out["mel_db"], db.numpy(), atol=2e-3, rtol=0)
     np.testing.assert_allclose(out["mel_log"], ln.numpy(), atol=5e-4, rtol=0)
-    np.testing.assert_allclose(out["wav"], wav[:, 0].numpy(), atol=2e-4, rtol=0)
+    np.testing.assert_allclose(out["wav"], wav[:, 0].numpy(), atol=1e-4, rtol=0)
 
 
 @pytest.mark.parametrize("hw,n", [((256, 256), 300), ((128, 128), 263)])
@@ -122,6 +122,7 @@ def test_ir_ws_matches_grid_kernel(rt, ac_state, monkeypatch, hw, n):
     values): the two differ by about their own distance from the fp32 oracle (~1e-5 of the scale,
     tools/diag_ir_ws.py), so the bar is the parity bar, 1e-4."""
     fr = torch.from_numpy(synth.synth_frames(1, n, hw=hw, seed=7)[0]).to(DEV)
+    monkeypatch.setenv("M2S_IRWS_MIN", "0")  # ir_ws at any pass size (the product runs it from 512 frames a pass)
     ws = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
     monkeypatch.setenv("M2S_IR_WS", "0")
     grid = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
@@ -139,6 +140,7 @@ def test_ir_ws_stride2_matches_grid_kernel_and_oracle(rt, ac_state, monkeypatch,
     summation order: the 1e-4 parity bar."""
     sd = {k: torch.from_numpy(v) for k, v in ac_state.items()}
     fr = torch.from_numpy(synth.synth_frames(1, n, seed=23)[0])
+    monkeypatch.setenv("M2S_IRWS_MIN", "0")  # ir_ws at any pass size (the product runs it from 512 frames a pass)
     ws = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
     monkeypatch.setenv("M2S_IR_WS_S2", "0")
     grid = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
@@ -249,6 +251,8 @@ def test_se_ws_matches_barrier_ring(rt, ac_state, monkeypatch, n):
     workgroup walks several tiles and its ring carries over)."""
     fr = torch.from_numpy(synth.synth_frames(1, n, seed=41)[0]).to(DEV)
     monkeypatch.setenv("M2S_SE_WS", "1")
+    monkeypatch.setenv("M2S_SEWS_MIN", "0")  # se_ws at any pass size (the product runs it from a full round of tiles)
+    monkeypatch.setenv("M2S_KSPLIT", "1")    # the barrier ring unsplit: the same K order as the flag ring
     ws = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
     monkeypatch.setenv("M2S_SE_WS", "0")
     ring = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)

@@ -7,7 +7,7 @@
               bench dtype (bf16x3); 17 clips (every 4th and the last) against the fp32 oracle in one
               batched oracle run (all 64 passed once: profiles/r03_cfg3_all64_oracle.txt), every clip against the bf16 path
   configs[4]  a 1000-frame clip end to end (bf16x3), the clip length of the fp8 config
-Tolerances (fp32 = the reference's precision): mel_norm <= 1e-4, mel_log <= 5e-4, wav <= 2e-4
+Tolerances (fp32 = the reference's precision): mel_norm <= 1e-4, mel_log <= 5e-4, wav <= 1e-4
 (1000 frames: mel_norm <= 2e-4 — fp32 summation order over 1000 recurrent steps); bf16:
 mel_norm <= 5e-2 and cosine >= 0.999, wav SNR >= 20 dB.  (scripts/run_mri_video_inference.py:218-242)
 """
@@ -21,7 +21,7 @@ from oracle import pipeline
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
-FP32_TOL = {"mel_norm": 1e-4, "mel_db": 2e-3, "mel_log": 5e-4, "wav": 2e-4}
+FP32_TOL = {"mel_norm": 1e-4, "mel_db": 2e-3, "mel_log": 5e-4, "wav": 1e-4}
 
 
 @pytest.fixture(scope="module")
@@ -122,3 +122,48 @@ def test_config4_1x1000_end_to_end(rt, weights):
     tol = dict(FP32_TOL, mel_norm=2e-4, mel_log=1e-3, mel_db=4e-3)
     for k, t in tol.items():
         np.testing.assert_allclose(out[k], ref[k], atol=t, rtol=0, err_msg=k)
+
+
+def _launches(fn):
+    from m2s import _native
+    _native.prof_enable(True)
+    out = fn()
+    torch.cuda.synchronize()
+    names = [r["name"] for r in _native.prof_launches()]
+    _native.prof_enable(False)
+    return out, names
+
+
+def test_config2_small_pass_plan(rt, weights, clip30, monkeypatch):
+    """The one-clip shape of the reference CLI (run_mri_video_inference.py:215-242) runs the small-pass plan: the grid
+    IR front halves (ir_pwdw / ir_pwdw_s2) instead of the one-workgroup-per-image ir_ws, the split-K conv_gemm SE
+    GEMM instead of se_ws, and split-K vocoder convs (conv_gemm_ksum_kernel).  Same split fp32 arithmetic up to
+    summation order: within 1e-4 of the persistent plan (M2S_IRWS_MIN=0, M2S_SEWS_MIN=0, M2S_KSPLIT=1) and of the
+    fp32 oracle at the configs[2] bar."""
+    fr, ref = clip30
+    x = torch.from_numpy(fr).to(DEV)
+    small, names = _launches(lambda: {k: v.cpu().numpy() for k, v in _pipe(rt, weights, "bf16x3").forward(x).items()})
+    assert not any(n.startswith(("ir_ws_kernel", "se_ws_kernel")) for n in names), sorted(set(names))
+    assert any(n.startswith("ir_pwdw_kernel") for n in names) and any(n.startswith("conv_gemm_ksum_kernel") for n in names)
+    monkeypatch.setenv("M2S_IRWS_MIN", "0")
+    monkeypatch.setenv("M2S_SEWS_MIN", "0")
+    monkeypatch.setenv("M2S_KSPLIT", "1")
+    big, names = _launches(lambda: {k: v.cpu().numpy() for k, v in _pipe(rt, weights, "bf16x3").forward(x).items()})
+    assert any(n.startswith("ir_ws_kernel") for n in names) and any(n.startswith("se_ws_kernel") for n in names)
+    assert not any(n.startswith("conv_gemm_ksum_kernel") for n in names)
+    for k, tol in FP32_TOL.items():
+        np.testing.assert_allclose(small[k], ref[k], atol=tol, rtol=0, err_msg=k)
+        np.testing.assert_allclose(small[k], big[k], atol=tol, rtol=0, err_msg=k)
+
+
+def test_config1_split_k_matches_unsplit(rt, weights, monkeypatch):
+    """configs[1] (8 x 4, bf16): the SE GEMMs of the small pass run split K (fp32 partial sums added in split order by
+    conv_gemm_ksum_kernel); against the unsplit launches (M2S_KSPLIT=1) the mel differs only by fp32 summation
+    order before the bf16 rounding of each layer's output."""
+    ac = weights[0]
+    x = torch.from_numpy(synth.synth_frames(8, 4, seed=301)).to(DEV)
+    a, names = _launches(lambda: rt.AcousticEngine(ac, dtype="bf16", device=DEV).forward(x).cpu().numpy())
+    assert any(n.startswith("conv_gemm_ksum_kernel") for n in names)
+    monkeypatch.setenv("M2S_KSPLIT", "1")
+    b = rt.AcousticEngine(ac, dtype="bf16", device=DEV).forward(x).cpu().numpy()
+    assert np.isfinite(a).all() and _cos(a, b) >= 0.9999 and np.abs(a - b).max() <= 2e-2
