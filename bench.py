@@ -120,16 +120,18 @@ def pmc_traffic(kernel):
     return None, None, sha
 
 
-def stage_records():
-    """Per-stage PMC record of THIS tree (profiles/*_stages.json whose meta.src_sha equals source_sha(); made
-    by tools/evidence.py from the rocprofv3 FETCH_SIZE / WRITE_SIZE / SQ passes of tools/profile_step.py, each
+def stage_records(workload="headline"):
+    """Per-stage PMC record of THIS tree and workload (profiles/*_stages.json whose meta.src_sha equals source_sha()
+    and meta.workload `workload`: "headline" = the 64 x 30 bench step, "configs4_fp8" = the fp8 engine at 8 x 1000;
+    made by tools/evidence.py from the rocprofv3 FETCH_SIZE / WRITE_SIZE / SQ passes of tools/profile_step.py, each
     dispatch given the stage libm2s tagged its launch with): HBM bytes per step and MFMA utilisation."""
     import glob
     sha = source_sha()
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_stages.json")), reverse=True):
         with open(f) as fh:
             rec = json.load(fh)
-        if rec.get("meta", {}).get("src_sha") == sha:
+        meta = rec.get("meta", {})
+        if meta.get("src_sha") == sha and meta.get("workload", "headline") == workload:
             return rec, os.path.relpath(f, REPO)
     return None, None
 
@@ -139,12 +141,12 @@ STAGE_ORDER = ("cnn", "bilstm", "head", "glue", "voc_pre", "ups_c256", "mrf_c256
                "mrf_c64", "ups_c32", "mrf_c32", "voc_post", "other")
 
 
-def stage_table(launches, steps):
+def stage_table(launches, steps, workload="headline"):
     """roofline.stages: per stage of the path, event time per step (the HIP-event pass over the timed region),
     algorithmic bytes / FLOP and their rates, and, from the PMC record of this tree, HBM bytes per step (FETCH x2
     + WRITE), achieved HBM GB/s = those bytes / the event time, its fraction of 8 TB/s, and MFMA utilisation."""
     from m2s import _native
-    rec, src = stage_records()
+    rec, src = stage_records(workload)
     pmc = (rec or {}).get("stages", {})
     out = {}
     agg = {a["name"]: a for a in _native.aggregate(launches, "stage")}
@@ -166,8 +168,8 @@ def stage_table(launches, steps):
                         "hbm_frac": round(hb / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                         "mfma_util": p.get("mfma_util"), "valu_per_mfma": p.get("valu_per_mfma")})
         out[st] = row
-    return {"stages": out, "stages_source": src or f"no *_stages.json of source {source_sha()} in profiles/ "
-            "(tools/gpu_evidence.sh + tools/evidence.py)"}
+    return {"stages": out, "stages_source": src or f"no *_stages.json of source {source_sha()} and workload {workload} in "
+            "profiles/ (tools/gpu_evidence.sh + tools/evidence.py)"}
 
 
 def parse(argv=None):
@@ -182,7 +184,8 @@ def parse(argv=None):
     p.add_argument("--chunk", type=int, default=CNN_CHUNK,
                    help="frames per CNN pass (default: the engine's shipped m2s.config.CNN_CHUNK = one pass over the 64x30 step)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="C3 sample of the CPU baseline (seconds)")
+    p.add_argument("--cpu-long-frames", type=int, default=1000, help="C5 clip length of the CPU baseline (0: skip)")
     p.add_argument("--no-profile", action="store_true")
     p.add_argument("--no-parity", action="store_true", help="skip the oracle check of clip 0")
     p.add_argument("--no-compare", action="store_true", help="skip the secondary bf16 / fp8 lines (N = 1)")
@@ -321,7 +324,10 @@ def cosine_vs(ref, out, clip=0):
 
 
 def cpu_baseline(args, ac_sd, gen_sd, mean, std):
-    """Oracle (torch-CPU fp32 restatement of the reference graph) on this host's cores."""
+    """Oracle (torch-CPU fp32 restatement of the reference graph) on this host's cores, per BASELINE.md's CPU plan:
+    C3 (one clip x args.frames end to end) repeated for ~cpu_seconds with per-stage wall time (CNN / BiLSTM / head +
+    glue / Generator), C1 (mel only) from the same runs' CNN + BiLSTM + head stages, and C5 (ONE 1000-frame clip end to
+    end, the CNN in 100-frame chunks).  `value` is the C3 end-to-end rate (the headline's workload per clip)."""
     sys.path.insert(0, REPO)
     from oracle import acoustic, effnet, hifigan
 
@@ -329,24 +335,54 @@ def cpu_baseline(args, ac_sd, gen_sd, mean, std):
     torch.set_num_threads(threads)
     sd = {k: torch.from_numpy(v) for k, v in ac_sd.items()}
     gsd = {k: torch.from_numpy(v) for k, v in gen_sd.items()}
+
+    def clip(frames, T, acc, chunk=100):
+        t0 = time.perf_counter()
+        f = torch.cat([effnet.effnet_gap(sd, frames.reshape(T, args.hw, args.hw)[i:i + chunk])
+                       for i in range(0, T, chunk)]).view(1, T, -1)
+        t1 = time.perf_counter()
+        h = acoustic.bilstm_summerge(sd, f)
+        t2 = time.perf_counter()
+        mn = acoustic.head(sd, h)
+        ln = acoustic.mel_db_to_log(acoustic.denormalize_mel(mn[0], mean, std))
+        t3 = time.perf_counter()
+        hifigan.generator(gsd, HIFIGAN_H, ln.t().unsqueeze(0))
+        t4 = time.perf_counter()
+        for k, v in zip(("cnn", "bilstm", "head_glue", "generator"), (t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
+            acc[k] = acc.get(k, 0.0) + v
+        return t4 - t0
+
     T = args.frames
     frames = torch.from_numpy(synth.synth_frames(1, T, hw=(args.hw, args.hw), seed=77))
-    done, t0 = 0, time.perf_counter()
+    st3, done, el = {}, 0, 0.0
     with torch.no_grad():
-        while True:
-            f = effnet.effnet_gap(sd, frames.reshape(T, args.hw, args.hw)).view(1, T, -1)
-            mn = acoustic.head(sd, acoustic.bilstm_summerge(sd, f))
-            ln = acoustic.mel_db_to_log(acoustic.denormalize_mel(mn[0], mean, std))
-            hifigan.generator(gsd, HIFIGAN_H, ln.t().unsqueeze(0))
+        while el < args.cpu_seconds and done < 50:
+            el += clip(frames, T, st3)
             done += 1
-            el = time.perf_counter() - t0
-            if el >= args.cpu_seconds or done >= 50:
-                break
+    audio3 = T * HOP / SR
+    mel_s = st3["cnn"] + st3["bilstm"] + st3["head_glue"]
+    per = {"C1": {"what": f"1 clip x {T} frames -> mel (CNN-BiLSTM + head), from the C3 runs' stages",
+                  "frames_per_s": round(done * T / mel_s, 3)},
+           "C3": {"what": f"1 clip x {T} frames end to end", "clips": done, "frames_per_s": round(done * T / el, 3),
+                  "rtf": round(el / done / audio3, 4),
+                  "stage_ms_per_clip": {k: round(1e3 * v / done, 2) for k, v in st3.items()}}}
+    if args.cpu_long_frames > 0:  # C5: one long clip, end to end
+        TL = args.cpu_long_frames
+        fl = torch.from_numpy(synth.synth_frames(1, TL, hw=(args.hw, args.hw), seed=78))
+        st5 = {}
+        with torch.no_grad():
+            e5 = clip(fl, TL, st5)
+        per["C5"] = {"what": f"1 clip x {TL} frames end to end (CNN in 100-frame chunks)", "frames_per_s": round(TL / e5, 3),
+                     "rtf": round(e5 / (TL * HOP / SR), 4), "stage_ms": {k: round(1e3 * v, 1) for k, v in st5.items()}}
     return {"value": round(done * T / el, 3), "unit": "rtMRI frames/s", "cores": threads, "affinity_cpus": aff,
             "kind": "port",
-            "sample": f"{done} clip(s) x {T} frames at {args.hw}x{args.hw}, end to end (CNN-BiLSTM + glue + "
-                      f"HiFi-GAN), fp32 oracle (torch-CPU restatement of the reference graph), {el:.1f} s, "
-                      f"{threads} threads (sched_getaffinity {aff}, OMP_NUM_THREADS cap)"}
+            "sample": f"C3: {done} clip(s) x {T} frames at {args.hw}x{args.hw}, end to end (CNN-BiLSTM + glue + HiFi-GAN), "
+                      f"fp32 oracle (torch-CPU restatement of the reference graph), {el:.1f} s; C5: one "
+                      f"{args.cpu_long_frames}-frame clip; {threads} threads",
+            "threads_note": (f"{threads} threads = min(sched_getaffinity {aff}, OMP_NUM_THREADS): the GPU box grants one "
+                             "GPU's job a 16-CPU share (OMP_NUM_THREADS=16 there) although the affinity mask shows the "
+                             "whole host"),
+            "per_config": per}
 
 
 def long_clip_lines(args, build, device, sync, world, ref_args, clips=8, frames=1000, steps=3):
@@ -383,7 +419,8 @@ def long_clip_lines(args, build, device, sync, world, ref_args, clips=8, frames=
             _native.prof_enable(True)
             timed_loop(lambda: p.forward(x), steps, world, sync, device)
             _native.prof_enable(False)
-            line["roofline"] = roofline(_native.prof_launches(), dt, steps, line["value"], clips * frames)
+            line["roofline"] = roofline(_native.prof_launches(), dt, steps, line["value"], clips * frames, stages=True,
+                                        stage_workload="configs4_fp8")
         res[dt] = line
         del p
     res["fp8_over_bf16x3_step"] = round(res["fp8"]["ms_per_step"] / res["bf16x3"]["ms_per_step"], 3)
@@ -528,7 +565,7 @@ def caller_lines(args, pipe, build, device, sync, world, ref_args, runs=60):
     return res
 
 
-def roofline(launches, dtype, steps, fps, frames_per_step, stages=False):
+def roofline(launches, dtype, steps, fps, frames_per_step, stages=False, stage_workload="headline"):
     from m2s import _native
     stats = _native.aggregate(launches, "name")
     tot_ms = sum(s["ms"] for s in stats)
@@ -572,7 +609,7 @@ def roofline(launches, dtype, steps, fps, frames_per_step, stages=False):
     if traffic:
         r["traffic_over_compulsory_plus_spill"] = round(traffic / max(r["algorithmic_bytes_per_launch"] + r["spill_bytes_per_launch"], 1), 3)
     if stages:
-        r.update(stage_table(launches, steps))
+        r.update(stage_table(launches, steps, stage_workload))
     return r
 
 

@@ -764,8 +764,11 @@ void launch_tile(const ConvBatch& b, hipStream_t s, int phases, double flops, do
   int nks = 1;
   if (force > 0)
     nks = std::min(force, std::max(1, nst));
-  else if (2 * tiles <= slots && nst >= 8)
-    nks = std::max(1, std::min({slots / tiles, nst / 4, 16}));
+  else if (2 * tiles <= slots && nst >= 8) {
+    const char* mx = getenv("M2S_KSPLIT_MAX");  // A/B of the split count (tools/ab_env.py)
+    const char* ms = getenv("M2S_KSPLIT_MINST");
+    nks = std::max(1, std::min({slots / tiles, nst / (ms ? std::max(1, atoi(ms)) : 4), mx ? std::max(1, atoi(mx)) : 16}));
+  }
   const size_t part_bytes = (size_t)phases * nks * a.M * a.cs_out * sizeof(float);
   if (nks > 1 && part_bytes > ((size_t)256 << 20)) nks = 1;
   float* kpart = nks > 1 ? ksplit_scratch(s, part_bytes) : nullptr;

@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     ir_ws_kernel(const bf16_t* __restrict__ x, int N, int H, int cs_mid, const bf16_t* __restrict__ wpw,
                  const float* __restrict__ bpw, const float* __restrict__ wdw, const float* __restrict__ bdw,
                  bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, unsigned long long* __restrict__ trace,
-                 unsigned spin_max, unsigned* __restrict__ err, int pad_t, int pad_l) {
+                 unsigned spin_max, unsigned* __restrict__ err, int pad_t, int pad_l, int fm32) {
   static_assert(S == 1 || (S == 2 && W == 16), "stride 2: the 16-wide maps");
   constexpr int OWS = W / S;                      // output row width
   constexpr int OPB = (WS_BR / S) * OWS;          // output pixels of a full band
@@ -457,7 +457,8 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     TR(f, 4);
     const uint32_t pbase = (uint32_t)(d.img * PO + (r0 / S) * OWS);  // uniform
-    const uint32_t yoffb = __builtin_amdgcn_readfirstlane(4u * (uint32_t)c0) + 8u * (uint32_t)cg +
+    // fm32: plain fp32 rows (channel c at byte 4 c of its position), else the interleaved split layout
+    const uint32_t yoffb = __builtin_amdgcn_readfirstlane(4u * (uint32_t)c0) + (fm32 ? 16u : 8u) * (uint32_t)cg +
                            pbase * (4u * (uint32_t)cs_mid);  // launch_ir_ws: < 2^32
     const uint32_t yoff0 = yoffb + (uint32_t)cpo * (4u * (uint32_t)cs_mid);
     // lane = (4-channel plane cg, pixels cpl + 64 k): the plane's 9 taps stay in registers
@@ -490,11 +491,15 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
         a[j] = silu(a[j]);
         s[j] += a[j];
       }
-      uint2 hi, lo;  // the SE GEMM's interleaved operand: [hi 32 | lo 32] per 32-channel group
-      split4(a, hi, lo);
       char* u = reinterpret_cast<char*>(y) + (yoff0 + (uint32_t)k * 256u * (uint32_t)cs_mid);
-      *reinterpret_cast<uint2*>(u) = hi;
-      *reinterpret_cast<uint2*>(u + 64) = lo;
+      if (fm32) {
+        *reinterpret_cast<float4*>(u) = make_float4(a[0], a[1], a[2], a[3]);
+      } else {
+        uint2 hi, lo;  // the SE GEMM's interleaved operand: [hi 32 | lo 32] per 32-channel group
+        split4(a, hi, lo);
+        *reinterpret_cast<uint2*>(u) = hi;
+        *reinterpret_cast<uint2*>(u + 64) = lo;
+      }
     };
     // W = 16, full band: the lane's two pixels are vertically adjacent, (2 a, c) and (2 a + 1, c) for cpl =
     // 16 a + c, so their windows share two tap rows: 12 tile reads for both instead of 18
@@ -525,11 +530,15 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
           a[j] = silu(a[j]);
           s[j] += a[j];
         }
-        uint2 hi, lo;
-        split4(a, hi, lo);
         char* u = reinterpret_cast<char*>(y) + (yoffb + pos * (4u * (uint32_t)cs_mid));
-        *reinterpret_cast<uint2*>(u) = hi;
-        *reinterpret_cast<uint2*>(u + 64) = lo;
+        if (fm32) {
+          *reinterpret_cast<float4*>(u) = make_float4(a[0], a[1], a[2], a[3]);
+        } else {
+          uint2 hi, lo;
+          split4(a, hi, lo);
+          *reinterpret_cast<uint2*>(u) = hi;
+          *reinterpret_cast<uint2*>(u + 64) = lo;
+        }
       };
       out(a0, po);
       out(a1, po + 16u);
@@ -741,7 +750,8 @@ bool ir_ws_supported(int H, int W, int cs_in, int kp, int cs_mid) {
 
 void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_mid, const void* wpw, const float* bpw,
                   const float* wdw, const float* bdw, void* y, void* se_mean, double flops, double bytes,
-                  hipStream_t s, AsyncReport rep, int stride, int OH, int OW, int pad_t, int pad_l, double spill) {
+                  hipStream_t s, AsyncReport rep, int stride, int OH, int OW, int pad_t, int pad_l, double spill,
+                  bool fm32) {
   M2S_CHECK(stride == 1 ? ir_ws_supported(H, W, cs_in, kp, cs_mid)
                         : stride == 2 && ir_ws_s2_supported(H, W, cs_in, kp, cs_mid, OH, OW, pad_t, pad_l),
             "ir_ws: unsupported shape");
@@ -771,7 +781,7 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
     allow_lds(reinterpret_cast<const void*>(&ir_ws_kernel<W_, KS_, S_>));                             \
     ProfScope ps(NAME_, flops, bytes, s, spill);                                                        \
     hipLaunchKernelGGL((ir_ws_kernel<W_, KS_, S_>), grid, dim3(64 * (WS_NP + WS_NC)), L.total, s, xb, N, H, cs_mid, wb, \
-                       bpw, wdw, bdw, yb, mb, tr, rep.spin_max, rep.err, pad_t, pad_l);                  \
+                       bpw, wdw, bdw, yb, mb, tr, rep.spin_max, rep.err, pad_t, pad_l, fm32 ? 1 : 0);     \
     M2S_IRWS_DUMP(NAME_)                                                                                \
     M2S_HIP(hipGetLastError());                                                                         \
     return;                                                                                             \

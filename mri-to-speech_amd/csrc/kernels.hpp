@@ -80,8 +80,10 @@ void launch_se_gemm_sp(const void* x, int M, int P, int cs_in, const void* w, in
 bool se_ws_supported(int P, int cs_in, int cs_out);
 // Every FULL / FREE wait is bounded by rep.spin_max polls; a timeout is reported through rep.err and the
 // consumer's tiles from then on are stored as NaN.
+// x_f32: x holds plain fp32 rows [M][cs_in] (ir_ws's fm32 output) instead of the interleaved split layout.
 void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_pad, const float* bias, const void* gate,
-                  const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes, AsyncReport rep = {});
+                  const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes, AsyncReport rep = {},
+                  bool x_f32 = false);
 
 // fp8 engines: launch_se_gemm_f8's operation (e4m3 x8 / w8, bf16 gate / res / y) on the same warp-specialised
 // flag ring.  (se_ws.hip)
@@ -104,7 +106,9 @@ bool ir_ws_s2_supported(int H, int W, int cs_in, int kp, int cs_mid, int OH, int
 void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_mid, const void* wpw, const float* bpw,
                   const float* wdw, const float* bdw, void* y, void* se_mean, double flops, double bytes,
                   hipStream_t s, AsyncReport rep = {}, int stride = 1, int OH = 0, int OW = 0, int pad_t = 0,
-                  int pad_l = 0, double spill = 0.0);
+                  int pad_l = 0, double spill = 0.0, bool fm32 = false);
+// fm32: y is stored as plain fp32 rows [N * OH * OW][cs_mid] (for launch_se_ws(x_f32 = true)) instead of the
+// interleaved split layout: one 16-byte store per 4 channels, no split in the consumers.
 // Stride-2 IR front half on bands of 4 output rows (blocks.3.0: 32x32 -> 16x16), split fp32 or bf16: y =
 // the SE GEMM's operand (N, OH*OW, cs_mid; split: interleaved hi/lo), psum = squeeze partial sums
 // (N, OH / 4, cs_mid) for launch_se_mean.  wdw: fp32 tap-major [9][cs_mid].  (ir_s2band.hip)

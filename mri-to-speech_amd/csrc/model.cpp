@@ -84,6 +84,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_IR_WS")) ir_ws_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_IR_WS_S2")) ir_ws_s2_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_IRWS_MIN")) irws_min_ = std::atoi(e);
+  if (const char* e = std::getenv("M2S_IRWS_F32")) irws_f32_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_SEWS_MIN")) sews_min_cus_ = std::atoi(e);
   if (const char* e = std::getenv("M2S_STEM_FUSED")) stem_fused_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_F8_EXPAND")) f8_expand_ = std::strcmp(e, "0") != 0;
@@ -780,6 +781,13 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
         // bf16 feeds the fused kernel bf16 depthwise taps (dword halves), split fp32 the fp32 taps
         const void* wdw = arena_.ptr(SPL ? b.dw_w : b.dw_w2);
         const bool big = nc >= irws_min_;  // persistent ir_ws only where its one-image workgroups fill the chip
+        // the SE-gated conv_pwl runs on se_ws (below): then ir_ws hands it the expanded map as plain fp32 rows
+        // (one 16-byte store per 4 channels, no split; se_ws gates the fp32 value before its one split)
+        const bool sews = SPL && se_ws_ && se_ws_supported(nh * nw, cs, chan_stride(b.cout)) &&
+                          // se_ws runs one persistent workgroup per tile (256 rows; 128 at 8 x 8) up to one per CU:
+                          // below a full round of tiles the split-K conv_gemm SE GEMM fills the chip instead
+                          ceil_div(nc * nh * nw, nh * nw == 64 ? 128 : 256) >= sews_min_cus_ * device_cus();
+        bool mid_f32 = false;
         if (SPL && b.stride == 1 && ir_fused_ && ir_ws_ && big && ir_ws_supported(nh, nw, b.c1.cs_in, b.c1.kp, cs)) {
           const double P = (double)nh * nw;
           launch_ir_ws(cur, nc, nh, nw, b.c1.cs_in, b.c1.kp, cs, b.c1.w, b.c1.b, static_cast<const float*>(arena_.ptr(b.dw_w)),
@@ -788,7 +796,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                        // block input, the split expand weights, taps and biases, the SE means out; the depthwise output
                        // map is a spill (written here only for the SE-gated conv_pwl to read back: m2s.h spill_bytes)
                        4.0 * nc * P * b.c1.cin + 4.0 * b.mid * (b.c1.cin + 11.0) + 4.0 * nc * b.mid, s, ws_report(), 1, 0, 0,
-                       0, 0, 4.0 * nc * P * b.mid);
+                       0, 0, 4.0 * nc * P * b.mid, mid_f32 = sews && irws_f32_);
         } else if (FUSABLE && b.stride == 1 && ir_fused_ && ir_fused_supported(nh, nw, b.c1.cs_in, cs, SPL)) {
           const double P = (double)nh * nw, es = SPL ? 4.0 : 2.0;
           f8 = b.f8_pwl && se_gemm_f8_supported(nh * nw, cs, chan_stride(b.cout));
@@ -808,7 +816,7 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
           launch_ir_ws(cur, nc, oh, ow, b.c1.cs_in, b.c1.kp, cs, b.c1.w, b.c1.b, static_cast<const float*>(arena_.ptr(b.dw_w)),
                        static_cast<const float*>(arena_.ptr(b.dw_b)), M2, se_mean, 2.0 * nc * b.mid * (Pi * b.c1.cin + Po * 9),
                        4.0 * nc * Pi * b.c1.cin + 4.0 * b.mid * (b.c1.cin + 11.0) + 4.0 * nc * b.mid, s, ws_report(), 2, nh, nw,
-                       qt, ql, 4.0 * nc * Po * b.mid);
+                       qt, ql, 4.0 * nc * Po * b.mid, mid_f32 = sews && irws_f32_);
         } else if (FUSABLE && b.stride == 2 && ir_fused_ && ir_fused_s2_supported(oh, ow, b.c1.cs_in, cs, SPL) &&
                    nh * nw <= 64) {
           const double Pi = (double)oh * ow, Po = (double)nh * nw, es = SPL ? 4.0 : 2.0;
@@ -891,15 +899,12 @@ void Acoustic::effnet_t(const float* frames, int N, int H, int W, float* feats, 
                             rows * cs + 2.0 * rows * co * (b.skip ? 2.0 : 1.0) + (double)b.f8_npad * b.f8_kp +
                                 2.0 * nc * cs + (next8 ? rows * ld8 : 0.0),
                             next8, ld8);
-        } else if (SPL && se_ws_ && se_ws_supported(nh * nw, cs, chan_stride(b.cout)) &&
-                   // se_ws runs one persistent workgroup per tile (256 rows; 128 at 8 x 8) up to one per CU: below a
-                   // full round of tiles the split-K conv_gemm SE GEMM fills the chip instead
-                   ceil_div(nc * nh * nw, nh * nw == 64 ? 128 : 256) >= sews_min_cus_ * device_cus()) {
+        } else if (sews) {
           const double rows = (double)nc * nh * nw;
           launch_se_ws(M2, nc * nh * nw, nh * nw, cs, b.c2.w, b.c2.n_pad, b.c2.b, scale, b.skip ? cur : nullptr, nxt,
                        chan_stride(b.cout), s, 2.0 * rows * b.mid * b.cout,
                        4.0 * rows * b.mid + 4.0 * rows * b.cout * (b.skip ? 2.0 : 1.0) + 4.0 * b.cout * b.mid + 4.0 * nc * b.mid,
-                       ws_report());
+                       ws_report(), mid_f32);
         } else if (SPL && se_sp_ && se_gemm_sp_supported(nh * nw, cs, chan_stride(b.cout))) {
           const double rows = (double)nc * nh * nw, co = chan_stride(b.cout);
           launch_se_gemm_sp(M2, nc * nh * nw, nh * nw, cs, b.c2.w, b.c2.n_pad, b.c2.b, scale, b.skip ? cur : nullptr, nxt,

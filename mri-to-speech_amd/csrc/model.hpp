@@ -106,6 +106,8 @@ class Acoustic {
   // (ir_pwdw / ir_pwdw_s2, the split-K conv_gemm SE GEMM).  Env M2S_IRWS_MIN (images per pass) / M2S_SEWS_MIN (se_ws
   // tiles, in CUs: 1 = one full round) override.
   int irws_min_ = 512;
+  // ir_ws -> se_ws hand-off of the expanded map as plain fp32 rows instead of split pairs (env M2S_IRWS_F32=0: split)
+  bool irws_f32_ = true;
   int sews_min_cus_ = 1;
   bool stem_fused_ = true;  // bf16: stem + blocks.0 in one kernel (env M2S_STEM_FUSED=0 disables)
   bool f8_er_ = true;            // fp8: EdgeResidual blocks.1.1/.2 on e4m3 (env M2S_F8_ER=0: bf16 er_fused)

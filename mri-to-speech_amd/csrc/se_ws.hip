@@ -104,8 +104,13 @@ __device__ __forceinline__ int gate4_f8(int d, const float* s) {
 // engines' e4m3 form (K step = 128 e4m3 channels, v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales,
 // the gate applied to the e4m3 activation fragments in registers, wscale in the epilogue, bf16 in / out) of
 // gemm128.hip KIND_F8_SE, on the same ring.
-template <int WM, int WN, int NT, int NL, int NS, int IF, bool F8>
+// XF (split engine only): the activations are plain fp32 rows [M][cs_in] (ir_ws's expanded map, launch_ir_ws fm32):
+// a K step's 32 channels are still one 128-byte row, a fragment's 8 channels its chunks 2g, 2g + 1 (the e4m3 rows'
+// swizzle), and the gating multiplies the fp32 value before the one split -- no hi + lo sum, and ir_ws's consumers
+// store one 16-byte vector per 4 channels instead of splitting them.
+template <int WM, int WN, int NT, int NL, int NS, int IF, bool F8, bool XF = false>
 __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeWsArgs a) {
+  static_assert(!(F8 && XF), "fp32 activations: split engine");
   constexpr int NC = WM * WN;                       // consumer waves
   constexpr int BM = 64 * WM, BN = 16 * NT * WN, MT = 4;
   constexpr int BLK = (BN + BM) / 8;                // 8-row (1 KB) DMA blocks per step: weights, then activations
@@ -168,7 +173,7 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
           const int b = l + NL * j, r = b * 8 + lrow;
-          const int c = pch ^ swz_k<F8>(r & 15);
+          const int c = pch ^ ((XF && b >= BN / 8) ? swz_k<true>(r & 15) : swz_k<F8>(r & 15));
           const void* src;
           if (b < BN / 8) {
             src = F8 ? a.w + ((size_t)r * wrow_b + st * ROWB + c * 16)
@@ -208,6 +213,11 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
   const uint32_t sm0 = lds_u32(smem);
   const uint32_t a_lds0 = sm0 + (uint32_t)((wn * NT * 16 + r16) * ROWB);
   const uint32_t b_lds0 = sm0 + (uint32_t)((BN + wm * 64 + r16) * ROWB);
+  // XF: the activation rows' chunks (fp32 rows: chunks 2g, 2g + 1 under the e4m3 rows' swizzle), folded into the row base
+  // (one register more than the split form, whose 16 x 16 variant sits at 255)
+  const uint32_t bx0 = XF ? b_lds0 + (uint32_t)(((2 * g) ^ swz_k<true>(r16)) << 4) : 0u;
+  const uint32_t bx1 = XF ? b_lds0 + (uint32_t)(((2 * g + 1) ^ swz_k<true>(r16)) << 4) : 0u;
+  const uint32_t wa0 = XF ? a_lds0 + ch0 : 0u, wa1 = XF ? a_lds0 + ch1 : 0u;  // XF: the weight chunks folded likewise
   const uint32_t g_lds0 = lds_u32(gbuf) + (uint32_t)(g * (F8 ? 64 : 16));
   bool bad = false;  // a FULL wait (or a loader's FREE wait) timed out: this wave's tiles are stored as NaN from then on
   int s = 0;
@@ -289,7 +299,7 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
       // gates k = 32 st + 8 g + j (hi and lo halves) and the MT activation fragments first; their gating
       // runs while the NT weight fragments are read; the slot is released once those returned too
       u32x4 gh, glo, bh[MT], bl[MT], ah[NT], al[NT];
-      const uint32_t ga = gl + (uint32_t)(st * 64), ba0 = b_lds0 + so + ch0, ba1 = b_lds0 + so + ch1;
+      const uint32_t ga = gl + (uint32_t)(st * 64), ba0 = XF ? bx0 + so : b_lds0 + so + ch0, ba1 = XF ? bx1 + so : b_lds0 + so + ch1;
       const uint32_t gal = ga + (uint32_t)(a.cs_in * 2);  // the lo halves of the gate row
       asm volatile(
           "ds_read_b128 %0, %10\n\tds_read_b128 %1, %13\n\t"
@@ -303,8 +313,11 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
       static_assert(MT == 4, "the read statement above covers four 16-row fragments");
 #pragma unroll
       for (int ni = 0; ni < NT; ++ni) {
-        const uint32_t aa = a_lds0 + so + (uint32_t)(ni * 16 * ROWB);
-        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3" : "=&v"(ah[ni]), "=&v"(al[ni]) : "v"(aa + ch0), "v"(aa + ch1) : "memory");
+        const uint32_t aa = (XF ? so : a_lds0 + so) + (uint32_t)(ni * 16 * ROWB);
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3"
+                     : "=&v"(ah[ni]), "=&v"(al[ni])
+                     : "v"(XF ? wa0 + aa : aa + ch0), "v"(XF ? wa1 + aa : aa + ch1)
+                     : "memory");
       }
       // gate hi + lo (fp32), gated activations re-split (17 significant bits kept)
       float gsc[8], gl8[8];
@@ -317,13 +330,22 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
       // per activation fragment: gate + re-split, then its NT x 3 MFMAs (the next fragment's VALU
       // overlaps them); the slot is released after the first fragment, once the weight reads returned
       auto gate_frag = [&](int mi, bf16x8& xh, bf16x8& xl) {
-        float v[8], w[8];
-        unpack_bf16x4(make_uint2(bh[mi][0], bh[mi][1]), v);
-        unpack_bf16x4(make_uint2(bh[mi][2], bh[mi][3]), v + 4);
-        unpack_bf16x4(make_uint2(bl[mi][0], bl[mi][1]), w);
-        unpack_bf16x4(make_uint2(bl[mi][2], bl[mi][3]), w + 4);
+        float v[8];
+        if constexpr (XF) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (v[j] + w[j]) * gsc[j];
+          for (int j = 0; j < 4; ++j) {
+            v[j] = __uint_as_float(bh[mi][j]) * gsc[j];
+            v[4 + j] = __uint_as_float(bl[mi][j]) * gsc[4 + j];
+          }
+        } else {
+          float w[8];
+          unpack_bf16x4(make_uint2(bh[mi][0], bh[mi][1]), v);
+          unpack_bf16x4(make_uint2(bh[mi][2], bh[mi][3]), v + 4);
+          unpack_bf16x4(make_uint2(bl[mi][0], bl[mi][1]), w);
+          unpack_bf16x4(make_uint2(bl[mi][2], bl[mi][3]), w + 4);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (v[j] + w[j]) * gsc[j];
+        }
         uint2 h0, l0, h1, l1;
         split4(v, h0, l0);
         split4(v + 4, h1, l1);
@@ -445,11 +467,11 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
   }
 }
 
-template <int WM, int WN, int NT, int NL, int NS, int IF, bool F8 = false>
+template <int WM, int WN, int NT, int NL, int NS, int IF, bool F8 = false, bool XF = false>
 void launch_cfg(SeWsArgs& a, hipStream_t s, double flops, double bytes) {
   static_assert(IF <= 3, "tail waits");
   constexpr int BM = 64 * WM, BN = 16 * NT * WN;
-  const void* fn = reinterpret_cast<const void*>(&se_ws_kernel<WM, WN, NT, NL, NS, IF, F8>);
+  const void* fn = reinterpret_cast<const void*>(&se_ws_kernel<WM, WN, NT, NL, NS, IF, F8, XF>);
   allow_lds(fn);
   const int nimg = BM / a.P > 0 ? BM / a.P : 1;
   const int gimg = ((F8 ? a.cs_in * 2 : a.cs_in * 4) + 1023) / 1024 * 1024;
@@ -460,11 +482,14 @@ void launch_cfg(SeWsArgs& a, hipStream_t s, double flops, double bytes) {
   M2S_CHECK((F8 ? a.kp / 128 : a.cs_in / 32) >= NS, "se_ws: K steps per tile >= ring slots (gate rows are double-buffered per tile)");
   a.n_tiles_m = ceil_div(a.M, BM);
   const dim3 grid(std::min(a.n_tiles_m, device_cus()));
-  char name[64];
-  snprintf(name, sizeof(name), "se_ws_kernel<%d, %d, %d, %d, %d, %d, %s>", WM, WN, NT, NL, NS, IF,
-           F8 ? "true" : "false");  // rocprof's symbol
+  char name[72];
+  if (XF)
+    snprintf(name, sizeof(name), "se_ws_kernel<%d, %d, %d, %d, %d, %d, false, true>", WM, WN, NT, NL, NS, IF);
+  else
+    snprintf(name, sizeof(name), "se_ws_kernel<%d, %d, %d, %d, %d, %d, %s>", WM, WN, NT, NL, NS, IF,
+             F8 ? "true" : "false");  // rocprof's symbol
   ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((se_ws_kernel<WM, WN, NT, NL, NS, IF, F8>), grid, dim3(64 * (WM * WN + NL)), lds, s, a);
+  hipLaunchKernelGGL((se_ws_kernel<WM, WN, NT, NL, NS, IF, F8, XF>), grid, dim3(64 * (WM * WN + NL)), lds, s, a);
   M2S_HIP(hipGetLastError());
 }
 
@@ -475,7 +500,8 @@ bool se_ws_supported(int P, int cs_in, int cs_out) {
 }
 
 void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_pad, const float* bias, const void* gate,
-                  const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes, AsyncReport rep) {
+                  const void* res, void* y, int cs_out, hipStream_t s, double flops, double bytes, AsyncReport rep,
+                  bool x_f32) {
   M2S_CHECK(se_ws_supported(P, cs_in, cs_out) && M % P == 0 && cs_out % 4 == 0, "se_ws: unsupported shape");
   M2S_CHECK(x && w && bias && gate && y && y != res && y != x, "se_ws: operand pointers");
   M2S_CHECK((double)M * cs_in * 4 < 2147483647.0 * 2, "se_ws: input too large");
@@ -499,6 +525,14 @@ void launch_se_ws(const void* x, int M, int P, int cs_in, const void* w, int n_p
     const char* e = std::getenv("M2S_SE_WS_CFG");
     return e ? std::atoi(e) : 0;
   }();
+  if (x_f32) {  // fp32 activations (ir_ws fm32): the default tiles only
+    if (cs_out <= 128) {
+      M2S_CHECK(n_pad >= 128, "se_ws: weight rows");
+      return launch_cfg<4, 1, 8, 4, 3, 2, false, true>(a, s, flops, bytes);
+    }
+    M2S_CHECK(n_pad >= 224, "se_ws: weight rows");
+    return launch_cfg<2, 2, 7, 4, 3, 2, false, true>(a, s, flops, bytes);
+  }
   if (cs_out <= 128) {
     M2S_CHECK(n_pad >= 128, "se_ws: weight rows");
     switch (cfg) {

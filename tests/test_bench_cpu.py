@@ -169,3 +169,18 @@ def test_ragged_bench_step_gloo(world):
     res = sorted(q.get(timeout=10) for _ in range(world))
     assert all(ok for _, ok in res), res
     assert sorted(set(bench.ragged_lengths(64, 30))) == [24, 30, 36]
+
+
+def test_cpu_baseline_reports_every_config_and_stage():
+    """BASELINE.md's CPU plan: C3 end to end with per-stage wall time (CNN / BiLSTM / head + glue / Generator), C1 (mel
+    only) from the same runs, C5 (one long clip); the thread count and why.  Tiny shapes here (the oracle on CPU)."""
+    from m2s import synth
+    args = bench.parse(["--frames", "3", "--hw", "64", "--cpu-seconds", "0.01", "--cpu-long-frames", "5"])
+    ac, gen = synth.synth_acoustic_state(0), synth.synth_generator_state(0)
+    mean, std = synth.synth_scaler()
+    r = bench.cpu_baseline(args, ac, gen, mean, std)
+    assert r["kind"] == "port" and r["cores"] >= 1 and r["value"] > 0 and "threads_note" in r
+    per = r["per_config"]
+    assert set(per) == {"C1", "C3", "C5"}
+    assert set(per["C3"]["stage_ms_per_clip"]) == {"cnn", "bilstm", "head_glue", "generator"}
+    assert per["C1"]["frames_per_s"] >= per["C3"]["frames_per_s"] > 0 and per["C5"]["rtf"] > 0

@@ -123,6 +123,7 @@ def test_ir_ws_matches_grid_kernel(rt, ac_state, monkeypatch, hw, n):
     tools/diag_ir_ws.py), so the bar is the parity bar, 1e-4."""
     fr = torch.from_numpy(synth.synth_frames(1, n, hw=hw, seed=7)[0]).to(DEV)
     monkeypatch.setenv("M2S_IRWS_MIN", "0")  # ir_ws at any pass size (the product runs it from 512 frames a pass)
+    monkeypatch.setenv("M2S_SEWS_MIN", "0")  # and se_ws after it, so ir_ws hands over fp32 rows (fm32) at both sizes
     ws = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
     monkeypatch.setenv("M2S_IR_WS", "0")
     grid = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
@@ -265,3 +266,26 @@ def test_se_ws_matches_barrier_ring(rt, ac_state, monkeypatch, n):
         ref = effnet.effnet_gap(sd, fr.cpu()).numpy()
         assert _rel(ws.effnet(fr).cpu().numpy(), ref) <= 1e-4
 
+
+
+@pytest.mark.parametrize("n", [520])
+def test_ir_ws_fp32_handoff_matches_split(rt, ac_state, monkeypatch, n):
+    """ir_ws -> se_ws hands the expanded depthwise map over as plain fp32 rows (launch_ir_ws fm32, se_ws XF): one
+    16-byte store per 4 channels and no split in ir_ws's consumers, the gate applied to the fp32 value before se_ws's
+    one split.  Against the split hand-off (M2S_IRWS_F32=0) the only difference is the dropped 17-bit rounding of the
+    map, so every tap agrees within the parity bar; the launch log shows the XF se_ws."""
+    from m2s import _native
+    fr = torch.from_numpy(synth.synth_frames(1, n, seed=43)[0]).to(DEV)
+    f32 = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    monkeypatch.setenv("M2S_IRWS_F32", "0")
+    spl = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    _native.prof_enable(True)
+    f32.effnet(fr)
+    torch.cuda.synchronize()
+    names = {r["name"] for r in _native.prof_launches()}
+    _native.prof_enable(False)
+    assert any(k.startswith("ir_ws_kernel") for k in names), names
+    assert any(k.endswith("false, true>") and k.startswith("se_ws_kernel") for k in names), names
+    for i in (13, 18, 19, 20, 28):  # after blocks 4.0, 4.5, 5.0 (stride 2), 5.1, 5.9
+        a, b = f32.probe(fr, i).cpu().numpy(), spl.probe(fr, i).cpu().numpy()
+        assert np.isfinite(a).all() and _rel(a, b) <= 1e-4, f"tap {i}: {_rel(a, b)}"

@@ -84,13 +84,14 @@ def stage_counters(d, st_map):
     return agg
 
 
-def stages(src, sha, prefix):
-    """<prefix>_stages.json: per stage of the path (libm2s's StageTag labels: cnn, bilstm, mrf_c<C>, ...), HBM
-    bytes per step (FETCH_SIZE x2 + WRITE_SIZE, KiB -> bytes), MFMA utilisation and VALU per MFMA."""
+def stages(src, sha, prefix, suffix="", workload="headline"):
+    """<prefix>_stages.json (suffix "8": <prefix>_c4fp8_stages.json from the fp8 engine's passes at configs[4]'s
+    8 x 1000 frames): per stage of the path (libm2s's StageTag labels: cnn, bilstm, mrf_c<C>, ...), HBM bytes per
+    step (FETCH_SIZE x2 + WRITE_SIZE, KiB -> bytes), MFMA utilisation and VALU per MFMA."""
     res = collections.defaultdict(dict)
     notes = {}
     for pas in ("fetch", "write", "mfma", "valu"):
-        d = os.path.join(src, pas)
+        d = os.path.join(src, pas + suffix)
         st_map, steps, matched, n = dispatch_stages(d)
         if st_map is None:
             return None
@@ -113,9 +114,11 @@ def stages(src, sha, prefix):
         r["hbm_bytes_per_step"] = r.get("fetch_bytes_per_step", 0.0) + r.get("write_bytes_per_step", 0.0)
         mi = r.get("mfma_insts_per_step")
         r["valu_per_mfma"] = round(r.get("valu_insts_per_step", 0.0) / mi, 2) if mi else None
-    meta = {"src_sha": sha, "source": f"rocprofv3 --pmc passes in {src} (tools/gpu_evidence.sh, tools/profile_step.py "
-            "bench workload), dispatches aligned with libm2s's stage-tagged launch log", "alignment": notes}
-    with open(prefix + "_stages.json", "w") as fh:
+    meta = {"src_sha": sha, "workload": workload,
+            "source": f"rocprofv3 --pmc passes in {src} (tools/gpu_evidence.sh, tools/profile_step.py "
+            f"{'bench workload' if workload == 'headline' else workload}), dispatches aligned with libm2s's stage-tagged "
+            "launch log", "alignment": notes}
+    with open(prefix + ("_c4fp8" if suffix else "") + "_stages.json", "w") as fh:
         json.dump({"meta": meta, "stages": res}, fh, indent=1)
     return res
 
@@ -164,10 +167,10 @@ def main(src, prefix):
     with open(prefix + "_sq_mfma.txt", "w") as fh:
         fh.write("\n".join(lines) + "\n")
     print("\n".join(lines[:40]))
-    st = stages(src, sha, prefix)
-    if st:
-        for k, v in st.items():
-            print(f"stage {k:10s} hbm {v['hbm_bytes_per_step'] / 1e6:9.1f} MB/step  mfma {v.get('mfma_util')}  "
+    for suffix, wl in (("", "headline"), ("8", "configs4_fp8")):
+        st = stages(src, sha, prefix, suffix, wl)
+        for k, v in (st or {}).items():
+            print(f"{wl} stage {k:10s} hbm {v['hbm_bytes_per_step'] / 1e6:9.1f} MB/step  mfma {v.get('mfma_util')}  "
                   f"valu/mfma {v.get('valu_per_mfma')}")
 
 

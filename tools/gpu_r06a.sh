@@ -6,7 +6,7 @@ TAG=${1:-r06a}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_bf16x3.py tests/test_gpu_parity.py -m gpu -x -q \
+timeout -k 10 900 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_bf16x3.py tests/test_gpu_parity.py tests/test_gpu_ops.py tests/test_gpu_plugin.py -m gpu -x -q \
   --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
 tail -3 "$OUT/pytest.log"
 bash tools/gpu_small.sh "$TAG/small" || exit 1
