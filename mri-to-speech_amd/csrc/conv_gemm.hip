@@ -753,7 +753,9 @@ void launch_tile(const ConvBatch& b, hipStream_t s, int phases, double flops, do
   const size_t lds = (size_t)S * (R * (BM + BN) + 16) * ROW + (size_t)se_imgs * a.cs_in * sizeof(float);
   M2S_CHECK(lds <= 160 * 1024, "conv_gemm: LDS budget");
   // Split K where the tiles fill under half a round of the chip's workgroup slots (one clip, the 8 x 4 acoustic
-  // batch: a few dozen tiles walking 20..88 K steps each): nks K ranges of >= 4 steps, up to a full round.
+  // batch: a few dozen tiles walking 20..88 K steps each): nks K ranges of >= 4 steps, up to a full round and at
+  // most 8 (the partial sums' round trip grows with nks: same-box A/B at one clip / configs[1], M2S_KSPLIT_MAX 4 / 8
+  // / 16: 2.378 / 2.286 / 2.300 ms and 1.106 / 1.107 / 1.119 ms, gpurun_out/r06d/ab.txt).
   // M2S_KSPLIT=n forces n ranges (A/B, tests; 1 = never split).
   int nst = 0;
   for (int i = 0; i < (KIND == KIND_CONV1D ? phases : 1); ++i) nst = std::max(nst, b.a[i].kp / 32);
@@ -767,7 +769,7 @@ void launch_tile(const ConvBatch& b, hipStream_t s, int phases, double flops, do
   else if (2 * tiles <= slots && nst >= 8) {
     const char* mx = getenv("M2S_KSPLIT_MAX");  // A/B of the split count (tools/ab_env.py)
     const char* ms = getenv("M2S_KSPLIT_MINST");
-    nks = std::max(1, std::min({slots / tiles, nst / (ms ? std::max(1, atoi(ms)) : 4), mx ? std::max(1, atoi(mx)) : 16}));
+    nks = std::max(1, std::min({slots / tiles, nst / (ms ? std::max(1, atoi(ms)) : 4), mx ? std::max(1, atoi(mx)) : 8}));
   }
   const size_t part_bytes = (size_t)phases * nks * a.M * a.cs_out * sizeof(float);
   if (nks > 1 && part_bytes > ((size_t)256 << 20)) nks = 1;

@@ -102,15 +102,30 @@ __global__ void __launch_bounds__(256) stem32_kernel(const float* __restrict__ f
 }
 
 // ---------------------------------------------------------------------------------------------
+// One image per workgroup: lane = channel (64 at a time), the four waves take every fourth position and their
+// partial sums meet in LDS in a fixed order (one thread per (image, channel) walking all P positions made a
+// 32-frame batch a 26-workgroup, 20 us launch)
 template <typename T>
 __global__ void __launch_bounds__(256) gap_kernel(const T* __restrict__ x, int N, int P, int C, int cs,
                                                   float* __restrict__ feats) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long)N * C) return;
-  const int n = (int)(i / C), c = (int)(i - (long)(i / C) * C);
-  float acc = 0.f;
-  for (int k = 0; k < P; ++k) acc += act_ld<T>(x, (long)n * P + k, cs, c);
-  feats[i] = acc / (float)P;
+  __shared__ float part[4][64];
+  const int n = blockIdx.x, q = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    const int c = c0 + l;
+    float a0 = 0.f, a1 = 0.f;
+    if (c < C) {
+      int k = q;
+      for (; k + 4 < P; k += 8) {
+        a0 += act_ld<T>(x, (long)n * P + k, cs, c);
+        a1 += act_ld<T>(x, (long)n * P + k + 4, cs, c);
+      }
+      if (k < P) a0 += act_ld<T>(x, (long)n * P + k, cs, c);
+    }
+    if (c0 > 0) __syncthreads();  // the previous channel block's partials were read
+    part[q][l] = a0 + a1;
+    __syncthreads();
+    if (q == 0 && c < C) feats[(long)n * C + c] = ((part[0][l] + part[1][l]) + (part[2][l] + part[3][l])) / (float)P;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -358,7 +373,8 @@ void launch_stem(const float* frames, int N, int H, int W, int OH, int OW, int p
 
 template <typename T>
 void launch_gap(const T* x, int N, int P, int C, int cs, float* feats, hipStream_t s) {
-  hipLaunchKernelGGL(gap_kernel<T>, dim3(nblk((long)N * C)), dim3(256), 0, s, x, N, P, C, cs, feats);
+  if (N <= 0) return;
+  hipLaunchKernelGGL(gap_kernel<T>, dim3(N), dim3(256), 0, s, x, N, P, C, cs, feats);
   M2S_HIP(hipGetLastError());
 }
 

@@ -255,8 +255,12 @@ __global__ void __launch_bounds__(RB_NW * 64) rb1_fused_kernel(const RbArgs a) {
   const bf16_t* xc = a.x + (size_t)clip * a.L * C * HR;
 
   // ---- A = lrelu(x) for rows [-16, R) (guard rows and t outside the clip: zeros); T = 0; biases -
+  // 16 consecutive lanes take 16 consecutive rows of one plane (ROWS % 16 == 0: rb_history rounds H to 16), so each
+  // ds_write_b128 lane group fills 16 distinct bank slots; with the planes of one row on consecutive lanes (the planes
+  // lie a multiple of 256 B apart) every store was 4-way conflicted: 0.7 / 1.0 / 1.6 conflict cycles per LDS
+  // instruction at k = 11 / 7 / 3 (profiles/r05fin6_sq_mfma.txt)
   for (int i = tid; i < ROWS * NPL; i += RB_NW * 64) {
-    const int pr = i / NPL, c = i - pr * NPL, t = t0 + pr - 16;
+    const int pr = (i / (16 * NPL)) * 16 + (i & 15), c = (i >> 4) % NPL, t = t0 + pr - 16;
     if constexpr (SP) {
       uint2 h0 = make_uint2(0u, 0u), l0 = h0, h1 = h0, l1 = h0;
       if (pr >= 16 && t >= 0 && t < a.L) {

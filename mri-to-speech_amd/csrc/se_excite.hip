@@ -68,6 +68,19 @@ __global__ void __launch_bounds__(64 * NW) se_excite_kernel(const bf16_t* __rest
   const int g = lane >> 4, r16 = lane & 15;
   const int n0 = blockIdx.x * SE_IMG;
   const bool img_ok = n0 + r16 < N;
+  // the expand weights of this wave's first channel tile, fetched before the reduce so their latency hides under it
+  // (a small batch's launch is a chain of dependent load round trips)
+  const int nks = kp2 / 32, ntile = cs_mid / 16, t_first = NW * blockIdx.y + wave;
+  bf16x8 pa[SE_RDMAX / 32], pal[SE_RDMAX / 32];
+  {
+    const int c = 16 * t_first + r16;
+#pragma unroll
+    for (int ks = 0; ks < SE_RDMAX / 32; ++ks) {
+      const bf16_t* wp = w2 + (size_t)c * kp2 * R + 32 * ks + 8 * g;
+      pa[ks] = ld8(wp, t_first < ntile && c < mid && ks < nks);
+      if constexpr (SP) pal[ks] = ld8(wp + kp2, t_first < ntile && c < mid && ks < nks);
+    }
+  }
 
   // ---- conv_reduce + SiLU: RT = ceil(rd / 16) row tiles; the NW waves split K NW / RT ways -------
   // (wave w: row tile w % RT, k-steps w / RT, w / RT + KSP, ...), partials summed in LDS in a fixed
@@ -124,8 +137,6 @@ __global__ void __launch_bounds__(64 * NW) se_excite_kernel(const bf16_t* __rest
     hb[ks] = *reinterpret_cast<const bf16x8*>(&hid[0][r16][32 * ks + 8 * g]);
     if constexpr (SP) hl[ks] = *reinterpret_cast<const bf16x8*>(&hid[R - 1][r16][32 * ks + 8 * g]);
   }
-  const int nks = kp2 / 32;
-  const int ntile = cs_mid / 16;
   // channel tiles dealt over the gridDim.y workgroups of these images and their 4 waves (tile
   // 4 * (y + gridDim.y * v) + wave); 4 tiles per batch, all their weight fragments loaded first
   const int ts = NW * gridDim.y;
@@ -136,6 +147,11 @@ __global__ void __launch_bounds__(64 * NW) se_excite_kernel(const bf16_t* __rest
       const int c = 16 * (t0 + ts * u) + r16;  // weight row of this lane's A fragment
 #pragma unroll
       for (int ks = 0; ks < SE_RDMAX / 32; ++ks) {
+        if (u == 0 && t0 == t_first) {  // prefetched
+          a[u][ks] = pa[ks];
+          if constexpr (SP) al[u][ks] = pal[ks];
+          continue;
+        }
         const bf16_t* wp = w2 + (size_t)c * kp2 * R + 32 * ks + 8 * g;
         a[u][ks] = ld8(wp, c < mid && ks < nks);
         if constexpr (SP) al[u][ks] = ld8(wp + kp2, c < mid && ks < nks);

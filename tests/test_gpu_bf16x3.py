@@ -254,6 +254,7 @@ def test_se_ws_matches_barrier_ring(rt, ac_state, monkeypatch, n):
     monkeypatch.setenv("M2S_SE_WS", "1")
     monkeypatch.setenv("M2S_SEWS_MIN", "0")  # se_ws at any pass size (the product runs it from a full round of tiles)
     monkeypatch.setenv("M2S_KSPLIT", "1")    # the barrier ring unsplit: the same K order as the flag ring
+    monkeypatch.setenv("M2S_IRWS_F32", "0")  # and the same split operand (ir_ws at 600 frames hands se_ws fp32 rows)
     ws = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
     monkeypatch.setenv("M2S_SE_WS", "0")
     ring = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
