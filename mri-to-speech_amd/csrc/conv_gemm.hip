@@ -704,13 +704,27 @@ __global__ void __launch_bounds__(256) conv_gemm_ksum_kernel(const ConvBatch ab,
 }
 
 // Split-K partial sums live in one device buffer per (device, stream), grown on demand (only small grids split,
-// so it stays a few MB); launches on one stream are ordered, so one buffer per stream is race-free.
+// so it stays a few MB); launches on one stream are ordered, so one buffer per stream is race-free.  A stream under
+// HIP graph capture cannot allocate: it borrows the device's largest buffer (the eager warm-up calls made it) and,
+// if none is large enough, gets nullptr, and the launch runs unsplit.
 float* ksplit_scratch(hipStream_t s, size_t bytes) {
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> bufs;
   int dev = 0;
   M2S_HIP(hipGetDevice(&dev));
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  M2S_HIP(hipStreamIsCapturing(s, &cap));
   std::lock_guard<std::mutex> g(mu);
+  if (cap != hipStreamCaptureStatusNone) {
+    void* best = nullptr;
+    size_t best_sz = 0;
+    for (auto& kv : bufs)
+      if (kv.first.first == dev && kv.second.second > best_sz) {
+        best = kv.second.first;
+        best_sz = kv.second.second;
+      }
+    return best_sz >= bytes ? static_cast<float*>(best) : nullptr;
+  }
   auto& b = bufs[{dev, s}];
   if (b.second < bytes) {
     if (b.first) {
@@ -774,6 +788,7 @@ void launch_tile(const ConvBatch& b, hipStream_t s, int phases, double flops, do
   const size_t part_bytes = (size_t)phases * nks * a.M * a.cs_out * sizeof(float);
   if (nks > 1 && part_bytes > ((size_t)256 << 20)) nks = 1;
   float* kpart = nks > 1 ? ksplit_scratch(s, part_bytes) : nullptr;
+  if (!kpart) nks = 1;  // (a stream under graph capture with no scratch large enough)
   dim3 grid(m_tiles * n_tiles, nks, phases);
   char name[96];
   static const bool detail = getenv("M2S_PROF_DETAIL") != nullptr;

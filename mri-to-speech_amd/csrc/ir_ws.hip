@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     ir_ws_kernel(const bf16_t* __restrict__ x, int N, int H, int cs_mid, const bf16_t* __restrict__ wpw,
                  const float* __restrict__ bpw, const float* __restrict__ wdw, const float* __restrict__ bdw,
                  bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, unsigned long long* __restrict__ trace,
-                 unsigned spin_max, unsigned* __restrict__ err, int pad_t, int pad_l, int fm32) {
+                 unsigned spin_max, unsigned* __restrict__ err, int pad_t, int pad_l, int fm32, int n_full, int parts) {
   static_assert(S == 1 || (S == 2 && W == 16), "stride 2: the 16-wide maps");
   constexpr int OWS = W / S;                      // output row width
   constexpr int OPB = (WS_BR / S) * OWS;          // output pixels of a full band
@@ -182,8 +182,24 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const bool prod = wave < WS_NP;
-  const int n_units = blockIdx.x < N ? (N - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  const int T = n_units * NB * NS;
+  // Work units, dealt round-robin over the workgroups: images 0 .. n_full - 1 whole, then the tail images cut into
+  // `parts` slice ranges each (launch_ir_ws: 1920 images on 256 CUs were 7 or 8 images a workgroup, 6 % of the
+  // launch idle; 1792 whole + 128 halves are 7.5 each).  Every slice of an image still runs all its bands in one
+  // workgroup, so its squeeze stays in that workgroup's LDS.
+  const int n_units = n_full + (N - n_full) * parts;
+  struct Unit {
+    int img, lo, hi;  // image and slice range [lo, hi)
+  };
+  auto unit_of = [&](int u) {
+    if (u < n_full) return Unit{u, 0, NS};
+    const int q = u - n_full, pt = q % parts;
+    return Unit{n_full + q / parts, pt * NS / parts, (pt + 1) * NS / parts};
+  };
+  int T = 0;
+  for (int u = blockIdx.x; u < n_units; u += gridDim.x) {
+    const Unit un = unit_of(u);
+    T += NB * (un.hi - un.lo);
+  }
 
   auto TR = [&](int i, int k) {
 #ifdef IRWS_TRACE
@@ -195,17 +211,19 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     (void)i; (void)k; (void)trace;
 #endif
   };
-  // (image, band, slice) of a flat step, advanced incrementally (no integer divisions per step)
+  // (image, band, slice) of a flat step, advanced incrementally (a division only at a unit's end); lo / hi: the
+  // unit's slice range, u: the unit
   struct Step {
-    int img, band, sl;
+    int img, band, sl, lo, hi, u;
+  };
+  auto first_step = [&](int u) {
+    const Unit un = unit_of(u);
+    return Step{un.img, 0, un.lo, un.lo, un.hi, u};
   };
   auto next_step = [&](Step d) {
-    if (++d.sl == NS) {
-      d.sl = 0;
-      if (++d.band == NB) {
-        d.band = 0;
-        d.img += gridDim.x;
-      }
+    if (++d.sl == d.hi) {
+      d.sl = d.lo;
+      if (++d.band == NB) d = first_step(d.u + (int)gridDim.x);
     }
     return d;
   };
@@ -612,7 +630,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   __syncthreads();  // the counters and the tiles' zero halo columns
   if (prod) {
     __builtin_amdgcn_s_setprio(2);
-    Step cur{(int)blockIdx.x, 0, 0};
+    Step cur = first_step(blockIdx.x);
     if (T > 0) issue_w(0, cur);
     if (T > 1) issue_w(1, next_step(cur));
     if (TAPS_AHEAD && T > 0 && tap_wave) issue_wd(0, cur);
@@ -626,7 +644,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     for (int i = 0; i < T; ++i) {
       const Step nxt = next_step(cur), nxt2 = next_step(nxt);
       TR(i, 0);
-      if (cur.sl == 0) {  // a new band: its input rows, once every producer is done with the last band's
+      if (cur.sl == cur.lo) {  // a new band: its input rows, once every producer is done with the last band's
         if (i > 0) wait_ge(pdone, (unsigned)(WS_NP * i));
         issue_x(cur.img, cur.band);
         wait_vm0();
@@ -672,7 +690,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       cur = nxt;
     }
   } else {
-    Step cur{(int)blockIdx.x, 0, 0};
+    Step cur = first_step(blockIdx.x);
     for (int i = 0; i < T; ++i) {
       wait_ge(tfull, (unsigned)(WS_NP * (i + 1)));  // tile i and taps i
       consume(i, cur);
@@ -760,6 +778,15 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
   const WsLayout L = ws_layout(H, W, cs_in, cs_mid, stride);
   const int n_cu = device_cus();
   const dim3 grid(std::min(N, n_cu));
+  // tail balancing (kernel comment): whole images up to a multiple of the grid, the rest in `parts` slice ranges,
+  // parts ~ grid / tail images so the units come to a whole number of rounds; a range keeps >= 3 slices (the
+  // squeeze's reuse distance; each range of a band reloads the band's input rows)
+  const int G = (int)grid.x, NSl = cs_mid / WS_SL;
+  const int n_full = N / G * G, rem = N - n_full;
+  int parts = rem > 0 ? std::max(1, (G + rem / 2) / rem) : 1;
+  parts = std::max(1, std::min(parts, NSl / 3));
+  if (const char* e = getenv("M2S_IRWS_PARTS"))  // A/B: n = n ranges (1 = no tail split), 0 = the rule above
+    if (atoi(e) > 0) parts = std::min(atoi(e), std::max(1, NSl / 3));
 #ifdef IRWS_TRACE
   static unsigned long long* tr = [] {
     unsigned long long* p = nullptr;
@@ -781,7 +808,7 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
     allow_lds(reinterpret_cast<const void*>(&ir_ws_kernel<W_, KS_, S_>));                             \
     ProfScope ps(NAME_, flops, bytes, s, spill);                                                        \
     hipLaunchKernelGGL((ir_ws_kernel<W_, KS_, S_>), grid, dim3(64 * (WS_NP + WS_NC)), L.total, s, xb, N, H, cs_mid, wb, \
-                       bpw, wdw, bdw, yb, mb, tr, rep.spin_max, rep.err, pad_t, pad_l, fm32 ? 1 : 0);     \
+                       bpw, wdw, bdw, yb, mb, tr, rep.spin_max, rep.err, pad_t, pad_l, fm32 ? 1 : 0, n_full, parts); \
     M2S_IRWS_DUMP(NAME_)                                                                                \
     M2S_HIP(hipGetLastError());                                                                         \
     return;                                                                                             \

@@ -37,5 +37,6 @@ for dt in dtypes:
         engs[v] = rt.AcousticEngine(st, dtype=dt, device=dev)
     for rnd in range(2):
         for v, e in engs.items():
+            os.environ[var] = v  # (switches read per launch, e.g. M2S_IRWS_PARTS, take the engine's value here too)
             print(f"{var}={v} {dt:7s} probe({nb}) {timed(lambda: e.probe(x, nb)):7.3f} ms  cnn {timed(lambda: e.effnet(x)):7.3f} ms",
                   flush=True)
