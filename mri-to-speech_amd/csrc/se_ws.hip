@@ -80,6 +80,8 @@ struct SeWsArgs {
   bf16_t* y;              // split output; F8: bf16 [M][cs_out]
   uint8_t* y8;            // F8: e4m3 copy of y (the next IR block's expand operand, rows of ld8 bytes) or null
   int M, P, cs_in, cs_out, n_tiles_m, kp;  // kp: F8 weight row bytes (cs_in rounded up to 128)
+  // tail balancing: tiles >= full_tiles are half tiles of BM / 2 rows (n_tiles_m counts both kinds), launch_cfg
+  int full_tiles;
   int ld8;
   unsigned spin_max;  // polls per flag wait before it times out
   unsigned* err;      // host-mapped error word (M2S_ASYNC_WS on a timeout) or null
@@ -131,6 +133,12 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
   const int nsteps = F8 ? a.kp / 128 : a.cs_in / 32;
   const int n_tiles = a.n_tiles_m;                  // one n tile: BN covers cs_out
   const int my_tiles = (int)blockIdx.x < n_tiles ? (n_tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  // tile -> first row and row end: BM rows, or BM / 2 past full_tiles (the last round's tail, split so that the
+  // workgroups' tile counts even out: 1920 16x16 images on 256 CUs were 7 or 8 tiles a workgroup)
+  auto tile_rows = [&](int tile, int& m0, int& mend) {
+    m0 = tile < a.full_tiles ? tile * BM : a.full_tiles * BM + (tile - a.full_tiles) * (BM / 2);
+    mend = min(m0 + (tile < a.full_tiles ? BM : BM / 2), a.M);
+  };
 
   if (tid <= 2 * NS) flags[tid] = 0u;  // FULL, FREE and the loaders' poison word
   __syncthreads();  // the only workgroup barrier
@@ -147,7 +155,8 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
     int s = 0;
     for (int it = 0; it < my_tiles; ++it) {
       const int tile = blockIdx.x + it * gridDim.x;
-      const int m0 = tile * BM;
+      int m0, mend;
+      tile_rows(tile, m0, mend);
       const uint8_t* xt = a.x + (size_t)m0 * xrow_b;
       for (int st = 0; st < nsteps; ++st, ++s) {
         const int slot = s % NS, use = s / NS;
@@ -180,7 +189,7 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
                      : a.w + ((size_t)r * wrow_b + (c < 4 ? c * 16 : wlo + (c - 4) * 16) + st * 64);
           } else {
             const int m = m0 + r - BN;
-            const bool in = m < a.M && (!F8 || st * ROWB + c * 16 < a.cs_in);  // F8: zeros past cs_in
+            const bool in = m < mend && (!F8 || st * ROWB + c * 16 < a.cs_in);  // F8: zeros past cs_in
             src = in ? static_cast<const void*>(xt + ((r - BN) * xrow_b + c * 16 + st * ROWB)) : static_cast<const void*>(zp);
           }
           dma16(src, lds_u32(base + b * 1024));
@@ -223,7 +232,11 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
   int s = 0;
   for (int it = 0; it < my_tiles; ++it) {
     const int tile = blockIdx.x + it * gridDim.x;
-    const int m0 = tile * BM;
+    int m0, mend;
+    tile_rows(tile, m0, mend);
+    // a half tile's upper waves have no rows: they keep the flag protocol (FULL before their FREE, so no wave gets a
+    // step ahead of the ring) and skip the reads, MFMAs and stores
+    const bool active = m0 + wm * 64 < mend;
     const int wimg = (min(m0 + wm * 64, a.M - 1)) / a.P - m0 / a.P;  // this wave's image within the tile
     const uint32_t gl = g_lds0 + (uint32_t)(((it & 1) * nimg + wimg) * gimg);
     f32x4 acc[NT][MT];
@@ -237,6 +250,10 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
       if (!wait_flag(full0 + 4 * slot, (unsigned)(NL * (use + 1)), a.spin_max)) {
         report_async(a.err, M2S_ASYNC_WS, lane);
         bad = true;
+      }
+      if (!active) {  // nothing to read: release the slot at once
+        bump_flag(free0 + 4 * slot, lane);
+        continue;
       }
       const uint32_t so = (uint32_t)(slot * SLOT);
       if constexpr (F8) {
@@ -391,13 +408,13 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
 #pragma unroll
         for (int ni = 0; ni < NT; ++ni) {
           const int m = m0 + wm * 64 + mi * 16 + r16, n4 = wn * NT * 16 + ni * 16 + 4 * g;
-          rv[mi][ni] = (a.res && m < a.M && n4 < a.cs_out) ? *reinterpret_cast<const uint2*>(a.res + (size_t)m * a.cs_out + n4)
+          rv[mi][ni] = (a.res && m < mend && n4 < a.cs_out) ? *reinterpret_cast<const uint2*>(a.res + (size_t)m * a.cs_out + n4)
                                                            : make_uint2(0u, 0u);
         }
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi) {
         const int m = m0 + wm * 64 + mi * 16 + r16;
-        if (m >= a.M) continue;
+        if (m >= mend) continue;
 #pragma unroll
         for (int ni = 0; ni < NT; ++ni) {
           const int n4 = wn * NT * 16 + ni * 16 + 4 * g;
@@ -434,7 +451,7 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
         const int n4 = wn * NT * 16 + ni * 16 + 4 * g;
 #pragma unroll
         for (int h = 0; h < 2; ++h)
-          rv[ni][h] = (R && m < a.M && n4 < a.cs_out)
+          rv[ni][h] = (R && m < mend && n4 < a.cs_out)
                           ? *reinterpret_cast<const uint2*>(R + (size_t)m * a.cs_out * 2 + h * a.cs_out + n4)
                           : make_uint2(0u, 0u);
       }
@@ -445,7 +462,7 @@ __global__ void __launch_bounds__(64 * (WM * WN + NL), 1) se_ws_kernel(const SeW
     for (int mi = 0; mi < MT; ++mi) {
       if (mi + 1 < MT) load_res(mi + 1, rv[(mi + 1) & 1]);
       const int m = m0 + wm * 64 + mi * 16 + r16;
-      if (m >= a.M) continue;
+      if (m >= mend) continue;
 #pragma unroll
       for (int ni = 0; ni < NT; ++ni) {
         const int n4 = wn * NT * 16 + ni * 16 + 4 * g;
@@ -480,8 +497,18 @@ void launch_cfg(SeWsArgs& a, hipStream_t s, double flops, double bytes) {
   M2S_CHECK(BM % a.P == 0 || a.P % BM == 0, "se_ws: tile rows vs image size");
   M2S_CHECK(a.cs_out <= BN, "se_ws: one n tile covers the outputs");
   M2S_CHECK((F8 ? a.kp / 128 : a.cs_in / 32) >= NS, "se_ws: K steps per tile >= ring slots (gate rows are double-buffered per tile)");
-  a.n_tiles_m = ceil_div(a.M, BM);
-  const dim3 grid(std::min(a.n_tiles_m, device_cus()));
+  // tail balancing (M2S_SEWS_HALF=1, off by default): when the last round's tiles would fill at most half the
+  // workgroups, they run as twice as many half tiles (BM / 2 rows, still whole 64-row consumer blocks and whole images
+  // or halves of one) spread over them.  Parity-green, but a half tile costs about a full one here (the weight rows,
+  // the ring and the flag protocol stay; half the consumers idle): same-box CNN 31.36 / 31.68 ms off, 31.54 / 31.51 on
+  // (gpurun_out/r06i/ab.txt), unlike ir_ws's slice-range split
+  const int tiles = ceil_div(a.M, BM), G = std::min(tiles, device_cus());
+  const int full = tiles / G * G, rem = tiles - full;
+  const bool halve = rem > 0 && 2 * rem <= G && (BM / 2) % 64 == 0 && ((BM / 2) % a.P == 0 || a.P % (BM / 2) == 0) &&
+                     getenv("M2S_SEWS_HALF") && atoi(getenv("M2S_SEWS_HALF")) == 1;
+  a.full_tiles = halve ? full : tiles;
+  a.n_tiles_m = halve ? full + 2 * rem : tiles;
+  const dim3 grid(G);
   char name[72];
   if (XF)
     snprintf(name, sizeof(name), "se_ws_kernel<%d, %d, %d, %d, %d, %d, false, true>", WM, WN, NT, NL, NS, IF);

@@ -255,7 +255,8 @@ def test_se_ws_matches_barrier_ring(rt, ac_state, monkeypatch, n):
     monkeypatch.setenv("M2S_SEWS_MIN", "0")  # se_ws at any pass size (the product runs it from a full round of tiles)
     monkeypatch.setenv("M2S_KSPLIT", "1")    # the barrier ring unsplit: the same K order as the flag ring
     monkeypatch.setenv("M2S_IRWS_F32", "0")  # and the same split operand (ir_ws at 600 frames hands se_ws fp32 rows)
-    ws = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
+    monkeypatch.setenv("M2S_SEWS_HALF", "1")  # the tail's half tiles (300 / 600 frames: 44 / 88 tiles past the last
+    ws = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)  # full round), off in the product
     monkeypatch.setenv("M2S_SE_WS", "0")
     ring = rt.AcousticEngine(ac_state, dtype="bf16x3", device=DEV)
     for i in (13, 18, 20, 28):  # after blocks 4.0 (16x16, no skip), 4.5, 5.1 (8x8, skip), 5.9
