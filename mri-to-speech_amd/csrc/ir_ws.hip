@@ -133,7 +133,8 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     ir_ws_kernel(const bf16_t* __restrict__ x, int N, int H, int cs_mid, const bf16_t* __restrict__ wpw,
                  const float* __restrict__ bpw, const float* __restrict__ wdw, const float* __restrict__ bdw,
                  bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, unsigned long long* __restrict__ trace,
-                 unsigned spin_max, unsigned* __restrict__ err, int pad_t, int pad_l, int fm32, int n_full, int parts) {
+                 unsigned spin_max, unsigned* __restrict__ err, int pad_t, int pad_l, int fm32, int n_full, int parts,
+                 int par) {
   static_assert(S == 1 || (S == 2 && W == 16), "stride 2: the 16-wide maps");
   constexpr int OWS = W / S;                      // output row width
   constexpr int OPB = (WS_BR / S) * OWS;          // output pixels of a full band
@@ -177,6 +178,14 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   // on stores NaN, so the images of this workgroup come out NaN instead of silently wrong
   unsigned* poison = ctr + 4;
   unsigned* tfree = ctr + 8;   // [WS_NC] slices whose tile and taps consumer wave c is done reading
+  // par (per-parity W ring): a producer's units all have channel tile wave & 1, so even and odd producer waves DMA and
+  // read disjoint halves of a slice's expand weights (rows 0-15 / 16-31) and biases; W(f)'s slot-free and W-ready
+  // counts are kept per parity (ctr 0 / 5 and 1 / 6) and a wave waits only for the other waves of its parity.  The
+  // x band and the tiles stay shared (a band's x rows are free once both parities are past it)
+  const int pw = __builtin_amdgcn_readfirstlane(tid >> 6) & 1;
+  unsigned* const pdone_p = par ? (pw ? ctr + 5 : ctr + 0) : pdone;  // this producer's slot-free count
+  unsigned* const wrdy_p = par ? (pw ? ctr + 6 : ctr + 1) : wrdy;    // this producer's W-ready count
+  const unsigned NPC = par ? WS_NP / 2 : WS_NP;                        // waves behind each of those counts
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -274,7 +283,8 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     char* base = wbuf + (f & 1) * KS * 4096;
     int ln = lane;  // rebuilt per call (asm barrier): hoisted lane offsets cost registers the consumers need
     asm volatile("" : "+v"(ln));
-    if (wave == 0 && ln < 8) dma16(bpw + (sl * WS_SL + 4 * ln), lds_addr(bpl + (f & 1) * 32));
+    if (par ? (wave < 2 && ln < 4) : (wave == 0 && ln < 8))  // (par: each parity's first wave its 16 biases)
+      dma16(bpw + (sl * WS_SL + (par ? 16 * wave : 0) + 4 * ln), lds_addr(bpl + (f & 1) * 32 + (par ? 16 * wave : 0)));
     const int q = (ln & 3) ^ swz_f((ln >> 4) & 3);
     for (int j = wave; j < 4 * KS; j += WS_NP) {
       const int ks = j >> 2, plane = (j >> 1) & 1, half = j & 1;
@@ -318,13 +328,13 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   // says W(f + 1) is complete.  (Waiting for pdone right after the MFMAs put the slowest wave's MFMA tail and
   // the hand-off latency, ~800 cycles a slice, on every producer's critical path; in-kernel stamps r05k.)
   const bool tap_wave = wave >= WS_NP - 2;  // issue_wd's two waves
-  const int npw = (wave < 4 * KS ? (4 * KS - 1 - wave) / WS_NP + 1 : 0) + (wave == 0 ? 1 : 0);  // W pieces a slice
+  const int npw = (wave < 4 * KS ? (4 * KS - 1 - wave) / WS_NP + 1 : 0) + ((par ? wave < 2 : wave == 0) ? 1 : 0);  // W pieces a slice
   // (JOINT) every producer done with slice f's MFMAs -> W(f + 2) issued; every consumer done with slice f - 2 -> return.
   // One lane polls pdone and lanes 0..WS_NC-1 the consumer words, one ds_read pair and one lgkmcnt wait a poll
   auto wait_pd_tf = [&](int f, Step d2) {
-    const unsigned pd_t = f + 1 < T ? (unsigned)(WS_NP * (f + 1)) : 0u, tf_t = f >= 2 ? (unsigned)(f - 1) : 0u;
+    const unsigned pd_t = f + 1 < T ? NPC * (unsigned)(f + 1) : 0u, tf_t = f >= 2 ? (unsigned)(f - 1) : 0u;
     bool wdone = !(f + 2 < T);
-    const uint32_t ap = (uint32_t)(uintptr_t)pdone, at = (uint32_t)(uintptr_t)(tfree + (lane < WS_NC ? lane : 0));
+    const uint32_t ap = (uint32_t)(uintptr_t)pdone_p, at = (uint32_t)(uintptr_t)(tfree + (lane < WS_NC ? lane : 0));
     for (unsigned n = 0; n < spin_max; ++n) {
       unsigned vp, vt;
       asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)" : "=&v"(vp), "=&v"(vt) : "v"(ap), "v"(at) : "memory");
@@ -344,17 +354,17 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   };
   auto after_mfma = [&](int f, Step d2) {
     if (HAND_END) {
-      bump(pdone);
+      bump(pdone_p);
     } else {  // W(f + 1) of this wave landed (younger: only the tap waves' slice-f taps), then every producer's
       if (tap_wave) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
       else wait_vm0();
       TR(f, 13);
-      bump(pdone);
+      bump(pdone_p);
       if (JOINT) {
         wait_pd_tf(f, d2);
         return;
       }
-      if (f + 1 < T) wait_ge(pdone, (unsigned)(WS_NP * (f + 1)));
+      if (f + 1 < T) wait_ge(pdone_p, NPC * (unsigned)(f + 1));
       TR(f, 14);
       if (f + 2 < T) issue_w(f + 2, d2);
     }
@@ -636,8 +646,8 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     if (TAPS_AHEAD && T > 0 && tap_wave) issue_wd(0, cur);
     if (T > 0) {  // W(0) landed (W(1) and the taps may stay in flight)
       wait_vm_le((T > 1 ? npw : 0) + (TAPS_AHEAD && tap_wave ? 1 : 0));
-      bump(wrdy);
-      if (!HAND_END) wait_ge(wrdy, (unsigned)WS_NP);
+      bump(wrdy_p);
+      if (!HAND_END) wait_ge(wrdy_p, NPC);
     }
     static_assert(4 * KS <= 4 * WS_NP, "pieces per wave");
     int bands = 0;
@@ -645,7 +655,10 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       const Step nxt = next_step(cur), nxt2 = next_step(nxt);
       TR(i, 0);
       if (cur.sl == cur.lo) {  // a new band: its input rows, once every producer is done with the last band's
-        if (i > 0) wait_ge(pdone, (unsigned)(WS_NP * i));
+        if (i > 0) {  // (both parities: every producer reads the whole band)
+          wait_ge(pdone_p, NPC * (unsigned)i);
+          if (par) wait_ge(pw ? ctr + 0 : ctr + 5, NPC * (unsigned)i);
+        }
         issue_x(cur.img, cur.band);
         wait_vm0();
         bump(xrdy);
@@ -656,7 +669,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
         if (i >= 3) wait_all(tfree, (unsigned)(i - 2));
         issue_wd(i, cur);
       }
-      if (HAND_END) wait_ge(wrdy, (unsigned)(WS_NP * (i + 1)));  // W(i) complete
+      if (HAND_END) wait_ge(wrdy_p, NPC * (unsigned)(i + 1));  // W(i) complete (this parity's half)
       TR(i, 2);
       produce(i, cur, nxt2);
       if (HAND_END) {
@@ -664,7 +677,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
         wait_vm0();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile stores
         if (lane == 0) {
-          asm volatile("ds_add_u32 %0, %1" ::"v"((uint32_t)(uintptr_t)wrdy), "v"(1u) : "memory");
+          asm volatile("ds_add_u32 %0, %1" ::"v"((uint32_t)(uintptr_t)wrdy_p), "v"(1u) : "memory");
           asm volatile("ds_add_u32 %0, %1" ::"v"((uint32_t)(uintptr_t)tfull), "v"(1u) : "memory");
         }
         TR(i, 12);
@@ -673,7 +686,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
           // W(i)'s slot is free once every producer is done with slice i.  Slice i + 1's taps go to taps[(i + 1) % 3],
           // which held slice i - 2's: produce(i) waited for every consumer to be done with that slice before its
           // tile stores.  Both land during slice i + 1
-          wait_ge(pdone, (unsigned)(WS_NP * (i + 1)));
+          wait_ge(pdone_p, NPC * (unsigned)(i + 1));
           if (nw) issue_w(i + 2, nxt2);
           if (nt) issue_wd(i + 1, nxt);
         }
@@ -785,6 +798,9 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
   const int n_full = N / G * G, rem = N - n_full;
   int parts = rem > 0 ? std::max(1, (G + rem / 2) / rem) : 1;
   parts = std::max(1, std::min(parts, NSl / 3));
+  // per-parity W ring hand-off (kernel comment); M2S_IRWS_PAR=0/1 selects (A/B)
+  int par = 0;
+  if (const char* e = getenv("M2S_IRWS_PAR")) par = atoi(e) != 0;
   if (const char* e = getenv("M2S_IRWS_PARTS"))  // A/B: n = n ranges (1 = no tail split), 0 = the rule above
     if (atoi(e) > 0) parts = std::min(atoi(e), std::max(1, NSl / 3));
 #ifdef IRWS_TRACE
@@ -808,7 +824,7 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
     allow_lds(reinterpret_cast<const void*>(&ir_ws_kernel<W_, KS_, S_>));                             \
     ProfScope ps(NAME_, flops, bytes, s, spill);                                                        \
     hipLaunchKernelGGL((ir_ws_kernel<W_, KS_, S_>), grid, dim3(64 * (WS_NP + WS_NC)), L.total, s, xb, N, H, cs_mid, wb, \
-                       bpw, wdw, bdw, yb, mb, tr, rep.spin_max, rep.err, pad_t, pad_l, fm32 ? 1 : 0, n_full, parts); \
+                       bpw, wdw, bdw, yb, mb, tr, rep.spin_max, rep.err, pad_t, pad_l, fm32 ? 1 : 0, n_full, parts, par); \
     M2S_IRWS_DUMP(NAME_)                                                                                \
     M2S_HIP(hipGetLastError());                                                                         \
     return;                                                                                             \
