@@ -125,6 +125,12 @@ __host__ __device__ inline WsLayout ws_layout(int H, int W, int cs_in, int cs_mi
 #ifndef IRWS_JOINT
 #define IRWS_JOINT 1
 #endif
+// PAR = the per-parity W ring hand-off (kernel comment at `par`).  Same-box A/B of the two builds (tools/ab_kern.py,
+// three alternating rounds, gpurun_out/r06k/ab_par.txt, us per launch): <16,4,1> 668-676 -> 668-674, <16,4,2> 638-645
+// -> 626-637, <8,7,1> 548-554 -> 545-546, CNN 31.80-32.11 -> 31.76-31.87 ms: a small gain, on (-DIRWS_PAR=0: shared)
+#ifndef IRWS_PAR
+#define IRWS_PAR 1
+#endif
 // S = depthwise stride.  S = 2 (blocks.5.0, 16x16 -> 8x8, TF-SAME pads pad_t / pad_l): the producers expand the
 // same input bands; a band's output rows are its 4 stride-2 rows, one pixel a consumer lane (lanes of consumer
 // waves 0-3; waves 4-7 only take part in the hand-offs and the squeeze count).
@@ -133,8 +139,8 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
     ir_ws_kernel(const bf16_t* __restrict__ x, int N, int H, int cs_mid, const bf16_t* __restrict__ wpw,
                  const float* __restrict__ bpw, const float* __restrict__ wdw, const float* __restrict__ bdw,
                  bf16_t* __restrict__ y, bf16_t* __restrict__ se_mean, unsigned long long* __restrict__ trace,
-                 unsigned spin_max, unsigned* __restrict__ err, int pad_t, int pad_l, int fm32, int n_full, int parts,
-                 int par) {
+                 unsigned spin_max, unsigned* __restrict__ err, int pad_t, int pad_l, int fm32, int n_full, int parts) {
+  constexpr int par = IRWS_PAR;
   static_assert(S == 1 || (S == 2 && W == 16), "stride 2: the 16-wide maps");
   constexpr int OWS = W / S;                      // output row width
   constexpr int OPB = (WS_BR / S) * OWS;          // output pixels of a full band
@@ -178,19 +184,19 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
   // on stores NaN, so the images of this workgroup come out NaN instead of silently wrong
   unsigned* poison = ctr + 4;
   unsigned* tfree = ctr + 8;   // [WS_NC] slices whose tile and taps consumer wave c is done reading
-  // par (per-parity W ring): a producer's units all have channel tile wave & 1, so even and odd producer waves DMA and
-  // read disjoint halves of a slice's expand weights (rows 0-15 / 16-31) and biases; W(f)'s slot-free and W-ready
-  // counts are kept per parity (ctr 0 / 5 and 1 / 6) and a wave waits only for the other waves of its parity.  The
-  // x band and the tiles stay shared (a band's x rows are free once both parities are past it)
-  const int pw = __builtin_amdgcn_readfirstlane(tid >> 6) & 1;
-  unsigned* const pdone_p = par ? (pw ? ctr + 5 : ctr + 0) : pdone;  // this producer's slot-free count
-  unsigned* const wrdy_p = par ? (pw ? ctr + 6 : ctr + 1) : wrdy;    // this producer's W-ready count
-  const unsigned NPC = par ? WS_NP / 2 : WS_NP;                        // waves behind each of those counts
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const bool prod = wave < WS_NP;
+  // par (per-parity W ring): a producer's units all have channel tile wave & 1, so even and odd producer waves DMA and
+  // read disjoint halves of a slice's expand weights (rows 0-15 / 16-31) and biases; W(f)'s slot-free and W-ready
+  // counts are kept per parity (ctr 0 / 5 and 1 / 6) and a wave waits only for the other waves of its parity.  The
+  // x band and the tiles stay shared (a band's x rows are free once both parities are past it)
+  const int pw = wave & 1;
+  unsigned* const pdone_p = par ? (pw ? ctr + 5 : ctr + 0) : pdone;  // this producer's slot-free count
+  unsigned* const wrdy_p = par ? (pw ? ctr + 6 : ctr + 1) : wrdy;    // this producer's W-ready count
+  const unsigned NPC = par ? WS_NP / 2 : WS_NP;                        // waves behind each of those counts
   // Work units, dealt round-robin over the workgroups: images 0 .. n_full - 1 whole, then the tail images cut into
   // `parts` slice ranges each (launch_ir_ws: 1920 images on 256 CUs were 7 or 8 images a workgroup, 6 % of the
   // launch idle; 1792 whole + 128 halves are 7.5 each).  Every slice of an image still runs all its bands in one
@@ -798,9 +804,6 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
   const int n_full = N / G * G, rem = N - n_full;
   int parts = rem > 0 ? std::max(1, (G + rem / 2) / rem) : 1;
   parts = std::max(1, std::min(parts, NSl / 3));
-  // per-parity W ring hand-off (kernel comment); M2S_IRWS_PAR=0/1 selects (A/B)
-  int par = 0;
-  if (const char* e = getenv("M2S_IRWS_PAR")) par = atoi(e) != 0;
   if (const char* e = getenv("M2S_IRWS_PARTS"))  // A/B: n = n ranges (1 = no tail split), 0 = the rule above
     if (atoi(e) > 0) parts = std::min(atoi(e), std::max(1, NSl / 3));
 #ifdef IRWS_TRACE
@@ -824,7 +827,7 @@ void launch_ir_ws(const void* x, int N, int H, int W, int cs_in, int kp, int cs_
     allow_lds(reinterpret_cast<const void*>(&ir_ws_kernel<W_, KS_, S_>));                             \
     ProfScope ps(NAME_, flops, bytes, s, spill);                                                        \
     hipLaunchKernelGGL((ir_ws_kernel<W_, KS_, S_>), grid, dim3(64 * (WS_NP + WS_NC)), L.total, s, xb, N, H, cs_mid, wb, \
-                       bpw, wdw, bdw, yb, mb, tr, rep.spin_max, rep.err, pad_t, pad_l, fm32 ? 1 : 0, n_full, parts, par); \
+                       bpw, wdw, bdw, yb, mb, tr, rep.spin_max, rep.err, pad_t, pad_l, fm32 ? 1 : 0, n_full, parts); \
     M2S_IRWS_DUMP(NAME_)                                                                                \
     M2S_HIP(hipGetLastError());                                                                         \
     return;                                                                                             \

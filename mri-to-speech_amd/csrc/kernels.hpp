@@ -249,6 +249,12 @@ void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B
                             unsigned spin_max, unsigned* err_host, hipStream_t s);
 // B > 4 in split fp32 (the bf16x3 / bf16 / fp8 engines): three bf16 MFMA terms over W_hh and h_t split
 // hi / lo, h_t published split by write-through stores behind per-workgroup flags (no fences).
+// Split engines, 5..16 sequences: lstm_x3's arithmetic with the h_t hand-off as data-tagged granules (no flag round
+// trip, no store drain); `sync` = lstm_x3g_sync_bytes() (tags reset by the launcher).  (lstm_persistent.hip)
+bool lstm_x3g_supported(int B, int H);
+size_t lstm_x3g_sync_bytes();
+void launch_lstm_x3g(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,
+                     unsigned* err_host, hipStream_t s);
 // `sync` = lstm_x3_sync_bytes() (flags reset by the launcher).
 size_t lstm_x3_sync_bytes();
 void launch_lstm_x3(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,

@@ -390,6 +390,188 @@ __global__ void __launch_bounds__(64 * LX_W, 1) lstm_x3_kernel(const float* __re
   }
 }
 
+// ---- split fp32, small batches (B <= LG_BMAX: configs[4]'s 8 clips a GPU): lstm_x3 with a granule hand-off ------
+// lstm_x3's step is three memory round trips deep besides its arithmetic: the h_t stores drain (vmcnt(0)) before the
+// workgroup's flag store, a consumer polls its 40 producers' flags, and only then loads the payload (~3.7 us a step
+// at 8 x 1000, 78 % of its wave cycles waiting; verdict r05 item 8).  Here h_t travels as data-tagged granules as in
+// lstm_small_kernel: each cell-update thread publishes ONE 8-byte sc1 store {tag = step + 1 | hi bf16 | lo bf16} of
+// its (unit, sequence) (cdna_hip_programming.md Guideline 16 R2: the data is the flag; no drain, no flag, no
+// fence), and every workgroup of the direction sweeps the nb x 640 granules of h_{t-1} with 16-byte sc1 buffer
+// loads (two granules each, every one checked by its own tag; the stale ones re-polled together) into an LDS
+// image [sequence][hi 640 | lo 640] bf16 (rows padded by 16 B: the B-fragment reads of 16 sequences fall on
+// distinct banks), from which the MFMA B fragments are read.  Everything else is lstm_x3's: W_hh split into resident
+// hi / lo A fragments, three v_mfma_f32_32x32x16_bf16 terms, K-slice partials summed in LDS in a fixed order, fp32
+// cell state and gate math.  Granules are double-buffered by step parity (no workgroup of a direction can be more
+// than one step ahead of another: publishing h_{t+1} needs every h_t).
+constexpr int LG_BMAX = 16;                            // sequences (one half of lstm_x3's 32-sequence tile)
+constexpr int LG_ROWB = 2 * 2 * LP_H + 16;             // LDS image row bytes: hi 640 | lo 640 bf16 + pad
+constexpr int LG_PAIRS = LP_H / 2;                     // 16-byte granule pairs per sequence
+
+__global__ void __launch_bounds__(64 * LX_W, 1) lstm_x3g_kernel(const float* __restrict__ pre, const float* __restrict__ whh,
+                                                                 float* hs, int B, int T, unsigned* err,
+                                                                 unsigned long long* gran, unsigned spin_max,
+                                                                 unsigned* err_host) {
+  __shared__ float red[LX_W][2 * 32][LX_S + 1];
+  __shared__ float cst[LX_U][LG_BMAX];
+  __shared__ __attribute__((aligned(16))) char hxl[LG_BMAX * LG_ROWB];
+  __shared__ int abort_flag;
+  extern __shared__ char lx_pad[];  // occupancy only
+  const int H = LP_H;
+  const int dir = blockIdx.x / LX_G, ug = blockIdx.x % LX_G;
+  const int nb = B;  // launch_lstm_x3g: B <= LG_BMAX, one workgroup row of sequences
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hh = lane >> 5, l32 = lane & 31;
+  const int kw = wave * LX_KW;
+  float* hsd = hs + (size_t)dir * B * T * H;
+  unsigned long long* gd = gran + (size_t)dir * 2 * LG_BMAX * H;  // [parity][sequence][unit]
+  if (tid == 0) lx_pad[0] = 0;
+
+  bf16x8 whi[2][LX_KS], wlo[2][LX_KS];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int r = 32 * m + l32, g = r / LX_U, u = ug * LX_U + (r % LX_U);
+    const float* wr = whh + ((size_t)dir * 4 * H + (size_t)g * H + u) * H + kw + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < LX_KS; ++s) {
+      const float4 a = *reinterpret_cast<const float4*>(wr + 16 * s);
+      const float4 b = *reinterpret_cast<const float4*>(wr + 16 * s + 4);
+      const float v0[4] = {a.x, a.y, a.z, a.w}, v1[4] = {b.x, b.y, b.z, b.w};
+      uint2 h0, l0, h1, l1;
+      split4(v0, h0, l0);
+      split4(v1, h1, l1);
+      whi[m][s] = __builtin_bit_cast(bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+      wlo[m][s] = __builtin_bit_cast(bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+    }
+  }
+  for (int i = tid; i < LX_U * LG_BMAX; i += 64 * LX_W) (&cst[0][0])[i] = 0.f;
+  for (int i = tid; i < LG_BMAX * LG_ROWB / 16; i += 64 * LX_W)  // rows >= nb stay zero (their B columns unused)
+    reinterpret_cast<uint4*>(hxl)[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (tid == 0) abort_flag = 0;
+  __syncthreads();
+
+  const int cu = tid % LX_U, cb = tid / LX_U;  // cell-update pair (unit, sequence) of this thread
+  const uint32_t hx0 = (uint32_t)(uintptr_t)hxl;
+  for (int step = 0; step < T; ++step) {
+    const int t = dir == 0 ? step : T - 1 - step;
+    float prf[4];
+    {
+      const float* pr = pre + ((size_t)cb * T + t) * 8 * H + (size_t)dir * 4 * H + ug * LX_U + cu;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) prf[q] = cb < nb ? pr[q * H] : 0.f;
+    }
+    f32x16 acc[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][i] = 0.f;
+    if (step > 0) {
+      // ---- sweep h_{t-1}: granule pairs q = tid + 512 j (sequence q / 320, units 2 (q % 320) + {0, 1}), all loads
+      // issued first, then the tags checked; the stale pairs re-polled together ----------------------------------
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          gd + (size_t)((step - 1) & 1) * LG_BMAX * H, 0, nb * H * (int)sizeof(unsigned long long), 0x00020000);
+      constexpr int PJ = (LG_BMAX * LG_PAIRS + 64 * LX_W - 1) / (64 * LX_W);  // pairs per thread at most (10)
+      u32x4_t v[PJ];
+#pragma unroll
+      for (int j = 0; j < PJ; ++j) {
+        const int q = tid + 64 * LX_W * j;
+        v[j] = q < nb * LG_PAIRS ? __builtin_amdgcn_raw_buffer_load_b128(rs, q * 16, 0, 16) : u32x4_t{0u, 0u, 0u, 0u};
+      }
+      // stale pairs are re-polled together (one round trip a poll for all of them, not one per granule)
+      for (unsigned spins = 0;; ++spins) {
+        bool stale = false;
+#pragma unroll
+        for (int j = 0; j < PJ; ++j) {
+          const int q = tid + 64 * LX_W * j;
+          stale |= q < nb * LG_PAIRS && (v[j][1] != (unsigned)step || v[j][3] != (unsigned)step);
+        }
+        if (!stale && spin_max != 0) break;
+        if (spins >= spin_max || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          abort_flag = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int j = 0; j < PJ; ++j) {
+          const int q = tid + 64 * LX_W * j;
+          if (q < nb * LG_PAIRS && (v[j][1] != (unsigned)step || v[j][3] != (unsigned)step))
+            v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, q * 16, 0, 16);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < PJ; ++j) {
+        const int q = tid + 64 * LX_W * j;
+        if (q >= nb * LG_PAIRS) break;
+        // hi halves of the two units -> the sequence row's hi plane, lo halves -> its lo plane (4-byte stores)
+        const int sq = q / LG_PAIRS, u2 = 2 * (q - sq * LG_PAIRS);
+        const uint32_t hi = (v[j][0] & 0xffffu) | (v[j][2] << 16), lo = (v[j][0] >> 16) | (v[j][2] & 0xffff0000u);
+        *reinterpret_cast<uint32_t*>(hxl + sq * LG_ROWB + 2 * u2) = hi;
+        *reinterpret_cast<uint32_t*>(hxl + sq * LG_ROWB + 2 * H + 2 * u2) = lo;
+      }
+      __syncthreads();
+      if (abort_flag) {  // a peer stopped publishing: flag the host, poison the remaining outputs, leave
+        if (tid == 0 && err_host) __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int st = step; st < T; ++st) {
+          const int tt = dir == 0 ? st : T - 1 - st;
+          for (int p = tid; p < LX_U * nb; p += 64 * LX_W)
+            hsd[((size_t)(p / LX_U) * T + tt) * H + ug * LX_U + p % LX_U] = __builtin_nanf("");
+        }
+        return;
+      }
+      // ---- B fragments of h_{t-1} from the image: sequence l32, k = kw + 16 s + 8 hh (hi and lo) -------------
+      uint4 bh[LX_KS], bl[LX_KS];
+      const uint32_t o = hx0 + (uint32_t)(l32 * LG_ROWB + 2 * (kw + 8 * hh));
+#pragma unroll
+      for (int s = 0; s < LX_KS; ++s) {
+        if (l32 < LG_BMAX) {
+          bh[s] = *reinterpret_cast<const uint4*>(hxl + (o - hx0) + 32 * s);
+          bl[s] = *reinterpret_cast<const uint4*>(hxl + (o - hx0) + 32 * s + 2 * H);
+        } else {
+          bh[s] = bl[s] = make_uint4(0u, 0u, 0u, 0u);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < LX_KS; ++s)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wlo[m][s], __builtin_bit_cast(bf16x8, bh[s]), acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(whi[m][s], __builtin_bit_cast(bf16x8, bl[s]), acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(whi[m][s], __builtin_bit_cast(bf16x8, bh[s]), acc[m], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) red[wave][32 * m + 8 * (i / 4) + 4 * hh + (i % 4)][l32] = acc[m][i];
+    __syncthreads();
+    // ---- cell update (unit cu, sequence cb); h_t published as a granule {step + 1 | hi | lo} -------------------
+    if (cb < nb) {
+      float gs[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int r = g * LX_U + cu;
+        gs[g] = ((red[0][r][cb] + red[1][r][cb]) + (red[2][r][cb] + red[3][r][cb])) +
+                ((red[4][r][cb] + red[5][r][cb]) + (red[6][r][cb] + red[7][r][cb]));
+      }
+      const float gi = lstm_sig(prf[0] + gs[0]);
+      const float gf = lstm_sig(prf[1] + gs[1]);
+      const float gg = lstm_tanh(prf[2] + gs[2]);
+      const float go = lstm_sig(prf[3] + gs[3]);
+      const float c = step > 0 ? gf * cst[cu][cb] + gi * gg : gi * gg;
+      cst[cu][cb] = c;
+      const float h = go * lstm_tanh(c);
+      hsd[((size_t)cb * T + t) * H + ug * LX_U + cu] = h;
+      if (step + 1 < T) {
+        const bf16_t hb = f2bf(h), lb = f2bf(h - bf2f(hb));  // the split of sp_t (17 bits)
+        __hip_atomic_store(gd + (size_t)(step & 1) * LG_BMAX * H + (size_t)cb * H + ug * LX_U + cu,
+                           ((unsigned long long)(step + 1) << 32) | ((unsigned)lb << 16) | (unsigned)hb, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();  // red and the image are rewritten next step
+  }
+}
+
 // ---- small batches (B <= LS_BMAX: the 1 x 1000-frame configs[4] clip, the 1 x 30 configs[0] clip) -----
 // At B = 1 the 32-wide MFMA B tile is 1/32 used and the counter barrier (store drain, agent release,
 // atomic, relaxed polls, acquire + L2 refill of h) cost ~20 us a step.  Here h_t travels as data-
@@ -799,6 +981,25 @@ void launch_lstm_x3(const float* pre, const float* whh, float* hs, int B, int T,
                        spin_max, err_host);
     M2S_HIP(hipGetLastError());
   }
+}
+
+size_t lstm_x3g_sync_bytes() { return 256 + (size_t)2 * 2 * LG_BMAX * LP_H * sizeof(unsigned long long); }
+
+bool lstm_x3g_supported(int B, int H) { return H == LP_H && B >= 1 && B <= LG_BMAX; }
+
+void launch_lstm_x3g(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,
+                     unsigned* err_host, hipStream_t s) {
+  M2S_CHECK(lstm_x3g_supported(B, H) && T > 0, "lstm_x3g: unsupported shape");
+  const int grid = 2 * LX_G;  // (direction, unit group): one row of <= 16 sequences
+  const int resident = device_resident(reinterpret_cast<const void*>(&lstm_x3g_kernel), 64 * LX_W, LX_PAD_LDS);
+  M2S_CHECK(grid <= resident, "lstm_x3g: grid not co-resident on this device");
+  // [256 B: error word][granules 2 dir x 2 parity x LG_BMAX x H]: every tag restarts at 0 each call
+  M2S_HIP(hipMemsetAsync(sync, 0, lstm_x3g_sync_bytes(), s));
+  unsigned* err = static_cast<unsigned*>(sync);
+  unsigned long long* gran = reinterpret_cast<unsigned long long*>(static_cast<char*>(sync) + 256);
+  hipLaunchKernelGGL(lstm_x3g_kernel, dim3(grid), dim3(64 * LX_W), LX_PAD_LDS, s, pre, whh, hs, B, T, err, gran, spin_max,
+                     err_host);
+  M2S_HIP(hipGetLastError());
 }
 
 }  // namespace m2s

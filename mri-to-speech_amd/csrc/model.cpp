@@ -102,6 +102,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   if (const char* e = std::getenv("M2S_LSTM_PERSISTENT")) lstm_persistent_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_LSTM_MID")) lstm_mid_ = std::strcmp(e, "0") != 0;
   if (const char* e = std::getenv("M2S_LSTM_X3")) lstm_x3_ = std::strcmp(e, "0") != 0;
+  if (const char* e = std::getenv("M2S_LSTM_X3G")) lstm_x3g_ = std::strcmp(e, "0") != 0;
   const std::string P = "cnn.backbone.";
   {  // stem: fold repeat(1,3,1,1) by summing the 3 input channels; then BN
     const float* w = need(sd, P + "conv_stem.weight", {EFF_STEM, 3, 3, 3}).data;
@@ -587,7 +588,7 @@ size_t Acoustic::workspace_bytes(int B, int T, int H, int W) const {
   ws.take<float>(BT * 8 * hidden_);
   ws.take<float>(2 * BT * hidden_);
   ws.take<float>((size_t)2 * B * hidden_);
-  ws.take<char>(std::max({lstm_persistent_sync_bytes(), lstm_small_sync_bytes(), lstm_mid_sync_bytes(), lstm_x3_sync_bytes()}));
+  ws.take<char>(std::max({lstm_persistent_sync_bytes(), lstm_small_sync_bytes(), lstm_mid_sync_bytes(), lstm_x3_sync_bytes(), lstm_x3g_sync_bytes()}));
   return ws.used();
 }
 
@@ -953,10 +954,14 @@ void Acoustic::bilstm(const float* feats, int B, int T, float* y, float* mel_nor
   a.y = pre;
   a.M = (int)BT;
   run_conv<float>(a, lstm_ih_, s);
-  void* sync = ws.take<char>(std::max({lstm_persistent_sync_bytes(), lstm_small_sync_bytes(), lstm_mid_sync_bytes(), lstm_x3_sync_bytes()}));
+  void* sync = ws.take<char>(std::max({lstm_persistent_sync_bytes(), lstm_small_sync_bytes(), lstm_mid_sync_bytes(), lstm_x3_sync_bytes(), lstm_x3g_sync_bytes()}));
   if (lstm_persistent_ && lstm_small_supported(B, H)) {
     ProfScope ps("lstm_small_kernel", 2.0 * 2 * B * 4.0 * H * H * (T - 1), 4.0 * 2 * 4 * H * H + 4.0 * BT * (8.0 * H + 2.0 * H), s);
     launch_lstm_small(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, lstm_spin_max_, err_dev_, s);
+  } else if (lstm_persistent_ && lstm_x3_ && lstm_x3g_ && dtype_ != M2S_DT_F32 && lstm_x3g_supported(B, H)) {
+    // 5..16 sequences (configs[4]'s 8 clips a GPU): the granule hand-off (lstm_persistent.hip lstm_x3g_kernel)
+    ProfScope ps("lstm_x3g_kernel", 3.0 * 2 * B * 4.0 * H * H * (T - 1), 4.0 * 2 * 4 * H * H + 4.0 * BT * (8.0 * H + 2.0 * H), s);
+    launch_lstm_x3g(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, lstm_spin_max_, err_dev_, s);
   } else if (lstm_persistent_ && lstm_x3_ && dtype_ != M2S_DT_F32 && lstm_persistent_supported(H)) {
     // split engines above the small-batch kernel: 4.1 / 5.2 / 9.9 us per step at B = 8 / 16 / 64 against
     // lstm_mid's 7.2 / 11.9 and the f32 counter-barrier kernel's 24 (gpurun_out lstm2, lstm3_x3small)

@@ -131,6 +131,7 @@ class Acoustic {
   bool lstm_persistent_ = true;  // one-launch BiLSTM recurrence (env M2S_LSTM_PERSISTENT=0: a launch per step)
   bool lstm_mid_ = true;         // 4 < B <= 16: granule-exchange recurrence (env M2S_LSTM_MID=0: counter barrier)
   bool lstm_x3_ = true;          // B > 4, non-fp32 engines: split-bf16 MFMA recurrence (env M2S_LSTM_X3=0: lstm_mid / f32)
+  bool lstm_x3g_ = true;   // ... and for 5..16 sequences its granule hand-off form (env M2S_LSTM_X3G=0: lstm_x3)
   // (the M2S_* switches are read once, when the engine is created: A/B tests of fused vs unfused)
 
   size_t workspace_bytes(int B, int T, int H, int W) const;

@@ -348,6 +348,27 @@ def test_bilstm_split_x3(rt, ac_state, monkeypatch, B, T):
     print(f"lstm_x3 B={B} T={T}: max |d| vs oracle {np.abs(y - ref_y).max():.2e}")
 
 
+@pytest.mark.parametrize("B,T", [(5, 17), (8, 1000), (16, 200)])
+def test_bilstm_x3g_matches_flag_handoff(rt, ac_state, monkeypatch, B, T):
+    """5..16 sequences in the split engines run lstm_x3g_kernel: lstm_x3's split arithmetic with h_t handed over as
+    data-tagged granules {step + 1 | hi | lo} swept into LDS instead of write-through rows behind per-workgroup flags.
+    The products, their order and the K-slice sums are lstm_x3's, so the two agree to fp32 rounding of the same
+    operations; the launch log names the kernel."""
+    from m2s import _native
+    x = torch.from_numpy(np.random.default_rng(B * 7 + T).normal(0, 0.5, (B, T, 208)).astype(np.float32)).to(DEV)
+    eng = rt.AcousticEngine(ac_state[1], dtype="bf16x3", device=DEV)
+    _native.prof_enable(True)
+    y, _ = eng.bilstm(x)
+    torch.cuda.synchronize()
+    names = {r["name"] for r in _native.prof_launches()}
+    _native.prof_enable(False)
+    assert "lstm_x3g_kernel" in names, names
+    monkeypatch.setenv("M2S_LSTM_X3G", "0")
+    y3, _ = rt.AcousticEngine(ac_state[1], dtype="bf16x3", device=DEV).bilstm(x)
+    eng.check()
+    np.testing.assert_allclose(y.cpu().numpy(), y3.cpu().numpy(), atol=1e-5, rtol=0)
+
+
 # ------------------------------------------------------------------------------ frame preprocessing
 def test_preprocess_matches_reference_golden(rt):
     """Device _preprocess_frame (preprocess.hip) vs the reference's own outputs (glue.npz)."""
@@ -374,7 +395,7 @@ def test_bilstm_barrier_timeout_is_reported(rt, ac_state, B, dtype):
     """A BiLSTM hand-off wait that times out (forced: spin limit 0 = the first wait fails) poisons the outputs and is
     reported: m2s_acoustic_status -> M2SError, and the next forward on the engine fails too.  B = 1:
     lstm_small_kernel, 8 / 12: lstm_mid_kernel with 4- / 8-sequence chunks (granule sweeps), 70: the counter
-    barrier (fp32); 8 / 70 bf16x3: the flag hand-off of lstm_x3_kernel."""
+    barrier (fp32); 8 bf16x3: the granule hand-off of lstm_x3g_kernel, 70 bf16x3: the flag hand-off of lstm_x3_kernel."""
     import ctypes
     from m2s import _native
     eng = rt.AcousticEngine(ac_state[1], dtype=dtype, device=DEV)
