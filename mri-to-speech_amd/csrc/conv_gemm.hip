@@ -824,6 +824,10 @@ void launch_kind_xf(const ConvBatch& a, hipStream_t s, int phases, double flops,
       if (SP == 1 && n <= 64) return launch_tile<128, 64, 4, 2, KIND, XF, SP>(a, s, phases, flops, bytes);
       return launch_tile<256, 64, 4, 4, KIND, XF, SP>(a, s, phases, flops, bytes);
     }
+    if constexpr (SP == 1 && KIND == KIND_CONV1D && XF == IN_NONE) {  // A/B: the split MRF convs on 128 x 64 tiles
+      static const bool bn64 = getenv("M2S_CG_BN64") && atoi(getenv("M2S_CG_BN64")) == 1;  // (3 stages, 2 per CU)
+      if (bn64) return launch_tile<128, 64, 4, 2, KIND, XF, SP>(a, s, phases, flops, bytes);
+    }
     return launch_tile<128, 128, 4, 4, KIND, XF, SP>(a, s, phases, flops, bytes);
   } else {
   if constexpr (KIND == KIND_GEMM || KIND == KIND_CONV2D) if (a.a[0].M >= 256 * 256 && n > 128 &&
