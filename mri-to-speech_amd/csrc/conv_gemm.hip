@@ -750,12 +750,12 @@ const char* kname(int k) {
 // rows of SE gates a tile needs: the images its BM rows touch
 inline int se_images(int BM, int OH) { return BM % OH == 0 ? BM / OH : OH % BM == 0 ? 1 : (BM + OH - 1) / OH + 1; }
 
-template <int BM, int BN, int MT, int NT, int KIND, int XF, int SP>
+template <int BM, int BN, int MT, int NT, int KIND, int XF, int SP, int SF = 0>
 void launch_tile(const ConvBatch& b, hipStream_t s, int phases, double flops, double bytes) {
   const ConvArgs& a = b.a[0];
   // keep two workgroups' LDS per CU (128 x 256: the SE gate table too, and 256 registers a wave);
-  // split operands double the slot, so they run two stages
-  constexpr int S = SP == 1 ? (BM == 128 && BN == 64 && XF != IN_SE_SCALE ? 3 : 2) : (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
+  // split operands double the slot, so they run two stages (SF: a forced stage count, A/B builds)
+  constexpr int S = SF ? SF : SP == 1 ? (BM == 128 && BN == 64 && XF != IN_SE_SCALE ? 3 : 2) : (BN >= 256 || BM + BN >= 384) ? 2 : (BM >= 256 ? 3 : 4);
   constexpr int R = SP == 1 ? 2 : 1;
   allow_lds(reinterpret_cast<const void*>(&conv_gemm_kernel<BM, BN, MT, NT, S, KIND, XF, SP>));
   const int m_tiles = ceil_div(a.M, BM), n_tiles = ceil_div(a.cs_out, BN);
@@ -827,6 +827,10 @@ void launch_kind_xf(const ConvBatch& a, hipStream_t s, int phases, double flops,
     if constexpr (SP == 1 && KIND == KIND_CONV1D && XF == IN_NONE) {  // A/B: the split MRF convs on 128 x 64 tiles
       static const bool bn64 = getenv("M2S_CG_BN64") && atoi(getenv("M2S_CG_BN64")) == 1;  // (3 stages, 2 per CU)
       if (bn64) return launch_tile<128, 64, 4, 2, KIND, XF, SP>(a, s, phases, flops, bytes);
+      // A/B: 3 or 4 stages at one workgroup per CU (101 / 135 KB) instead of 2 stages at two
+      static const int stg = getenv("M2S_CG_STAGES") ? atoi(getenv("M2S_CG_STAGES")) : 0;
+      if (stg == 3) return launch_tile<128, 128, 4, 4, KIND, XF, SP, 3>(a, s, phases, flops, bytes);
+      if (stg == 4) return launch_tile<128, 128, 4, 4, KIND, XF, SP, 4>(a, s, phases, flops, bytes);
     }
     return launch_tile<128, 128, 4, 4, KIND, XF, SP>(a, s, phases, flops, bytes);
   } else {

@@ -64,6 +64,27 @@ __device__ __forceinline__ float lo16(uint32_t u) { return __uint_as_float(u << 
 __device__ __forceinline__ float hi16(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 __device__ __forceinline__ uint32_t lrelu_pk(uint32_t u) { return pack_bf16x2(lrelu01(lo16(u)), lrelu01(hi16(u))); }
 
+// An epilogue store into a plane: lane (g, r16) holds 8 bytes (4 channels) of row r16, and lane groups g and g ^ 1
+// hold the two halves of the same 16-byte row chunk.  Stored as one ds_write_b64 per lane, each 16-lane group put
+// 16 rows x 8 bytes at a 16-byte stride: rows r and r + 8 share store banks ((a / 4) mod 32), a 2-way conflict
+// on every epilogue store (0.29 / 0.40 / 0.69 conflict cycles per LDS instruction at k = 11 / 7 / 3,
+// profiles/r06ev2_sq_mfma.txt).  Here the even groups take their partner's half (v_permlane16_swap: lanes l and
+// l + 16) and store whole 16-byte rows: every 8-lane ds_write_b128 group covers 128 contiguous bytes.
+// p16: the row chunk's start (16-byte aligned: told to the compiler, else it emits ds_write2_b64).
+#ifndef RB1_ROWST
+#define RB1_ROWST 0  // 1: row-wide stores (conflict-free, measured 5 % slower: DESIGN §13.2)
+#endif
+__device__ __forceinline__ void st_row16(char* p16, uint2 v, int g) {
+  if (!RB1_ROWST) {
+    *reinterpret_cast<uint2*>(p16 + 8 * (g & 1)) = v;
+    return;
+  }
+  const auto sx = __builtin_amdgcn_permlane16_swap(v.x, v.x, false, false);
+  const auto sy = __builtin_amdgcn_permlane16_swap(v.y, v.y, false, false);
+  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));  // (a uint4 store was scalarised into 4 stores)
+  if (!(g & 1)) *reinterpret_cast<u32x4_t*>(__builtin_assume_aligned(p16, 16)) = u32x4_t{v.x, v.y, sx[1], sy[1]};
+}
+
 enum { PASS_C1 = 0, PASS_C2 = 1, PASS_LAST = 2 };
 constexpr int RB_NW = 8;          // waves per workgroup
 constexpr int RB_STAGE = 8192;    // bytes per weight stage = one 1 KB piece per wave
@@ -169,7 +190,8 @@ __device__ __forceinline__ void conv_pass(const RbArgs& a, const Ring& ring, int
     for (int nt = 0; nt < NT; ++nt) {
       const int n = nt * 16 + 4 * g;
       const float4 bb = *reinterpret_cast<const float4*>(bias_lds + n);
-      char* p = io + (n >> 3) * PLANE + (r + 16) * 16 + (n & 7) * 2;
+      char* p16 = io + (n >> 3) * PLANE + (r + 16) * 16;  // the row chunk
+      char* p = p16 + (n & 7) * 2;
       float v[4] = {acc[i][nt][0] + bb.x, acc[i][nt][1] + bb.y, acc[i][nt][2] + bb.z, acc[i][nt][3] + bb.w};
       if constexpr (PASS != PASS_C1) {  // residual: x recovered from A = lrelu(x) at this row
         const uint2 u = *reinterpret_cast<const uint2*>(p);
@@ -193,10 +215,10 @@ __device__ __forceinline__ void conv_pass(const RbArgs& a, const Ring& ring, int
         if constexpr (SP) {
           uint2 oh, ol;
           split4(o, oh, ol);
-          *reinterpret_cast<uint2*>(p) = oh;
-          *reinterpret_cast<uint2*>(p + NPL * PLANE) = ol;
+          st_row16(p16, oh, g);
+          st_row16(p16 + NPL * PLANE, ol, g);
         } else {
-          *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+          st_row16(p16, make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])), g);
         }
       } else if (r >= a.H && t < a.L) {
         bf16_t* sp = a.s + ((size_t)clip * a.L + t) * C * HR + n;

@@ -62,7 +62,8 @@ struct StemB0Args {
   const float* b1;
   bf16_t* y;            // (N, OH, OW, 16) (SP: (N, OH, OW, [hi 16 | lo 16]))
   int N, H, W, OH, OW, pad_t, pad_l, kp0, kp1, tiles_x, tiles_y;
-  int per_xcd;  // strips (image, tile column) per XCD range (gridDim.x is a multiple of 8)
+  int per_xcd;  // units (strip part) per XCD range (gridDim.x is a multiple of 8)
+  int parts, tpp;  // a strip's tile rows cut into `parts` ranges of tpp rows (small batches; 1 = whole strips)
   unsigned long long* trace;  // diagnostic build (-DIRWS_TRACE): per-phase s_memtime stamps, else null
 };
 
@@ -110,9 +111,15 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
   // the rows the next tile shares (S rows 16..19 -> 0..3, A rows 16..17 -> 0..1: halo recompute 1.56x ->
   // 1.25x of the stem, 1.44x -> 1.25x of blocks.0.0).  Strips of XCD x (= blockIdx % 8) are
   // [x * per_xcd, (x + 1) * per_xcd) (neighbouring columns of the same frames share one L2).
-  const int nstrip = a.N * a.tiles_x;
+  // Units = (strip, part): part p is tile rows [p tpp, min((p + 1) tpp, tiles_y)); its first tile computes every S / A
+  // row (no rows carried in), as a strip's first tile does.  Parts > 1 only where whole strips leave workgroup slots
+  // idle (one clip: 240 strips for 512 slots).
+  const int nunit = a.N * a.tiles_x * a.parts;
   const int gx = gridDim.x / 8, xcd = blockIdx.x % 8;
-  const int s_end = min(nstrip, (xcd + 1) * a.per_xcd);
+  const int s_end = min(nunit, (xcd + 1) * a.per_xcd);
+  auto strip_of = [&](int u) { return u / a.parts; };
+  auto ty_lo = [&](int u) { return (u - (u / a.parts) * a.parts) * a.tpp; };
+  auto ty_hi = [&](int u) { return min(ty_lo(u) + a.tpp, a.tiles_y); };
 
   // ---- phase-1 work of a tile: S position subtiles j (16 S pixels OFS + 16 j ..), j = j0 + wave + 4 i: a
   // strip's first tile all 25 (rows 0..19), later tiles the 20 of rows 4..19 (j0 = 5; rows 0..3 are carried).
@@ -143,14 +150,14 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
   };
   float xin[NPF][3];
   unsigned xm = 0;  // 3 mask bits per prefetched subtile
-  auto load_in = [&](int st, int ty) {
-    const int j0 = ty == 0 ? 0 : 5;
+  auto load_in = [&](int u, int ty) {
+    const int j0 = ty == ty_lo(u) ? 0 : 5;
     xm = 0;
 #pragma unroll
-    for (int i = 0; i < NPF; ++i) xm |= load3(xin[i], st, ty, j0 + wave + 4 * i) << (3 * i);
+    for (int i = 0; i < NPF; ++i) xm |= load3(xin[i], strip_of(u), ty, j0 + wave + 4 * i) << (3 * i);
   };
-  int st = xcd * a.per_xcd + (int)blockIdx.x / 8, ty = 0;
-  if (st < s_end) load_in(st, 0);
+  int u = xcd * a.per_xcd + (int)blockIdx.x / 8, ty = ty_lo(u);
+  if (u < s_end) load_in(u, ty);
 
   // resident weights of both convs (A fragments)
   bf16x8 wf0[9], wf1[5], wl0[SP ? 9 : 1], wl1[SP ? 5 : 1];
@@ -200,9 +207,10 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
     (void)k;
 #endif
   };
-  while (st < s_end) {
+  while (u < s_end) {
+    const int st = strip_of(u);
     const int n = st / a.tiles_x, tx0 = (st - n * a.tiles_x) * SB_TW, ty0 = ty * TH;
-    const bool first = ty == 0;
+    const bool first = ty == ty_lo(u);
     TR(0);
     // ---- phase 1: stem (fp32 VALU) -> S -----------------------------------------------------
     // (S is free: every wave passed the previous tile's phase-2 barrier before reaching here.)
@@ -270,8 +278,9 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
         __builtin_amdgcn_sched_barrier(0);
       }
       // the next tile's frame pixels, in flight through phases 2 and 3
-      const int nst = ty + 1 < a.tiles_y ? st : st + gx, nty = ty + 1 < a.tiles_y ? ty + 1 : 0;
-      if (nst < s_end) load_in(nst, nty);
+      const bool endu = ty + 1 >= ty_hi(u);
+      const int nu = endu ? u + gx : u, nty = endu ? ty_lo(nu) : ty + 1;
+      if (nu < s_end) load_in(nu, nty);
     }
     TR(1);
     __syncthreads();
@@ -435,9 +444,9 @@ __global__ void __launch_bounds__(256, SP ? 2 : 3) stem_b0_kernel(const StemB0Ar
     }
     TR(5);
     ++it;
-    if (++ty == a.tiles_y) {
-      ty = 0;
-      st += gx;
+    if (++ty == ty_hi(u)) {
+      u += gx;
+      ty = ty_lo(u);
     }
   }
 }
@@ -483,8 +492,15 @@ void launch_stem_b0(const float* frames, int N, int H, int W, int OH, int OW, in
   // of 8 (one equal share per XCD); small inputs take fewer
   const int cus = device_cus();
   const int nstrip = N * a.tiles_x;  // a workgroup walks whole strips (image, tile column) top to bottom
-  a.per_xcd = ceil_div(nstrip, 8);
   const int per_cu = split ? 2 : 3;
+  // small batches: strips cut into tile-row ranges so the units fill the workgroup slots (a cut costs one more
+  // first tile, ~1.2 tiles of work).  M2S_STEM_PARTS=n forces n (tests, A/B).
+  const char* fp = getenv("M2S_STEM_PARTS");
+  int parts = fp ? atoi(fp) : (cus * per_cu) / std::max(1, nstrip);
+  parts = std::max(1, std::min(parts, a.tiles_y));
+  a.tpp = ceil_div(a.tiles_y, parts);
+  a.parts = ceil_div(a.tiles_y, a.tpp);  // (no empty parts)
+  a.per_xcd = ceil_div(nstrip * a.parts, 8);
   const int grid = 8 * std::max(1, std::min(ceil_div(cus * per_cu, 8), a.per_xcd));
   if (split) {
     ProfScope ps("stem_b0_kernel<16, 1>", flops, bytes, s);

@@ -156,6 +156,24 @@ def test_config2_small_pass_plan(rt, weights, clip30, monkeypatch):
         np.testing.assert_allclose(small[k], big[k], atol=tol, rtol=0, err_msg=k)
 
 
+@pytest.mark.parametrize("dtype,nc,nf,parts", [("bf16", 8, 4, None), ("bf16x3", 1, 30, None), ("bf16x3", 2, 30, "3"),
+                                               ("bf16", 1, 30, "8")])
+def test_stem_strip_parts_bitwise(rt, weights, monkeypatch, dtype, nc, nf, parts):
+    """Small batches cut the fused stem's strips (image, 16-column tile column) into tile-row ranges so the units
+    fill the workgroup slots (stem_b0.hip): a range's first tile recomputes the S / A rows a whole strip carries
+    over from the tile above, with the same arithmetic, so the mel is bit-identical to whole strips
+    (M2S_STEM_PARTS=1).  parts None = the automatic cut (3 at 8 x 4 bf16, 2 at one bf16x3 clip); "3" = uneven
+    ranges (3 + 3 + 2 tile rows); "8" = one tile row a unit."""
+    ac = weights[0]
+    x = torch.from_numpy(synth.synth_frames(nc, nf, seed=311)).to(DEV)
+    if parts is not None:
+        monkeypatch.setenv("M2S_STEM_PARTS", parts)
+    a = rt.AcousticEngine(ac, dtype=dtype, device=DEV).forward(x).cpu().numpy()
+    monkeypatch.setenv("M2S_STEM_PARTS", "1")
+    b = rt.AcousticEngine(ac, dtype=dtype, device=DEV).forward(x).cpu().numpy()
+    assert np.isfinite(a).all() and np.array_equal(a, b)
+
+
 def test_config1_split_k_matches_unsplit(rt, weights, monkeypatch):
     """configs[1] (8 x 4, bf16): the SE GEMMs of the small pass run split K (fp32 partial sums added in split order by
     conv_gemm_ksum_kernel); against the unsplit launches (M2S_KSPLIT=1) the mel differs only by fp32 summation
