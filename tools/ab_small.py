@@ -20,7 +20,7 @@ ac_sd, gen_sd = synth.synth_acoustic_state(0), synth.synth_generator_state(0)
 mean, std = synth.synth_scaler()
 x2 = torch.rand(1, 30, 256, 256, device=dev)
 x1 = torch.rand(8, 4, 256, 256, device=dev)
-KEYS = ("M2S_KSPLIT", "M2S_KSPLIT_MAX", "M2S_KSPLIT_MINST", "M2S_IRWS_MIN", "M2S_SEWS_MIN", "M2S_STEM_PARTS")
+KEYS = ("M2S_KSPLIT", "M2S_KSPLIT_MAX", "M2S_KSPLIT_MINST", "M2S_IRWS_MIN", "M2S_SEWS_MIN", "M2S_STEM_PARTS", "M2S_SE_FOLD")
 
 
 def apply(s):

@@ -1,12 +1,13 @@
 #!/bin/bash
-# Round 6: stem strip parts (small batches): parity tests and the small-shape timings, parts automatic vs whole strips.
+# Round 6: small-pass changes (stem strip parts, SE excitation fold): parity tests (KSEL) and the small-shape timings
+# against the settings in ABSET.
 set -o pipefail
 TAG=${1:-r06p}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
-  -k "stem or config2 or config1 or effnet_bf16x3_every_block" > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
+  -k "${KSEL:-stem or config2 or config1 or effnet_bf16x3_every_block or se_excitation}" > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
 tail -2 "$OUT/pytest.log"
-timeout -k 10 300 python -u tools/ab_small.py "" "M2S_STEM_PARTS=1" > "$OUT/ab.txt" 2>&1 || { cat "$OUT/ab.txt"; exit 1; }
+timeout -k 10 300 python -u tools/ab_small.py "" ${ABSET:-"M2S_STEM_PARTS=1"} > "$OUT/ab.txt" 2>&1 || { cat "$OUT/ab.txt"; exit 1; }
 grep -v "^#" "$OUT/ab.txt"
