@@ -302,11 +302,42 @@ __global__ void __launch_bounds__(256, (BN >= 256 || (BM >= 256 && BN >= 128) ? 
   // ---- SE scale table for this workgroup's images (GEMM kind only) ---------------------------
   int img0 = 0;
   if constexpr (SE) {
+    // only this workgroup's K range (split K: 1 / nks of the channels), 8 channels a 16-byte load, every load of a
+    // thread issued before the first conversion (the element-wise loop over every channel was a chain of global
+    // round trips: configs[1] 1.065 -> 1.034 ms, configs[2] 2.254 -> 2.245 ms, gpurun_out/r06r)
     img0 = m0 / a.OH;
-    for (int i = tid; i < se_imgs * a.cs_in; i += 256) {
-      const int im = i / a.cs_in, c = i - (i / a.cs_in) * a.cs_in;
-      const bf16_t* g = static_cast<const bf16_t*>(a.in_scale) + (size_t)(img0 + im) * xs + c;
-      se_tab[i] = (img0 + im) * a.OH < a.M ? (SP == 1 ? bf2f(g[0]) + bf2f(g[a.cs_in]) : bf2f(g[0])) : 0.f;
+    const int c_lo = kb * 32, nc8 = (min(a.cs_in, (kb + nsteps) * 32) - c_lo) / 8, tot = se_imgs * nc8;
+    const bf16_t* gb = static_cast<const bf16_t*>(a.in_scale);
+    for (int i0 = tid; i0 < tot; i0 += 4 * 256) {
+      uint4 h[4], l[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 256 * u, im = i / max(nc8, 1), c = c_lo + 8 * (i - im * nc8);
+        h[u] = l[u] = make_uint4(0u, 0u, 0u, 0u);
+        if (i < tot && (img0 + im) * a.OH < a.M) {
+          const bf16_t* g = gb + (size_t)(img0 + im) * xs + c;
+          h[u] = *reinterpret_cast<const uint4*>(g);
+          if constexpr (SP == 1) l[u] = *reinterpret_cast<const uint4*>(g + a.cs_in);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 256 * u, im = i / max(nc8, 1), c = c_lo + 8 * (i - im * nc8);
+        if (i >= tot) break;
+        float v[8];
+        unpack_bf16x4(make_uint2(h[u].x, h[u].y), v);
+        unpack_bf16x4(make_uint2(h[u].z, h[u].w), v + 4);
+        if constexpr (SP == 1) {
+          float w[8];
+          unpack_bf16x4(make_uint2(l[u].x, l[u].y), w);
+          unpack_bf16x4(make_uint2(l[u].z, l[u].w), w + 4);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += w[e];
+        }
+        float* d = se_tab + im * a.cs_in + c;
+        *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
     }
   }
   // SE scale on the weight fragments when the tile is one image (its k-scales are shared by every
@@ -761,7 +792,7 @@ void launch_tile(const ConvBatch& b, hipStream_t s, int phases, double flops, do
   const int m_tiles = ceil_div(a.M, BM), n_tiles = ceil_div(a.cs_out, BN);
   int se_imgs = 0;
   if (a.in_xform == IN_SE_SCALE) {
-    M2S_CHECK(KIND == KIND_GEMM && a.OH > 0, "SE scale needs the GEMM kind with OH = rows per image");
+    M2S_CHECK(KIND == KIND_GEMM && a.OH > 0 && a.cs_in % 8 == 0, "SE scale needs the GEMM kind with OH = rows per image");
     se_imgs = se_images(BM, a.OH);
   }
   const size_t lds = (size_t)S * (R * (BM + BN) + 16) * ROW + (size_t)se_imgs * a.cs_in * sizeof(float);

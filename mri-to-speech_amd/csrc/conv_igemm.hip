@@ -97,7 +97,11 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int m_base = (blockIdx.x * 4 + wave) * (MT * 16);
+  // kw (ConvArgs::kwave): the four waves take the same MT x 16 rows and split the K chunks (chunk i to wave i % 4),
+  // adding their partial sums in LDS in a fixed order.  For the BiLSTM input projection of a small pass (M = 30
+  // frames) one wave walking 88 chunks x 32 MFMAs alone, three idle, was a 20 us launch on 80 workgroups.
+  const bool kw = a.kwave != 0;
+  const int m_base = kw ? blockIdx.x * (MT * 16) : (blockIdx.x * 4 + wave) * (MT * 16);
   const int n_base = blockIdx.y * (NT * 16);
   const int phase = blockIdx.z;
   if (m_base >= a.M) return;
@@ -152,6 +156,7 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
   const int cchunks = multi_tap ? 1 : a.cs_in / KC;
   const uint4 zero4 = make_uint4(0, 0, 0, 0);
 
+  int it = 0;  // K chunk counter (kw)
   for (int tap0 = 0; tap0 < a.ntaps; tap0 += a.tpc) {
     const int tap = tap0 + tap_off;
     long xo[MT];
@@ -185,6 +190,9 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
       wrow[ni] = W + (size_t)(n_base + ni * 16 + r16) * a.kp + (size_t)tap * a.cs_in + c_off;
 
     for (int cc = 0; cc < cchunks; ++cc) {
+      const bool mine = !kw || (it & 3) == wave;
+      ++it;
+      if (!mine) continue;
       uint4 bx[MT], aw[NT];
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi)
@@ -205,6 +213,25 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
 #pragma unroll
         for (int mi = 0; mi < MT; ++mi) mfma_step<T>(acc[ni][mi], aw[ni], bx[mi]);
     }
+  }
+
+  if (kw) {  // waves 1-3 hand their partial sums to wave 0: ((w0 + w1) + (w2 + w3))
+    extern __shared__ __attribute__((aligned(16))) char kw_lds[];
+    f32x4* red = reinterpret_cast<f32x4*>(kw_lds);  // [3][NT * MT][64]
+    if (wave > 0)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi) red[((wave - 1) * NT * MT + ni * MT + mi) * 64 + lane] = acc[ni][mi];
+    __syncthreads();
+    if (wave > 0) return;
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) {
+        const int i = ni * MT + mi;
+        acc[ni][mi] = (acc[ni][mi] + red[i * 64 + lane]) + (red[(NT * MT + i) * 64 + lane] + red[(2 * NT * MT + i) * 64 + lane]);
+      }
   }
 
   // ---- epilogue: bias, activation, residual, MRF accumulation; 4 channels per lane ----------
@@ -251,16 +278,19 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
 
 template <typename T, int MT, int NT, int KIND>
 void launch_tile(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
-  dim3 grid(ceil_div(a.M, 4 * MT * 16), ceil_div(a.cs_out, NT * 16), phases);
+  dim3 grid(ceil_div(a.M, (a.kwave ? 1 : 4) * MT * 16), ceil_div(a.cs_out, NT * 16), phases);
   M2S_CHECK(grid.y * NT * 16 <= a.n_pad, "conv: weight rows not padded to the N tile");
   char name[96];
   snprintf(name, sizeof(name), "conv_igemm_kernel<%s, %d, %d, %d>", sizeof(T) == 4 ? "float" : "unsigned short", MT, NT, KIND);
   ProfScope ps(name, flops, bytes, s);
-  hipLaunchKernelGGL((conv_igemm_kernel<T, MT, NT, KIND>), grid, dim3(256), 0, s, a);
+  const size_t lds = a.kwave ? (size_t)3 * NT * MT * 64 * sizeof(f32x4) : 0;  // the kernel's kw reduction
+  hipLaunchKernelGGL((conv_igemm_kernel<T, MT, NT, KIND>), grid, dim3(256), lds, s, a);
 }
 
 template <typename T, int KIND>
 void launch_kind(const ConvArgs& a, hipStream_t s, int phases, double flops, double bytes) {
+  if (a.kwave && a.cs_out > 32)  // K split over the waves: 16-column tiles spread the N dimension over more workgroups
+    return launch_tile<T, 2, 1, KIND>(a, s, phases, flops, bytes);
   if (a.cs_out <= 16)
     launch_tile<T, 4, 1, KIND>(a, s, phases, flops, bytes);
   else if (a.cs_out <= 32)

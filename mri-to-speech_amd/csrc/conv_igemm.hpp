@@ -51,6 +51,9 @@ struct ConvArgs {
   // split conv_gemm only (the pre-activated MRF chain, model.cpp Vocoder::run_t):
   float res_unslope;    // != 0: res holds lrelu(x); x = r > 0 ? r : r * res_unslope (slope 0.1 -> 10)
   int act_after_res;    // act applied after the residual add (y = lrelu(v + x)) instead of before it
+  // fp32 conv_igemm only: the four waves of a workgroup split the K chunks of one wave's rows (the BiLSTM input
+  // projection of a small pass, model.cpp)
+  int kwave;
 };
 
 // Up to CONV_BATCH 1-D convs of one shape (same kind, M, cs_in, cs_out, n_pad; own x / w / bias / res

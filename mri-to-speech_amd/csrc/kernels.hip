@@ -102,30 +102,27 @@ __global__ void __launch_bounds__(256) stem32_kernel(const float* __restrict__ f
 }
 
 // ---------------------------------------------------------------------------------------------
-// One image per workgroup: lane = channel (64 at a time), the four waves take every fourth position and their
-// partial sums meet in LDS in a fixed order (one thread per (image, channel) walking all P positions made a
-// 32-frame batch a 26-workgroup, 20 us launch)
+// One (image, 64-channel block) per workgroup: lane = channel, the four waves take every fourth position (four
+// independent chains each) and their partial sums meet in LDS in a fixed order.  (One image per workgroup walking
+// its 22 channel blocks was a 9.6 us launch at 32 frames; one thread per (image, channel) over all P positions 20 us.)
 template <typename T>
 __global__ void __launch_bounds__(256) gap_kernel(const T* __restrict__ x, int N, int P, int C, int cs,
                                                   float* __restrict__ feats) {
   __shared__ float part[4][64];
   const int n = blockIdx.x, q = threadIdx.x >> 6, l = threadIdx.x & 63;
-  for (int c0 = 0; c0 < C; c0 += 64) {
-    const int c = c0 + l;
-    float a0 = 0.f, a1 = 0.f;
-    if (c < C) {
-      int k = q;
-      for (; k + 4 < P; k += 8) {
-        a0 += act_ld<T>(x, (long)n * P + k, cs, c);
-        a1 += act_ld<T>(x, (long)n * P + k + 4, cs, c);
-      }
-      if (k < P) a0 += act_ld<T>(x, (long)n * P + k, cs, c);
+  const int c = blockIdx.y * 64 + l;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    int k = q;
+    for (; k + 12 < P; k += 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] += act_ld<T>(x, (long)n * P + k + 4 * j, cs, c);
     }
-    if (c0 > 0) __syncthreads();  // the previous channel block's partials were read
-    part[q][l] = a0 + a1;
-    __syncthreads();
-    if (q == 0 && c < C) feats[(long)n * C + c] = ((part[0][l] + part[1][l]) + (part[2][l] + part[3][l])) / (float)P;
+    for (; k < P; k += 4) a[0] += act_ld<T>(x, (long)n * P + k, cs, c);
   }
+  part[q][l] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (q == 0 && c < C) feats[(long)n * C + c] = ((part[0][l] + part[1][l]) + (part[2][l] + part[3][l])) / (float)P;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -181,20 +178,21 @@ __global__ void __launch_bounds__(256) lstm_step_kernel(const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) mel_head_kernel(const float* __restrict__ hs, int rows, int H,
-                                                       const float* __restrict__ wt, const float* __restrict__ b,
-                                                       int n_mels, float* __restrict__ out) {
-  // one output row (frame) per workgroup: y = h_fwd + h_bwd staged in LDS, lane = mel (n_mels <= 64), the
-  // four waves take a quarter of K each with four independent FMA chains, the quarters added in a fixed order
-  // (a 640-long dependent FMA chain per thread made a 30-frame clip's head a 26 us launch)
-  extern __shared__ float ys[];  // [H] + [4][64] partial sums
+constexpr int HEAD_W = 16;  // waves of a mel_head workgroup (the K split)
+__global__ void __launch_bounds__(64 * HEAD_W) mel_head_kernel(const float* __restrict__ hs, int rows, int H,
+                                                              const float* __restrict__ wt, const float* __restrict__ b,
+                                                              int n_mels, float* __restrict__ out) {
+  // one output row (frame) per workgroup: y = h_fwd + h_bwd staged in LDS, lane = mel (n_mels <= 64), the 16 waves
+  // take a sixteenth of K each with four independent FMA chains, the partials added in a fixed order (four waves
+  // made a 32-frame head a 14 us launch of 160-long load chains; a 640-long chain per thread 26 us)
+  extern __shared__ float ys[];  // [H] + [HEAD_W][64] partial sums
   float* part = ys + H;
   const int row = blockIdx.x;
   const long plane = (long)rows * H;
-  for (int k = threadIdx.x; k < H; k += 256) ys[k] = hs[(long)row * H + k] + hs[plane + (long)row * H + k];
+  for (int k = threadIdx.x; k < H; k += 64 * HEAD_W) ys[k] = hs[(long)row * H + k] + hs[plane + (long)row * H + k];
   __syncthreads();
   const int q = threadIdx.x >> 6;
-  const int k0 = q * H / 4, k1 = (q + 1) * H / 4;
+  const int k0 = q * H / HEAD_W, k1 = (q + 1) * H / HEAD_W;
   for (int nb = 0; nb < n_mels; nb += 64) {  // 64 mels a pass (the reference's n_mels = 64: one pass)
     const int n = nb + (threadIdx.x & 63);
     float a[4] = {0.f, 0.f, 0.f, 0.f};
@@ -210,7 +208,16 @@ __global__ void __launch_bounds__(256) mel_head_kernel(const float* __restrict__
     part[threadIdx.x] = (a[0] + a[1]) + (a[2] + a[3]);
     __syncthreads();
     const int l = threadIdx.x & 63;
-    if (q == 0 && n < n_mels) out[(long)row * n_mels + n] = ((part[l] + part[64 + l]) + (part[128 + l] + part[192 + l])) + b[n];
+    if (q == 0 && n < n_mels) {
+      float t[HEAD_W];
+#pragma unroll
+      for (int w = 0; w < HEAD_W; ++w) t[w] = part[64 * w + l];
+#pragma unroll
+      for (int st = 1; st < HEAD_W; st *= 2)  // pairwise, fixed order
+#pragma unroll
+        for (int w = 0; w < HEAD_W; w += 2 * st) t[w] += t[w + st];
+      out[(long)row * n_mels + n] = t[0] + b[n];
+    }
   }
 }
 
@@ -374,7 +381,7 @@ void launch_stem(const float* frames, int N, int H, int W, int OH, int OW, int p
 template <typename T>
 void launch_gap(const T* x, int N, int P, int C, int cs, float* feats, hipStream_t s) {
   if (N <= 0) return;
-  hipLaunchKernelGGL(gap_kernel<T>, dim3(N), dim3(256), 0, s, x, N, P, C, cs, feats);
+  hipLaunchKernelGGL(gap_kernel<T>, dim3(N, ceil_div(C, 64)), dim3(256), 0, s, x, N, P, C, cs, feats);
   M2S_HIP(hipGetLastError());
 }
 
@@ -389,7 +396,8 @@ void launch_lstm_step(const float* pre, const float* whh, float* hs, float* cst,
 void launch_mel_head(const float* hs, int rows, int H, const float* wt, const float* b, int n_mels, float* out,
                      hipStream_t s) {
   M2S_CHECK(n_mels >= 1 && H >= 4, "mel_head: shape");
-  hipLaunchKernelGGL(mel_head_kernel, dim3(rows), dim3(256), (H + 4 * 64) * sizeof(float), s, hs, rows, H, wt, b, n_mels, out);
+  hipLaunchKernelGGL(mel_head_kernel, dim3(rows), dim3(64 * HEAD_W), (H + HEAD_W * 64) * sizeof(float), s, hs, rows, H, wt, b,
+                     n_mels, out);
   M2S_HIP(hipGetLastError());
 }
 

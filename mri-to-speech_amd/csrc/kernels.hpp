@@ -236,8 +236,10 @@ size_t lstm_persistent_sync_bytes();
 // counter barrier, VALU dot products (lstm_persistent.hip).  `sync` = lstm_small_sync_bytes().
 bool lstm_small_supported(int B, int H);
 size_t lstm_small_sync_bytes();
+// epoch: the engine's epoch count for a sync buffer of its own (tags continue across calls, no memset; null = zero
+// the buffer every call)
 void launch_lstm_small(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,
-                       unsigned* err_host, hipStream_t s);
+                       unsigned* err_host, hipStream_t s, unsigned* epoch = nullptr);
 constexpr unsigned LSTM_SPIN_MAX = 1u << 24;
 // 4 < B <= 64: the same granule exchange with 512-thread workgroups, sequences in chunks of 16 whose
 // sweep overlaps the previous chunk's dot products (lstm_persistent.hip).  `sync` = lstm_mid_sync_bytes().
@@ -250,11 +252,11 @@ void launch_lstm_persistent(const float* pre, const float* whh, float* hs, int B
 // B > 4 in split fp32 (the bf16x3 / bf16 / fp8 engines): three bf16 MFMA terms over W_hh and h_t split
 // hi / lo, h_t published split by write-through stores behind per-workgroup flags (no fences).
 // Split engines, 5..16 sequences: lstm_x3's arithmetic with the h_t hand-off as data-tagged granules (no flag round
-// trip, no store drain); `sync` = lstm_x3g_sync_bytes() (tags reset by the launcher).  (lstm_persistent.hip)
+// trip, no store drain); `sync` = lstm_x3g_sync_bytes() (epoch-tagged, see launch_lstm_small).  (lstm_persistent.hip)
 bool lstm_x3g_supported(int B, int H);
 size_t lstm_x3g_sync_bytes();
 void launch_lstm_x3g(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,
-                     unsigned* err_host, hipStream_t s);
+                     unsigned* err_host, hipStream_t s, unsigned* epoch = nullptr);
 // `sync` = lstm_x3_sync_bytes() (flags reset by the launcher).
 size_t lstm_x3_sync_bytes();
 void launch_lstm_x3(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,

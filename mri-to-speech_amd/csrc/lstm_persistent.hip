@@ -410,7 +410,7 @@ constexpr int LG_PAIRS = LP_H / 2;                     // 16-byte granule pairs 
 __global__ void __launch_bounds__(64 * LX_W, 1) lstm_x3g_kernel(const float* __restrict__ pre, const float* __restrict__ whh,
                                                                  float* hs, int B, int T, unsigned* err,
                                                                  unsigned long long* gran, unsigned spin_max,
-                                                                 unsigned* err_host) {
+                                                                 unsigned* err_host, unsigned ep) {
   __shared__ float red[LX_W][2 * 32][LX_S + 1];
   __shared__ float cst[LX_U][LG_BMAX];
   __shared__ __attribute__((aligned(16))) char hxl[LG_BMAX * LG_ROWB];
@@ -482,11 +482,11 @@ __global__ void __launch_bounds__(64 * LX_W, 1) lstm_x3g_kernel(const float* __r
 #pragma unroll
         for (int j = 0; j < PJ; ++j) {
           const int q = tid + 64 * LX_W * j;
-          stale |= q < nb * LG_PAIRS && (v[j][1] != (unsigned)step || v[j][3] != (unsigned)step);
+          stale |= q < nb * LG_PAIRS && (v[j][1] != ep + (unsigned)step || v[j][3] != ep + (unsigned)step);
         }
         if (!stale && spin_max != 0) break;
-        if (spins >= spin_max || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (spins >= spin_max || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ep + 1u) {
+          __hip_atomic_store(err, ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           abort_flag = 1;
           break;
         }
@@ -494,7 +494,7 @@ __global__ void __launch_bounds__(64 * LX_W, 1) lstm_x3g_kernel(const float* __r
 #pragma unroll
         for (int j = 0; j < PJ; ++j) {
           const int q = tid + 64 * LX_W * j;
-          if (q < nb * LG_PAIRS && (v[j][1] != (unsigned)step || v[j][3] != (unsigned)step))
+          if (q < nb * LG_PAIRS && (v[j][1] != ep + (unsigned)step || v[j][3] != ep + (unsigned)step))
             v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, q * 16, 0, 16);
         }
       }
@@ -564,7 +564,8 @@ __global__ void __launch_bounds__(64 * LX_W, 1) lstm_x3g_kernel(const float* __r
       if (step + 1 < T) {
         const bf16_t hb = f2bf(h), lb = f2bf(h - bf2f(hb));  // the split of sp_t (17 bits)
         __hip_atomic_store(gd + (size_t)(step & 1) * LG_BMAX * H + (size_t)cb * H + ug * LX_U + cu,
-                           ((unsigned long long)(step + 1) << 32) | ((unsigned)lb << 16) | (unsigned)hb, __ATOMIC_RELAXED,
+                           ((unsigned long long)(ep + (unsigned)step + 1u) << 32) | ((unsigned)lb << 16) | (unsigned)hb,
+                           __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -588,7 +589,8 @@ constexpr int LS_BCAP = 8;   // largest instantiation (M2S_LSTM_SMALL_B = 8 sele
 template <int LS_BMAX>
 __global__ void __launch_bounds__(256, 1) lstm_small_kernel(const float* __restrict__ pre, const float* __restrict__ whh,
                                                             float* hs, int B, int T, unsigned long long* gran,
-                                                            unsigned* err, unsigned spin_max, unsigned* err_host) {
+                                                            unsigned* err, unsigned spin_max, unsigned* err_host,
+                                                            unsigned ep) {
   __shared__ __attribute__((aligned(16))) float hsh[LS_BMAX][LP_H];  // h_{t-1}, all units
   __shared__ float red[8][32][LS_BMAX];                              // [K slice][gate row][sequence]
   __shared__ float cst[LP_U][LS_BMAX];
@@ -630,11 +632,11 @@ __global__ void __launch_bounds__(256, 1) lstm_small_kernel(const float* __restr
       for (int i = tid; i < B * H && ok; i += 256) {
         unsigned spins = 0;
         unsigned long long x;
-        while (((x = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != (unsigned)step ||
+        while (((x = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != ep + (unsigned)step ||
                spin_max == 0) {
           __builtin_amdgcn_s_sleep(1);
-          if (++spins > spin_max || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (++spins > spin_max || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ep + 1u) {
+            __hip_atomic_store(err, ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             abort_flag = 1;
             ok = false;
             break;
@@ -693,7 +695,7 @@ __global__ void __launch_bounds__(256, 1) lstm_small_kernel(const float* __restr
       hsd[((size_t)b * T + t) * H + unit] = h;
       if (step + 1 < T)
         __hip_atomic_store(gd + (size_t)(step & 1) * LS_BMAX * H + (size_t)b * H + unit,
-                           ((unsigned long long)(step + 1) << 32) | __float_as_uint(h), __ATOMIC_RELAXED,
+                           ((unsigned long long)(ep + (unsigned)step + 1u) << 32) | __float_as_uint(h), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();  // red and hsh are rewritten next step
@@ -918,10 +920,28 @@ bool lstm_persistent_supported(int H) { return H == LP_H; }
 
 bool lstm_small_supported(int B, int H) { return H == LP_H && B >= 1 && B <= small_cap(); }
 
+// Epoch tags for the granule hand-off (lstm_small, lstm_x3g): a launch publishes tags ep + step + 1 and waits for
+// ep + step, its timeout mark is ep + 1, and the engine's counter advances by T + 1 a launch, so every tag and mark of
+// an older launch is below every tag this one waits for: no memset node before each call (a ~4.6 us launch of a
+// 30-frame pass's ~1 ms).  The buffer is zeroed (and the count restarted) on first use, near the wrap, and under
+// stream capture, whose replays would repeat one epoch.
+unsigned lstm_epoch(void* sync, size_t bytes, int T, unsigned* epoch, hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  M2S_HIP(hipStreamIsCapturing(s, &cs));
+  if (!epoch || *epoch == 0 || cs != hipStreamCaptureStatusNone || *epoch > 0xF0000000u - (unsigned)T) {
+    M2S_HIP(hipMemsetAsync(sync, 0, bytes, s));
+    if (epoch) *epoch = (unsigned)T + 1u;
+    return 0u;
+  }
+  const unsigned e = *epoch;
+  *epoch += (unsigned)T + 1u;
+  return e;
+}
+
 size_t lstm_small_sync_bytes() { return 256 + (size_t)2 * 2 * LS_BCAP * LP_H * sizeof(unsigned long long); }
 
 void launch_lstm_small(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,
-                       unsigned* err_host, hipStream_t s) {
+                       unsigned* err_host, hipStream_t s, unsigned* epoch) {
   M2S_CHECK(lstm_small_supported(B, H) && T > 0, "lstm_small: unsupported shape");
   const int grid = 2 * (H / LP_U);
   const bool b8 = B > LS_BMAX;  // the 8-sequence instantiation (M2S_LSTM_SMALL_B = 8)
@@ -929,16 +949,16 @@ void launch_lstm_small(const float* pre, const float* whh, float* hs, int B, int
                       : reinterpret_cast<const void*>(&lstm_small_kernel<LS_BMAX>);
   const int resident = device_resident(fn, 256, 0);
   M2S_CHECK(grid <= resident, "lstm_small: grid not co-resident on this device");
-  // [256 B: error word][granules 2 dir x 2 parity x LS_BMAX x H]: every tag restarts at 0 each call
-  M2S_HIP(hipMemsetAsync(sync, 0, lstm_small_sync_bytes(), s));
+  // [256 B: error word][granules 2 dir x 2 parity x LS_BMAX x H], epoch-tagged (lstm_epoch)
+  const unsigned ep = lstm_epoch(sync, lstm_small_sync_bytes(), T, epoch, s);
   unsigned* err = static_cast<unsigned*>(sync);
   unsigned long long* gran = reinterpret_cast<unsigned long long*>(static_cast<char*>(sync) + 256);
   if (b8)
     hipLaunchKernelGGL(lstm_small_kernel<LS_BCAP>, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, T, gran, err, spin_max,
-                       err_host);
+                       err_host, ep);
   else
     hipLaunchKernelGGL(lstm_small_kernel<LS_BMAX>, dim3(grid), dim3(256), 0, s, pre, whh, hs, B, T, gran, err, spin_max,
-                       err_host);
+                       err_host, ep);
   M2S_HIP(hipGetLastError());
 }
 
@@ -988,17 +1008,17 @@ size_t lstm_x3g_sync_bytes() { return 256 + (size_t)2 * 2 * LG_BMAX * LP_H * siz
 bool lstm_x3g_supported(int B, int H) { return H == LP_H && B >= 1 && B <= LG_BMAX; }
 
 void launch_lstm_x3g(const float* pre, const float* whh, float* hs, int B, int T, int H, void* sync, unsigned spin_max,
-                     unsigned* err_host, hipStream_t s) {
+                     unsigned* err_host, hipStream_t s, unsigned* epoch) {
   M2S_CHECK(lstm_x3g_supported(B, H) && T > 0, "lstm_x3g: unsupported shape");
   const int grid = 2 * LX_G;  // (direction, unit group): one row of <= 16 sequences
   const int resident = device_resident(reinterpret_cast<const void*>(&lstm_x3g_kernel), 64 * LX_W, LX_PAD_LDS);
   M2S_CHECK(grid <= resident, "lstm_x3g: grid not co-resident on this device");
-  // [256 B: error word][granules 2 dir x 2 parity x LG_BMAX x H]: every tag restarts at 0 each call
-  M2S_HIP(hipMemsetAsync(sync, 0, lstm_x3g_sync_bytes(), s));
+  // [256 B: error word][granules 2 dir x 2 parity x LG_BMAX x H], epoch-tagged (lstm_epoch)
+  const unsigned ep = lstm_epoch(sync, lstm_x3g_sync_bytes(), T, epoch, s);
   unsigned* err = static_cast<unsigned*>(sync);
   unsigned long long* gran = reinterpret_cast<unsigned long long*>(static_cast<char*>(sync) + 256);
   hipLaunchKernelGGL(lstm_x3g_kernel, dim3(grid), dim3(64 * LX_W), LX_PAD_LDS, s, pre, whh, hs, B, T, err, gran, spin_max,
-                     err_host);
+                     err_host, ep);
   M2S_HIP(hipGetLastError());
 }
 

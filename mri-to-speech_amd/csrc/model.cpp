@@ -491,6 +491,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
   M2S_HIP(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
   *err_host_ = 0;
   M2S_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0));
+  M2S_HIP(hipMalloc(&gsync_, std::max(lstm_small_sync_bytes(), lstm_x3g_sync_bytes())));
   for (auto& b : blocks_) {
     b.c1.resolve(arena_);
     if (b.type != 0) b.c2.resolve(arena_);
@@ -504,6 +505,7 @@ Acoustic::Acoustic(const StateDict& sd, int n_mels, int hidden, int dtype, int d
 
 Acoustic::~Acoustic() {
   if (err_host_) (void)hipHostFree(err_host_);
+  if (gsync_) (void)hipFree(gsync_);
 }
 
 unsigned Acoustic::take_async_error() { return __atomic_exchange_n(err_host_, 0u, __ATOMIC_ACQ_REL); }
@@ -953,15 +955,21 @@ void Acoustic::bilstm(const float* feats, int B, int T, float* y, float* mel_nor
   a.x = feats;
   a.y = pre;
   a.M = (int)BT;
+  // small passes (<= 64 frames): the four waves of a row tile split K (one 30-frame clip: 20 -> 12 us); larger passes
+  // keep four row groups a workgroup sharing the weight tile (K split there: the 1920-frame step's projection
+  // 0.13 ms slower).  The K summation order therefore differs between the two size classes (fp32 rounding only).
+  a.kwave = BT <= 64 ? 1 : 0;
   run_conv<float>(a, lstm_ih_, s);
   void* sync = ws.take<char>(std::max({lstm_persistent_sync_bytes(), lstm_small_sync_bytes(), lstm_mid_sync_bytes(), lstm_x3_sync_bytes(), lstm_x3g_sync_bytes()}));
   if (lstm_persistent_ && lstm_small_supported(B, H)) {
     ProfScope ps("lstm_small_kernel", 2.0 * 2 * B * 4.0 * H * H * (T - 1), 4.0 * 2 * 4 * H * H + 4.0 * BT * (8.0 * H + 2.0 * H), s);
-    launch_lstm_small(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, lstm_spin_max_, err_dev_, s);
+    launch_lstm_small(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, gsync_, lstm_spin_max_, err_dev_, s,
+                      &gsync_epoch_);
   } else if (lstm_persistent_ && lstm_x3_ && lstm_x3g_ && dtype_ != M2S_DT_F32 && lstm_x3g_supported(B, H)) {
     // 5..16 sequences (configs[4]'s 8 clips a GPU): the granule hand-off (lstm_persistent.hip lstm_x3g_kernel)
     ProfScope ps("lstm_x3g_kernel", 3.0 * 2 * B * 4.0 * H * H * (T - 1), 4.0 * 2 * 4 * H * H + 4.0 * BT * (8.0 * H + 2.0 * H), s);
-    launch_lstm_x3g(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, sync, lstm_spin_max_, err_dev_, s);
+    launch_lstm_x3g(pre, static_cast<const float*>(arena_.ptr(whh_)), hs, B, T, H, gsync_, lstm_spin_max_, err_dev_, s,
+                    &gsync_epoch_);
   } else if (lstm_persistent_ && lstm_x3_ && dtype_ != M2S_DT_F32 && lstm_persistent_supported(H)) {
     // split engines above the small-batch kernel: 4.1 / 5.2 / 9.9 us per step at B = 8 / 16 / 64 against
     // lstm_mid's 7.2 / 11.9 and the f32 counter-barrier kernel's 24 (gpurun_out lstm2, lstm3_x3small)

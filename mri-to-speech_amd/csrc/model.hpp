@@ -186,6 +186,10 @@ class Acoustic {
   int max_mid_cs_ = 0;
   unsigned* err_host_ = nullptr;  // pinned, host-mapped: set by lstm_persistent_kernel on a barrier timeout
   unsigned* err_dev_ = nullptr;
+  // the granule BiLSTM kernels' sync buffer (lstm_small / lstm_x3g), zeroed once, and its epoch count
+  // (lstm_persistent.hip lstm_epoch)
+  void* gsync_ = nullptr;
+  unsigned gsync_epoch_ = 0;
 };
 
 class Vocoder {

@@ -389,6 +389,26 @@ def test_preprocess_vs_oracle_shapes_and_bgr(rt, shape):
     np.testing.assert_allclose(out, ref, atol=1e-6, rtol=0)
 
 
+def test_bilstm_epoch_tags_across_calls(rt, ac_state):
+    """The granule BiLSTM kernels (lstm_small B = 1, lstm_x3g B = 5..16) keep one sync buffer per engine whose tags
+    continue an epoch count instead of a memset per call (lstm_persistent.hip lstm_epoch): calls of both kinds and
+    different lengths interleaved on one engine give bit-identical outputs to fresh engines (a stale granule of an
+    earlier call never passes for a current one)."""
+    eng = rt.AcousticEngine(ac_state[1], dtype="bf16x3", device=DEV)
+    xs = [torch.randn(b, t, 208, device=DEV, generator=torch.Generator(device=DEV).manual_seed(40 + i))
+          for i, (b, t) in enumerate([(1, 30), (8, 50), (1, 31), (8, 17), (12, 30)])]
+    want = []
+    for x in xs:
+        fresh = rt.AcousticEngine(ac_state[1], dtype="bf16x3", device=DEV)
+        want.append(fresh.bilstm(x)[0].cpu())
+        fresh.check()
+    for rnd in range(3):
+        for x, w in zip(xs, want):
+            y = eng.bilstm(x)[0].cpu()
+            eng.check()
+            assert torch.equal(y, w), (rnd, tuple(x.shape))
+
+
 # ------------------------------------------------------------------------------ asynchronous failure report
 @pytest.mark.parametrize("B,dtype", [(1, "fp32"), (8, "fp32"), (12, "fp32"), (70, "fp32"), (8, "bf16x3"), (70, "bf16x3")])
 def test_bilstm_barrier_timeout_is_reported(rt, ac_state, B, dtype):

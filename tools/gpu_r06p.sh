@@ -11,3 +11,6 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -2 "$OUT/pytest.log"
 timeout -k 10 300 python -u tools/ab_small.py "" ${ABSET:-"M2S_STEM_PARTS=1"} > "$OUT/ab.txt" 2>&1 || { cat "$OUT/ab.txt"; exit 1; }
 grep -v "^#" "$OUT/ab.txt"
+if [ -n "$TIMELINE" ]; then bash tools/gpu_small.sh "$TAG/small" || exit 1; fi
+if [ -n "$BENCH" ]; then bash tools/ab_bench_stages.sh "$TAG/bench" M2S_DUMMY_SWITCH 1 "0" || exit 1; fi
+if [ -n "$GRAPH" ]; then timeout -k 10 300 python -u tools/graph_small.py > "$OUT/graph.txt" 2>&1 || { tail -20 "$OUT/graph.txt"; exit 1; }; grep -v "^#" "$OUT/graph.txt"; fi
