@@ -83,10 +83,14 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(const HaloArgs a) {
   const int mstride = gridDim.x / a.n_tiles;
   int mt = blockIdx.x / a.n_tiles;
 
+  // the zero page's address in SGPRs for the whole kernel: named directly in the DMA loops it was re-fetched from the
+  // GOT (s_getpc + s_load + s_waitcnt lgkmcnt(0), which also drains the wave's LDS reads) at every piece
+  const void* zpage = g_halo_zero;
+  asm volatile("" : "+s"(zpage));
   // ---- weights of this N tile -> LDS, once ----------------------------------------------------
   for (int blk = wave; blk < nsteps * BN / 16; blk += 4) {
     const int row = blk * 16 + lrow, st = row / BN, n = n0 + (row - st * BN);
-    const void* src = n < a.n_pad ? (const void*)(a.w + (size_t)n * a.kp + st * 32 + q * 8) : (const void*)g_halo_zero;
+    const void* src = n < a.n_pad ? (const void*)(a.w + (size_t)n * a.kp + st * 32 + q * 8) : zpage;
     dma16(src, wbuf + blk * 16 * ROWB);
   }
 
@@ -106,7 +110,7 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(const HaloArgs a) {
       }
       const int hy = hp / HW, hx = hp - (hp / HW) * HW;
       const int iy = ty0 + hy, ix = tx0 + hx;
-      const void* src = g_halo_zero;
+      const void* src = zpage;
       if (row < hrows && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
         src = xi + ((size_t)iy * a.W + ix) * a.cs_in + coff;
       dma16(src, hb + blk * 16 * ROWB);

@@ -67,6 +67,10 @@ __global__ void __launch_bounds__(512, 1) er2_fused_kernel(const Er2Args a) {
   const int g = lane >> 4, r16 = lane & 15;
   const int tpi = a.tiles_x * a.tiles_y, ntiles = a.N * tpi;
 
+  // the zero page's address in SGPRs for the whole kernel: named directly in the DMA loops it was re-fetched from the
+  // GOT (s_getpc + s_load + s_waitcnt lgkmcnt(0), which also drains the wave's LDS reads) at every piece
+  const void* zpage = g_er2_zero;
+  asm volatile("" : "+s"(zpage));
   auto stage_dma = [&](int ls, int slot) {  // 2 pieces per wave
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -83,7 +87,7 @@ __global__ void __launch_bounds__(512, 1) er2_fused_kernel(const Er2Args a) {
       const int piece = wave * 6 + j, c = piece / 6, pb = piece - c * 6;
       const int p = pb * 64 + lane, hy = p / E2_HW, hx = p - hy * E2_HW;
       const int iy = ty0 + hy, ix = tx0 + hx;
-      const void* src = g_er2_zero;
+      const void* src = zpage;
       if (p < E2_HPIX && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) src = xi + ((size_t)iy * a.W + ix) * 64 + c * 8;
       dma16(src, buf + c * E2_PLANE + pb * 1024);
     }

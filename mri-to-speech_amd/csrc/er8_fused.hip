@@ -107,6 +107,10 @@ __global__ void __launch_bounds__(512, 1) er8_fused_kernel(const Er8Args a) {
   const int J = count(half), J0 = count(0);
 
   // this wave's 3 halo pieces of tile T: plane c, 64-pixel block pb
+  // the zero page's address in SGPRs for the whole kernel: named directly in the DMA loops it was re-fetched from the
+  // GOT (s_getpc + s_load + s_waitcnt lgkmcnt(0), which also drains the wave's LDS reads) at every piece
+  const void* zpage = g_er8_zero;
+  asm volatile("" : "+s"(zpage));
   auto issue_halo = [&](int T, char* buf) {
     const int n = T / tpi, tr = T - n * tpi;
     const int ty0 = (tr / a.tiles_x) * E8_TH - 1, tx0 = (tr - (tr / a.tiles_x) * a.tiles_x) * E8_TW - 1;
@@ -116,7 +120,7 @@ __global__ void __launch_bounds__(512, 1) er8_fused_kernel(const Er8Args a) {
       const int piece = lw * 3 + j, c = piece / 3, pb = piece - c * 3;
       const int p = pb * 64 + lane, hy = p / E8_HW, hx = p - hy * E8_HW;
       const int iy = ty0 + hy, ix = tx0 + hx;
-      const void* src = g_er8_zero;
+      const void* src = zpage;
       if (p < E8_HPIX && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) src = xi + ((size_t)iy * a.W + ix) * 32 + c * 8;
       dma16(src, buf + c * E8_PLANE + pb * 1024);
     }
@@ -131,7 +135,7 @@ __global__ void __launch_bounds__(512, 1) er8_fused_kernel(const Er8Args a) {
       const int pl = piece / 3, pb = piece - pl * 3;
       const int p = pb * 64 + lane, hy = p / E8_HW, hx = p - hy * E8_HW;
       const int iy = ty0 + hy, ix = tx0 + hx;
-      const void* src = g_er8_zero;
+      const void* src = zpage;
       if (p < E8_HPIX && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) src = xi + ((size_t)iy * a.W + ix) * 32 + pl * 16;
       dma16(src, buf + pl * E8_P8 + pb * 1024);
     }

@@ -93,6 +93,10 @@ __global__ void __launch_bounds__(512, 1) er8w_fused_kernel(const Er8wArgs a) {
 
   // stage ls of the stream -> ring slot: conv_exp K steps 4 pieces a wave (n16 tiles 2 wave, 2 wave + 1), the
   // conv_pwl stage 2 pieces a wave
+  // the zero page's address in SGPRs for the whole kernel: named directly in the DMA loops it was re-fetched from the
+  // GOT (s_getpc + s_load + s_waitcnt lgkmcnt(0), which also drains the wave's LDS reads) at every piece
+  const void* zpage = g_er8w_zero;
+  asm volatile("" : "+s"(zpage));
   auto stage_dma = [&](int ls, int slot) {
     int ln = lane;
     asm volatile("" : "+v"(ln));  // rebuilt per call: hoisted lane offsets cost registers
@@ -123,7 +127,7 @@ __global__ void __launch_bounds__(512, 1) er8w_fused_kernel(const Er8wArgs a) {
       const int piece = wave * 3 + j, pl = piece / 12, pb = piece - pl * 12;
       const int hp = pb * 32 + (ln >> 1), hy = hp / EW_HW, hx = hp - hy * EW_HW;
       const int iy = ty0 + hy, ix = tx0 + hx;
-      const void* src = g_er8w_zero;
+      const void* src = zpage;
       if (hp < EW_HPIX && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
         src = xi + ((size_t)iy * a.W + ix) * 64 + pl * 32 + (ln & 1) * 16;
       dma16(src, sm0 + (uint32_t)(EW_HALO0 + buf * EW_BUF + (pl ? EW_PB : 0) + pb * 1024));

@@ -68,6 +68,10 @@ __global__ void __launch_bounds__(512, 1) er_fused_kernel(const ErArgs a) {
   const int tpi = a.tiles_x * a.tiles_y, ntiles = a.N * tpi;
 
   // this wave's 3 halo pieces per tile: plane c, 64-pixel block pb
+  // the zero page's address in SGPRs for the whole kernel: named directly in the DMA loops it was re-fetched from the
+  // GOT (s_getpc + s_load + s_waitcnt lgkmcnt(0), which also drains the wave's LDS reads) at every piece
+  const void* zpage = g_er_zero;
+  asm volatile("" : "+s"(zpage));
   auto issue_halo = [&](int tile, char* buf) {
     const int n = tile / tpi, tr = tile - n * tpi;
     const int ty0 = (tr / a.tiles_x) * ER_TW - 1, tx0 = (tr - (tr / a.tiles_x) * a.tiles_x) * ER_TW - 1;
@@ -77,7 +81,7 @@ __global__ void __launch_bounds__(512, 1) er_fused_kernel(const ErArgs a) {
       const int piece = wave * 3 + j, c = piece / 6, pb = piece - c * 6;
       const int p = pb * 64 + lane, hy = p / ER_HW, hx = p - hy * ER_HW;
       const int iy = ty0 + hy, ix = tx0 + hx;
-      const void* src = g_er_zero;
+      const void* src = zpage;
       if (p < ER_HPIX && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) src = xi + ((size_t)iy * a.W + ix) * 32 + c * 8;
       dma16(src, buf + c * ER_PLANE + pb * 1024);
     }

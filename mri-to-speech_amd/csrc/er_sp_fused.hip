@@ -101,11 +101,15 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) er_sp_kernel(const E
   const int g = lane >> 4, r16 = lane & 15;
   const int tpi = a.tiles_x * a.tiles_y, ntiles = a.N * tpi;
 
+  // the zero page's address in SGPRs for the whole kernel: named directly in the DMA loops it was re-fetched from the
+  // GOT (s_getpc + s_load + s_waitcnt lgkmcnt(0), which also drains the wave's LDS reads) at every piece
+  const void* zpage = g_ersp_zero;
+  asm volatile("" : "+s"(zpage));
   auto stage_dma = [&](int ls, int slot) {
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
       const int piece = wave * PPW + j;
-      const void* src = piece < MRG * NT ? (const void*)(a.wst + ((size_t)(ls * MRG * NT + piece) * 64 + lane) * 8) : (const void*)g_ersp_zero;
+      const void* src = piece < MRG * NT ? (const void*)(a.wst + ((size_t)(ls * MRG * NT + piece) * 64 + lane) * 8) : zpage;
       dma16(src, ring + slot * SLOT + piece * 1024);
     }
   };
@@ -118,7 +122,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) er_sp_kernel(const E
       const int piece = wave * HP + j, pc = piece / HPB, pb = piece - pc * HPB;  // pc = plane * CH + chunk
       const int p = pb * 64 + lane, hy = p / HW, hx = p - hy * HW;
       const int iy = ty0 + hy, ix = tx0 + hx;
-      const void* src = g_ersp_zero;
+      const void* src = zpage;
       if (p < HPIX && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
         src = xi + ((size_t)iy * a.W + ix) * (2 * CSI) + (pc / CH) * CSI + (pc % CH) * 8;
       dma16(src, buf + pc * HPLANE + pb * 1024);

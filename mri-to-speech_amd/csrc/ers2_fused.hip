@@ -76,6 +76,10 @@ __global__ void __launch_bounds__(512, (CIN == 16 ? 2 : 1)) ers2_fused_kernel(co
   const int g = lane >> 4, r16 = lane & 15;
   const int tpi = a.tiles_x * a.tiles_y, ntiles = a.N * tpi;
 
+  // the zero page's address in SGPRs for the whole kernel: named directly in the DMA loops it was re-fetched from the
+  // GOT (s_getpc + s_load + s_waitcnt lgkmcnt(0), which also drains the wave's LDS reads) at every piece
+  const void* zpage = g_es2_zero;
+  asm volatile("" : "+s"(zpage));
   auto issue_halo = [&](int tile, char* buf) {
     const int n = tile / tpi, tr = tile - n * tpi, ty = tr / a.tiles_x, tx = tr - ty * a.tiles_x;
     const int iy0 = 2 * ES_TH * ty - a.pad_t, ix0 = 2 * ES_TW * tx - a.pad_l;
@@ -85,7 +89,7 @@ __global__ void __launch_bounds__(512, (CIN == 16 ? 2 : 1)) ers2_fused_kernel(co
       const int pl = p / ES_PPL, pb = p - pl * ES_PPL, c = pl >> 1, par = pl & 1;
       const int slot = pb * 64 + lane, hy = slot / ES_HC, hx = 2 * (slot - hy * ES_HC) + par;
       const int iy = iy0 + hy, ix = ix0 + hx;
-      const void* src = g_es2_zero;
+      const void* src = zpage;
       if (hy < ES_HR && hx <= 2 * ES_TW && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
         src = xi + ((size_t)iy * a.W + ix) * CIN + c * 8;
       dma16(src, buf + pl * ES_PLANE + pb * 1024);
@@ -200,6 +204,10 @@ __global__ void __launch_bounds__(512, 1) ers2_sp_kernel(const Es2Args a) {
   const int g = lane >> 4, r16 = lane & 15;
   const int tpi = a.tiles_x * a.tiles_y, ntiles = a.N * tpi;
 
+  // the zero page's address in SGPRs for the whole kernel: named directly in the DMA loops it was re-fetched from the
+  // GOT (s_getpc + s_load + s_waitcnt lgkmcnt(0), which also drains the wave's LDS reads) at every piece
+  const void* zpage = g_es2_zero;
+  asm volatile("" : "+s"(zpage));
   auto issue_halo = [&](int tile, char* buf) {
     const int n = tile / tpi, tr = tile - n * tpi, ty = tr / a.tiles_x, tx = tr - ty * a.tiles_x;
     const int iy0 = 2 * ES_TH * ty - a.pad_t, ix0 = 2 * ES_TW * tx - a.pad_l;
@@ -209,7 +217,7 @@ __global__ void __launch_bounds__(512, 1) ers2_sp_kernel(const Es2Args a) {
       const int pl = p / ES_PPL, pb = p - pl * ES_PPL, hl = pl / (2 * NCH), c = (pl >> 1) % NCH, par = pl & 1;
       const int slot = pb * 64 + lane, hy = slot / ES_HC, hx = 2 * (slot - hy * ES_HC) + par;
       const int iy = iy0 + hy, ix = ix0 + hx;
-      const void* src = g_es2_zero;
+      const void* src = zpage;
       if (hy < ES_HR && hx <= 2 * ES_TW && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
         src = xi + ((size_t)iy * a.W + ix) * CIN * 2 + hl * CIN + c * 8;
       dma16(src, buf + pl * ES_PLANE + pb * 1024);

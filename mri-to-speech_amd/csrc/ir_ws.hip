@@ -313,6 +313,10 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       dma16(src, lds_addr(dst + 256));
     }
   };
+  // the zero page's address in SGPRs for the whole kernel: named directly in the DMA loops it was re-fetched from the
+  // GOT (s_getpc + s_load + s_waitcnt lgkmcnt(0), which also drains the wave's LDS reads) at every piece
+  const void* zpage = g_ws_zero;
+  asm volatile("" : "+s"(zpage));
   auto issue_x = [&](int img, int band) {  // input rows of the band (+ halo rows), swizzled
     const int r0 = band * WS_BR, xr0 = max(r0 - 1, 0), xr1 = min(r0 + WS_BR + 1, H);
     const int ninstr = (xr1 - xr0) * W * CPR / 64;
@@ -322,7 +326,7 @@ __global__ void __launch_bounds__(64 * (WS_NP + WS_NC), 1)
       const int L = (p & ~15) | ((p & 15) ^ hx_of(r));
       const int plane = L / CPP, k8 = L - plane * CPP;
       const void* src = k8 * 8 < CS ? static_cast<const void*>(xi + (size_t)r * CS * 2 + plane * CS + k8 * 8)
-                                    : static_cast<const void*>(g_ws_zero);
+                                    : zpage;
       dma16(src, lds_addr(xs + j * 1024));
     }
   };
