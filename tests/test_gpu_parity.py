@@ -133,6 +133,24 @@ def test_bilstm_batch_over_32(ac_f32, ac_state):
     np.testing.assert_allclose(m.cpu().numpy(), acoustic.head(sd, ref_y).numpy(), atol=5e-5, rtol=0)
 
 
+@pytest.mark.parametrize("B,T", [(1, 30), (8, 4), (2, 32), (3, 40)])
+def test_bilstm_small_pass_projection(ac_f32, ac_state, B, T):
+    """Passes of <= 64 frames run the fp32 BiLSTM input projection with its K chunks split over the four waves of a
+    row tile (conv_igemm.hip kw, ConvArgs::kwave); larger passes keep one wave per row group.  Both against the
+    oracle at the fp32 bar, and the same clip inside a > 64-frame batch agrees with itself alone to fp32 rounding."""
+    sd = {k: torch.from_numpy(v) for k, v in ac_state[1].items()}
+    x = torch.from_numpy(np.random.default_rng(7 + B).normal(0, 0.5, (B, T, 208)).astype(np.float32))
+    ref_y = acoustic.bilstm_summerge(sd, x)
+    y, m = ac_f32.bilstm(x.to(DEV))
+    np.testing.assert_allclose(y.cpu().numpy(), ref_y.numpy(), atol=2e-5, rtol=0)
+    np.testing.assert_allclose(m.cpu().numpy(), acoustic.head(sd, ref_y).numpy(), atol=5e-5, rtol=0)
+    extra = max(4, 70 // T)
+    big = torch.cat([x, torch.from_numpy(np.random.default_rng(99).normal(0, 0.5, (extra, T, 208)).astype(np.float32))])
+    assert big.shape[0] * T > 64
+    yb, _ = ac_f32.bilstm(big.to(DEV))
+    np.testing.assert_allclose(yb[:B].cpu().numpy(), y.cpu().numpy(), atol=1e-5, rtol=0)
+
+
 # ------------------------------------------------------------------------------ CNN encoder
 def _rel(a, b):
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-6))
