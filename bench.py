@@ -327,7 +327,8 @@ def cpu_baseline(args, ac_sd, gen_sd, mean, std):
     """Oracle (torch-CPU fp32 restatement of the reference graph) on this host's cores, per BASELINE.md's CPU plan:
     C3 (one clip x args.frames end to end) repeated for ~cpu_seconds with per-stage wall time (CNN / BiLSTM / head +
     glue / Generator), C1 (mel only) from the same runs' CNN + BiLSTM + head stages, and C5 (ONE 1000-frame clip end to
-    end, the CNN in 100-frame chunks).  `value` is the C3 end-to-end rate (the headline's workload per clip)."""
+    end, the CNN in chunks of args.frames frames, C3's clip: in 100-frame chunks the oracle's CNN ran 3x slower per frame
+    on the box's 16-CPU share, 25 vs 8.3 ms).  `value` is the C3 end-to-end rate (the headline's workload per clip)."""
     sys.path.insert(0, REPO)
     from oracle import acoustic, effnet, hifigan
 
@@ -371,8 +372,8 @@ def cpu_baseline(args, ac_sd, gen_sd, mean, std):
         fl = torch.from_numpy(synth.synth_frames(1, TL, hw=(args.hw, args.hw), seed=78))
         st5 = {}
         with torch.no_grad():
-            e5 = clip(fl, TL, st5)
-        per["C5"] = {"what": f"1 clip x {TL} frames end to end (CNN in 100-frame chunks)", "frames_per_s": round(TL / e5, 3),
+            e5 = clip(fl, TL, st5, chunk=T)
+        per["C5"] = {"what": f"1 clip x {TL} frames end to end (CNN in {T}-frame chunks)", "frames_per_s": round(TL / e5, 3),
                      "rtf": round(e5 / (TL * HOP / SR), 4), "stage_ms": {k: round(1e3 * v, 1) for k, v in st5.items()}}
     return {"value": round(done * T / el, 3), "unit": "rtMRI frames/s", "cores": threads, "affinity_cpus": aff,
             "kind": "port",
